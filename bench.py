@@ -1,0 +1,223 @@
+"""Benchmark of the hot path: DeepFwFM Criteo-39 forward, batch 4096 per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one fused forward (libdfwfm.so, a single HIP launch) over one
+resident batch of 4096 synthetic Criteo-39 samples (BASELINE.json configs[1]).
+Every rank processes its own batch (data-parallel shards, no collective on
+the data path: "scaling": "weak").  Steps are replayed from a HIP graph
+capture of the forward; K steps are timed with HIP events on the stream the
+kernel runs on, bracketed by barrier + synchronize, max over ranks.
+
+Rank 0 prints one JSON line with the throughput, the roofline of the fused
+kernel (MFMA-bound: its MLP is 98.5 % of the arithmetic) and, at N = 1, the
+host-CPU baseline (oracle/torch_port.py, the reference's op sequence in fp32
+PyTorch-CPU) timed on this machine's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "CTR samples/sec (forward, batch 4096, Criteo-39) at 1/2/4/8 MI355X; AUC match"
+BATCH = 4096
+PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md, dense f32 MFMA (= f32 vector peak)
+PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md, HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--inputs", choices=["uniform", "zipf"], default="uniform")
+    return ap.parse_args()
+
+
+def algorithmic_counts(cfg):
+    """Per-sample algorithmic FLOPs and HBM bytes of the fused forward."""
+    F, D, N, H, num = 39, 10, 400, 3, 13
+    ncat = F - num
+    flops = 0
+    flops += 741 * D * 2                              # FwFM pairs
+    flops += 2 * (F * D * N + (H - 1) * N * N + N)     # MLP + fc
+    flops += F * D * 2 if cfg["use_fwlw"] else 0       # fwlw
+    bytes_ = ncat * 8 + num * 4 + ncat * D * 4 + 4     # Xi + Xv + gathered rows + logit
+    if not cfg["use_fwlw"]:
+        bytes_ += ncat * 4                             # first-order table rows
+    return flops, bytes_
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = synth.CRITEO_FEATURE_SIZES
+    fwlw = a.first_order == "fwlw"
+    cfg = dict(field_size=39, numerical=13, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0, use_deep=1,
+               use_lw=1, use_fwlw=int(fwlw), h_depth=3, deep_nodes=400)
+    model = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1,
+                    use_lw=1, use_fwlw=fwlw, numerical=13, use_cuda=True)
+    shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=1234)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    model = model.to(dev).eval()
+    model.strict_index_check = False
+
+    n_bufs = 4  # distinct resident batches, rotated, so gathers are not L2-hot repeats
+    batches = []
+    for i in range(n_bufs):
+        seed = 1000 * rank + i
+        if a.inputs == "zipf":
+            xi, xv = synth.zipf_inputs(sizes, 13, BATCH, seed=seed)
+        else:
+            xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=seed)
+        batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
+    out = torch.empty(BATCH, dtype=torch.float32, device=dev)
+
+    with torch.no_grad():
+        eng = model._sync_engine(dev)
+        stream = torch.cuda.Stream(dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(stream):
+            def step(i):
+                xi, xv = batches[i % n_bufs]
+                eng.forward(xi, xv, out)
+
+            graphs = None
+            if not a.no_graph:
+                graphs = []
+                for i in range(n_bufs):
+                    g = torch.cuda.CUDAGraph()
+                    step(i)  # ensure everything is initialised before capture
+                    with torch.cuda.graph(g, stream=stream):
+                        step(i)
+                    graphs.append(g)
+
+            def run(i):
+                if graphs is None:
+                    step(i)
+                else:
+                    graphs[i % n_bufs].replay()
+
+            for i in range(a.warmup):
+                run(i)
+            stream.synchronize()
+            if world > 1:
+                torch.distributed.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = torch.cuda.Event(enable_timing=True)
+            t1 = torch.cuda.Event(enable_timing=True)
+            wall0 = time.perf_counter()
+            t0.record(stream)
+            for i in range(a.steps):
+                run(i)
+            t1.record(stream)
+            stream.synchronize()
+            torch.cuda.synchronize(dev)
+            wall = time.perf_counter() - wall0
+            if world > 1:
+                torch.distributed.barrier()
+    ms = t0.elapsed_time(t1)
+    if world > 1:
+        t = torch.tensor([ms], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        ms = float(t.item())
+
+    ms_per_step = ms / a.steps
+    value = world * BATCH * a.steps / (ms / 1e3)
+    flops, bytes_ = algorithmic_counts(cfg)
+    t_launch = ms_per_step / 1e3
+    achieved_tf = flops * BATCH / t_launch / 1e12
+    achieved_gbs = bytes_ * BATCH / t_launch / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms_per_step, 6), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic Criteo-39 ({a.inputs} indices over the real field sizes, Xv integers 0..63; "
+                "deterministic hash-init weights with the reference's init_weights scales)",
+        "config": {"workload": f"DeepFwFM forward, Criteo-39, emb 10, MLP 3x400, FwFM + {a.first_order}; "
+                               f"batch {BATCH} per GPU",
+                   "global_batch": BATCH * world, "per_gpu_batch": BATCH,
+                   "parallelism": f"dp{world} (independent batch shards, no collective)",
+                   "launch": "eager" if a.no_graph else "hipGraph replay"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "traffic": traffic,
+                     "kernel": "dfwfm::fwd_kernel<10,7>", "flops_per_sample": flops, "units_per_launch": BATCH},
+        "roofline_hbm": {"achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "bytes_per_sample": bytes_},
+        "wall_s": round(wall, 4),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, params, sizes, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_baseline(cfg, params, sizes, seconds):
+    """oracle/torch_port.py (the reference's fp32 op sequence on PyTorch-CPU) on this host's cores."""
+    from oracle import torch_port
+    from xsdeepfwfm_deprecated_amd import synth
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    torch.set_num_threads(cores)
+    tp = {k: torch.from_numpy(v) for k, v in params.items()}
+    xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=99)
+    xi, xv = torch.from_numpy(xi), torch.from_numpy(xv)
+    torch_port.forward(cfg, tp, xi, xv)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        torch_port.forward(cfg, tp, xi, xv)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 2) or n >= 400:
+            break
+    cpu = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(n * BATCH / el, 1), "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"{n} batches x {BATCH} rows of the same Criteo-39 workload, {el:.1f} s, "
+                      f"torch {torch.__version__} CPU, {cores} threads, {cpu}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * dfwfm.h -- C ABI of the MI355X-native DeepFwFM forward engine (libdfwfm.so).
+ *
+ * This is the drop-in boundary for the one hot path of the reference
+ * (ShanningLiu/xsDeepFwFM_deprecated): `DeepFMs.forward(Xi, Xv) -> logits`
+ * (reference model/DeepFMs.py:285-469) together with the per-field embedding
+ * modules it calls (nn.Embedding / nn.EmbeddingBag, model/DeepFMs.py:201-210,
+ * 1066-1091, and QREmbeddingBag, model/QREmbeddingBag.py:156-174).
+ *
+ * Plain C: device pointers, sizes, an opaque model handle, and the HIP stream
+ * passed as `void*` (a hipStream_t; NULL = the default stream).  No torch
+ * types cross this boundary.  All pointers named "device" must be HIP device
+ * memory on the current device; nothing here synchronises the stream except
+ * dfwfm_read_error_flag().
+ *
+ * Error behaviour: every entry point returns a dfwfm_status (0 = ok, negative
+ * = error) and never aborts; dfwfm_last_error() gives a human-readable message
+ * for the calling thread.  Out-of-range embedding indices (the reference
+ * raises IndexError from nn.Embedding) cannot be reported synchronously by a
+ * kernel: the forward clamps the read to row 0 so it never faults, and sets a
+ * sticky device flag that dfwfm_read_error_flag() returns (and clears).
+ */
+#ifndef DFWFM_H
+#define DFWFM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFWFM_ABI_VERSION 1
+
+typedef enum {
+  DFWFM_OK = 0,
+  DFWFM_ERR_INVALID_ARG = -1,  /* null pointer, bad size, inconsistent config  */
+  DFWFM_ERR_UNSUPPORTED = -2,  /* a shape the compiled kernels do not cover     */
+  DFWFM_ERR_HIP = -3,          /* a HIP runtime call failed                    */
+  DFWFM_ERR_STATE = -4,        /* forward before tables / dense weights are set */
+} dfwfm_status;
+
+/* Error flag bits written by the forward kernel (dfwfm_read_error_flag). */
+#define DFWFM_FLAG_INDEX_OUT_OF_RANGE 1
+
+/* Model configuration -- mirrors the DeepFMs constructor switches
+ * (reference model/DeepFMs.py:81-89, utils/util.py:58-73).  Exactly one of
+ * use_fwfm / use_fm / use_logit may be set (reference :159-161). */
+typedef struct {
+  int32_t field_size;      /* F: fields (39 for Criteo)                         */
+  int32_t numerical;       /* leading numerical fields (13 for Criteo)          */
+  int32_t embedding_size;  /* D (10)                                            */
+  int32_t use_fwfm;        /* FwFM second order  sum_{k<l} r_kl <v_k, v_l>      */
+  int32_t use_fm;          /* FM second order (r_kl = 1)                        */
+  int32_t use_logit;       /* logistic regression: first order only            */
+  int32_t use_deep;        /* 3x400 ReLU MLP on the concatenated embeddings     */
+  int32_t use_lw;          /* first order projected by fm_1st.weight [1, F]     */
+  int32_t use_fwlw;        /* first order from fwfm_linear.weight [F, D]        */
+  int32_t h_depth;         /* hidden layers (3)                                 */
+  int32_t deep_nodes;      /* hidden width (400)                                */
+} dfwfm_config;
+
+/* Per-field embedding tables (device pointers into the caller's parameters).
+ *  - numerical field  (f < numerical): emb2 = v_f [1, D], emb1 = w1_f [1, 1]
+ *  - plain categorical: emb2 = [n, D], emb1 = [n, 1]
+ *  - QR categorical (qr_collisions > 0): emb2 = weight_q [ceil(n/c), D],
+ *    emb2_r = weight_r [c, D]; likewise emb1 / emb1_r for the first-order
+ *    QR bag (reference create_emb, model/DeepFMs.py:1066-1091).
+ * emb1 / emb1_r are NULL when the first order comes from fwlw or is unused. */
+typedef struct {
+  const float* emb2;
+  const float* emb2_r;
+  const float* emb1;
+  const float* emb1_r;
+  int64_t num_categories;  /* n: valid indices are [0, n)                     */
+  int64_t qr_collisions;   /* c; 0 = plain table                              */
+  int32_t qr_operation;    /* 0 = "mult", 1 = "add" ("concat" unsupported)    */
+  int32_t reserved;
+} dfwfm_field_tables;
+
+typedef struct dfwfm_model dfwfm_model;
+
+/* Allocates the model's device-side state (packed dense weights, field
+ * descriptors, error flag) on the current device. */
+int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out);
+void dfwfm_model_destroy(dfwfm_model* m);
+
+/* Uploads the F per-field table descriptors.  Call again whenever a table is
+ * re-allocated (e.g. after moving the module); in-place updates need no call. */
+int dfwfm_model_set_tables(dfwfm_model* m, const dfwfm_field_tables* tables,
+                           int32_t n_fields, void* stream);
+
+/* Packs the dense parameters into the kernel layout, on `stream` (no sync).
+ * Call again after any in-place update of these parameters.
+ *   field_cov  [F, F]    field_cov.weight (R; symmetrised as (R + R^T)/2)  or NULL
+ *   fwfm_lin   [F, D]    fwfm_linear.weight                                or NULL
+ *   fm_1st     [F]       fm_1st.weight                                     or NULL
+ *   bias       [1]       bias                                              or NULL
+ *   lin_w[h]   [N, K_h]  net_1_linear_{h+1}.weight, K_0 = F*D, K_h = N      (use_deep)
+ *   lin_b[h]   [N]       net_1_linear_{h+1}.bias                            (use_deep)
+ *   fc_w       [N]       net_1_fc.weight                                    (use_deep)
+ * lin_w / lin_b are host arrays of h_depth device pointers. */
+int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* fwfm_lin,
+                          const float* fm_1st, const float* bias,
+                          const float* const* lin_w, const float* const* lin_b,
+                          const float* fc_w, void* stream);
+
+/* The hot path: logits[b] for b in [0, batch).
+ *   xi  int64 [batch, F - numerical] (row stride xi_stride elements): categorical indices
+ *   xv  f32   [batch, >= numerical]  (row stride xv_stride elements): numerical values
+ *   out f32   [batch]  pre-sigmoid logits (reference forward return value)
+ * Replaces DeepFMs.forward, model/DeepFMs.py:285-469. */
+int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv,
+                  int64_t xv_stride, int64_t batch, float* out, void* stream);
+
+/* Synchronises `stream`, returns the sticky error-flag word and clears it. */
+int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream);
+
+/* Diagnostics. */
+const char* dfwfm_last_error(void);
+int dfwfm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFWFM_H */

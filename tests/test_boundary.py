@@ -1,0 +1,98 @@
+"""CPU: the C-ABI library loads and exports every symbol include/dfwfm.h declares; the DeepFMs
+mirror keeps the reference's state-dict contract; no compute without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, golden_names, load_golden, model_kwargs
+
+
+@pytest.fixture(scope="module")
+def built():
+    from xsdeepfwfm_deprecated_amd import _lib
+    _lib.build()
+    return _lib
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "dfwfm.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dfwfm_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_api():
+    assert header_functions() == sorted([
+        "dfwfm_abi_version", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy",
+        "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_read_error_flag"])
+
+
+def test_library_exports_every_header_symbol(built):
+    L = ctypes.CDLL(built.LIB_PATH)
+    for name in header_functions():
+        assert hasattr(L, name), name
+    assert set(built.SIGNATURES) == set(header_functions())
+
+
+def test_abi_version_and_error_string(built):
+    L = built.lib()
+    assert L.dfwfm_abi_version() == 1
+    assert isinstance(L.dfwfm_last_error(), bytes)
+    # invalid arguments are reported, never abort (no HIP call is reached)
+    assert L.dfwfm_model_create(None, None) == -1
+    assert b"null" in L.dfwfm_last_error()
+    assert L.dfwfm_forward(None, None, 0, None, 0, 0, None, None) == -1
+
+
+def test_struct_layouts_match_header(built):
+    assert ctypes.sizeof(built.dfwfm_config) == 11 * 4
+    assert ctypes.sizeof(built.dfwfm_field_tables) == 4 * 8 + 2 * 8 + 2 * 4
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_state_dict_contract_matches_reference(name):
+    """Parameter names and shapes equal the reference model's (recorded by gen_golden.py)."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs
+    cfg, params, *_ = load_golden(name)
+    m = DeepFMs(**model_kwargs(cfg))
+    sd = m.state_dict()
+    assert {k: list(v.shape) for k, v in sd.items()} == cfg["param_shapes"]
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    for k, v in m.state_dict().items():
+        assert np.array_equal(v.numpy(), params[k])
+
+
+def test_no_cpu_fallback():
+    from xsdeepfwfm_deprecated_amd import DeepFMs, DfwfmError
+    cfg, params, xi, xv, *_ = load_golden("deepfwfm_lw")
+    m = DeepFMs(**model_kwargs(cfg))
+    with pytest.raises(DfwfmError):
+        with torch.no_grad():
+            m(torch.from_numpy(xi), torch.from_numpy(xv))
+
+
+def test_init_weights_distributions():
+    from xsdeepfwfm_deprecated_amd import DeepFMs
+    cfg, *_ = load_golden("deepfwfm_fwlw_lw")
+    m = DeepFMs(**model_kwargs(cfg))
+    m.init_weights()
+    assert abs(m.fm_2nd_embeddings[20].weight.std().item() - 0.01) < 2e-3
+    assert abs(m.field_cov.weight.std().item() - np.sqrt(1 / 39)) < 0.03
+    assert abs(m.net_1_linear_2.weight.std().item() - np.sqrt(2 / 800)) < 0.005
+    assert abs(m.fm_1st.weight.std().item() - np.sqrt(2 / 450)) < 0.03
+    assert m.bias.item() == pytest.approx(0.01)
+
+
+def test_unsupported_variants_raise():
+    from xsdeepfwfm_deprecated_amd import DeepFMs
+    cfg, *_ = load_golden("deepfwfm_lw")
+    kw = model_kwargs(cfg)
+    with pytest.raises(NotImplementedError):
+        DeepFMs(**dict(kw, use_fwfm=0, use_ffm=1))
+    with pytest.raises(NotImplementedError):
+        DeepFMs(**kw, static_quantization=True)
+    with pytest.raises(SystemExit):
+        DeepFMs(**dict(kw, use_fm=1))  # fwfm and fm together

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU session: smoke, GPU parity tests, bench, rocprofv3 kernel-trace summary.
+# Each step has its own time limit; a crash/abort/timeout (rc >= 124) ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+step() {
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if [ "$rc" -ge 124 ]; then echo "fatal rc=$rc in $name: stopping"; exit "$rc"; fi
+  return 0
+}
+STEPS=${STEPS:-"smoke pytest bench prof"}
+for s in $STEPS; do
+  case $s in
+    smoke)  step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    bench)  step bench 400 python bench.py --steps 200 --warmup 20 ;;
+    bench_fwlw) step bench_fwlw 300 python bench.py --steps 200 --warmup 20 --first-order fwlw --no-cpu-baseline ;;
+    prof)   step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline ;;
+    pmc)    step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-graph &&
+            step pmc_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-graph ;;
+  esac
+done
+echo "== done"

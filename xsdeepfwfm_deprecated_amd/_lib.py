@@ -1,0 +1,117 @@
+"""ctypes binding of libdfwfm.so (the C ABI declared in include/dfwfm.h).
+
+The shared library is built in-tree with hipcc for gfx950 (``build()``) and
+loaded after ``torch`` so that it binds to the HIP runtime torch already
+loaded (both carry the SONAME ``libamdhip64.so.7``): torch's device memory and
+streams are then directly usable by the kernels.
+
+There is no CPU fallback: if the library cannot be loaded, every entry point
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import torch  # noqa: F401  -- must precede the library load (shared HIP runtime)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
+SOURCES = ["dfwfm_kernels.hip", "dfwfm_capi.hip"]
+HEADERS = ["dfwfm_internal.h", os.path.join("..", "..", "include", "dfwfm.h")]
+ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
+
+DFWFM_OK = 0
+STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported", -3: "HIP error", -4: "bad state"}
+FLAG_INDEX_OUT_OF_RANGE = 1
+
+
+class DfwfmError(RuntimeError):
+    pass
+
+
+class dfwfm_config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "field_size", "numerical", "embedding_size", "use_fwfm", "use_fm", "use_logit",
+        "use_deep", "use_lw", "use_fwlw", "h_depth", "deep_nodes")]
+
+
+class dfwfm_field_tables(ctypes.Structure):
+    _fields_ = [
+        ("emb2", ctypes.c_void_p), ("emb2_r", ctypes.c_void_p),
+        ("emb1", ctypes.c_void_p), ("emb1_r", ctypes.c_void_p),
+        ("num_categories", ctypes.c_int64), ("qr_collisions", ctypes.c_int64),
+        ("qr_operation", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/dfwfm.h declares
+_P = ctypes.c_void_p
+SIGNATURES = {
+    "dfwfm_model_create": (ctypes.c_int, [ctypes.POINTER(dfwfm_config), ctypes.POINTER(_P)]),
+    "dfwfm_model_destroy": (None, [_P]),
+    "dfwfm_model_set_tables": (ctypes.c_int, [_P, ctypes.POINTER(dfwfm_field_tables), ctypes.c_int32, _P]),
+    "dfwfm_model_set_dense": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P]),
+    "dfwfm_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
+    "dfwfm_read_error_flag": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
+    "dfwfm_last_error": (ctypes.c_char_p, []),
+    "dfwfm_abi_version": (ctypes.c_int, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile libdfwfm.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    if not force and not _stale():
+        return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def lib():
+    """The loaded library; raises DfwfmError if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise DfwfmError(f"{LIB_PATH} is missing: run xsdeepfwfm_deprecated_amd.build() "
+                             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.dfwfm_abi_version() != 1:
+            raise DfwfmError("libdfwfm ABI mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != DFWFM_OK:
+        msg = lib().dfwfm_last_error().decode(errors="replace")
+        raise DfwfmError(f"{what} failed ({STATUS.get(rc, rc)}): {msg}")

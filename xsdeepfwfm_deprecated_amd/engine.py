@@ -1,0 +1,123 @@
+"""Host-side driver of the HIP forward: owns a ``dfwfm_model`` handle and keeps
+it in sync with a DeepFMs module's parameters.
+
+* Embedding tables are passed to the kernel by pointer (no copy): a re-upload
+  of the 39 field descriptors happens only when a table is re-allocated
+  (``.cuda()``, ``load_state_dict`` into new storage, ...).
+* Dense parameters (R, fwlw, lw, bias, MLP) are re-packed into the kernel's
+  fragment layout on the current stream whenever any of them changes
+  (tracked with the tensors' in-place version counters), e.g. after every
+  optimizer step -- never per forward otherwise.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_f32_cuda(t, name, device):
+    if t.dtype != torch.float32 or not t.is_cuda or t.device != device:
+        raise RuntimeError(f"dfwfm: {name} must be a float32 tensor on {device}, got {t.dtype} on {t.device}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"dfwfm: {name} must be contiguous")
+
+
+class ForwardEngine:
+    """Binds one DeepFMs module to one device-resident dfwfm_model."""
+
+    def __init__(self, cfg: dict, device: torch.device):
+        self.device = device
+        self.cfg = dict(cfg)
+        c = _lib.dfwfm_config(**{k: int(v) for k, v in cfg.items()})
+        h = ctypes.c_void_p()
+        L = _lib.lib()
+        with torch.cuda.device(device):
+            _lib.check(L.dfwfm_model_create(ctypes.byref(c), ctypes.byref(h)), "dfwfm_model_create")
+        self.handle = h
+        self._tables_key = None
+        self._dense_key = None
+        self._keep = None  # host-side descriptor array kept alive
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            _lib.lib().dfwfm_model_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- parameter sync ----------------------------------------------------
+    def sync_tables(self, fields):
+        """fields: list of dicts(emb2, emb2_r, emb1, emb1_r, n, c, op) of tensors/ints."""
+        key = tuple((f["emb2"].data_ptr(), None if f["emb2_r"] is None else f["emb2_r"].data_ptr(),
+                     None if f["emb1"] is None else f["emb1"].data_ptr(),
+                     None if f["emb1_r"] is None else f["emb1_r"].data_ptr()) for f in fields)
+        if key == self._tables_key:
+            return
+        arr = (_lib.dfwfm_field_tables * len(fields))()
+        for i, f in enumerate(fields):
+            for nm in ("emb2", "emb2_r", "emb1", "emb1_r"):
+                if f[nm] is not None:
+                    _require_f32_cuda(f[nm], f"field {i} {nm}", self.device)
+            arr[i] = _lib.dfwfm_field_tables(
+                f["emb2"].data_ptr(),
+                None if f["emb2_r"] is None else f["emb2_r"].data_ptr(),
+                None if f["emb1"] is None else f["emb1"].data_ptr(),
+                None if f["emb1_r"] is None else f["emb1_r"].data_ptr(),
+                int(f["n"]), int(f["c"]), int(f["op"]), 0)
+        _lib.check(_lib.lib().dfwfm_model_set_tables(self.handle, arr, len(fields),
+                                                     _stream_handle(self.device)), "dfwfm_model_set_tables")
+        self._keep = arr
+        self._tables_key = key
+
+    def sync_dense(self, field_cov, fwfm_lin, fm_1st, bias, lin_w, lin_b, fc_w):
+        tensors = [field_cov, fwfm_lin, fm_1st, bias, fc_w] + list(lin_w) + list(lin_b)
+        key = tuple(None if t is None else (t.data_ptr(), t._version) for t in tensors)
+        if key == self._dense_key:
+            return
+        for i, t in enumerate(tensors):
+            if t is not None:
+                _require_f32_cuda(t, f"dense parameter {i}", self.device)
+        H = len(lin_w)
+        W = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_w])
+        B = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_b])
+        _lib.check(_lib.lib().dfwfm_model_set_dense(
+            self.handle, _ptr(field_cov), _ptr(fwfm_lin), _ptr(fm_1st), _ptr(bias),
+            W if H else None, B if H else None, _ptr(fc_w), _stream_handle(self.device)),
+            "dfwfm_model_set_dense")
+        self._dense_key = key
+
+    # -- hot path ----------------------------------------------------------
+    def forward(self, xi: torch.Tensor, xv: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        B = xi.shape[0]
+        ncat = self.cfg["field_size"] - self.cfg["numerical"]
+        num = self.cfg["numerical"]
+        if out is None:
+            out = torch.empty(B, dtype=torch.float32, device=self.device)
+        xs = xi.stride(0) if ncat > 0 else 0
+        vs = xv.stride(0) if num > 0 else 0
+        rc = _lib.lib().dfwfm_forward(self.handle, ctypes.c_void_p(xi.data_ptr()), xs,
+                                      ctypes.c_void_p(xv.data_ptr()), vs, B,
+                                      ctypes.c_void_p(out.data_ptr()), _stream_handle(self.device))
+        _lib.check(rc, "dfwfm_forward")
+        return out
+
+    def read_error_flag(self) -> int:
+        v = ctypes.c_int32(0)
+        _lib.check(_lib.lib().dfwfm_read_error_flag(self.handle, ctypes.byref(v), _stream_handle(self.device)),
+                   "dfwfm_read_error_flag")
+        return int(v.value)
