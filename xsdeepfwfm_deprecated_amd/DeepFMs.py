@@ -187,20 +187,24 @@ class DeepFMs(nn.Module):
     # -------------------------------------------------------------- HIP sync
     @staticmethod
     def _field_desc(mod_2nd, mod_1st):
+        """Descriptor of one field's tables; either family may be absent (fwlw: no 1st-order
+        tables; logistic regression: no 2nd-order tables).  Both families share QR-ness."""
         def parts(mod):
             if mod is None:
-                return None, None, 0, 0
+                return None, None
             if isinstance(mod, QREmbeddingBag):
                 if mod.operation not in ("mult", "add"):
                     raise NotImplementedError("QR 'concat' changes the field width; unsupported")
-                return mod.weight_q, mod.weight_r, mod.num_collisions, 0 if mod.operation == "mult" else 1
-            return mod.weight, None, 0, 0
-        e2, e2r, c, op = parts(mod_2nd)
-        e1, e1r, _, _ = parts(mod_1st)
-        n = mod_2nd.num_categories if isinstance(mod_2nd, QREmbeddingBag) else mod_2nd.weight.shape[0]
-        return dict(emb2=e2.detach(), emb2_r=None if e2r is None else e2r.detach(),
-                    emb1=None if e1 is None else e1.detach(), emb1_r=None if e1r is None else e1r.detach(),
-                    n=n, c=c, op=op)
+                return mod.weight_q.detach(), mod.weight_r.detach()
+            return mod.weight.detach(), None
+        ref = mod_2nd if mod_2nd is not None else mod_1st
+        if isinstance(ref, QREmbeddingBag):
+            n, c, op = ref.num_categories, ref.num_collisions, 0 if ref.operation == "mult" else 1
+        else:
+            n, c, op = ref.weight.shape[0], 0, 0
+        e2, e2r = parts(mod_2nd)
+        e1, e1r = parts(mod_1st)
+        return dict(emb2=e2, emb2_r=e2r, emb1=e1, emb1_r=e1r, n=n, c=c, op=op)
 
     def _sync_engine(self, device):
         if device.type != "cuda":
@@ -212,9 +216,9 @@ class DeepFMs(nn.Module):
             self._engine = ForwardEngine(self.engine_config(), device)
         eng = self._engine
         first = getattr(self, "fm_1st_embeddings", None)
-        fields = []
-        for f in range(self.field_size):
-            fields.append(self._field_desc(self.fm_2nd_embeddings[f], None if first is None else first[f]))
+        second = getattr(self, "fm_2nd_embeddings", None)
+        fields = [self._field_desc(None if second is None else second[f], None if first is None else first[f])
+                  for f in range(self.field_size)]
         eng.sync_tables(fields)
 
         def w(name, attr="weight"):

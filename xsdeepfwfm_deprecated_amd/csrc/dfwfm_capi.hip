@@ -3,6 +3,7 @@
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -15,13 +16,12 @@ struct dfwfm_model {
   dfwfm_config cfg;
   int device;
   int F, D, num, H, N;
-  int NT, NC0, SX, SY, TPW;
+  int NT, NC0, SX, SY, TPW, MT, S, W0, KS;
   int flags;
   size_t lds_bytes;
   // device state (owned)
   FieldDev* d_fields;
-  Pair* d_pairs;
-  int32_t* d_npairs;
+  float* d_upack;  // FwFM A-operand fragments [MT][S][64]
   int32_t* d_err;
   float4* d_wpack;
   size_t wpack_elems;
@@ -69,7 +69,7 @@ int dev_alloc(T** p, size_t count) {
 
 void free_model(dfwfm_model* m) {
   if (!m) return;
-  void* ptrs[] = {m->d_fields, m->d_pairs, m->d_npairs, m->d_err, m->d_wpack,
+  void* ptrs[] = {m->d_fields, m->d_upack, m->d_err, m->d_wpack,
                   m->d_mlp_b,  m->d_fc,    m->d_fwlw,   m->d_lw,  m->d_bias};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -133,23 +133,30 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   m->NT = NT;
   m->TPW = TPW;
   m->NC0 = (F * D + 15) / 16;
-  const int kx = m->NC0 * 16 > NT * 16 ? m->NC0 * 16 : NT * 16;
-  m->SX = kx + 4;
+  m->MT = (F + 15) / 16;
+  m->S = (F + 3) / 4;
+  // E-tile columns read by the MLP (NC0*16) and by the FwFM contraction (4*S fields)
+  m->W0 = m->NC0 * 16 > 4 * m->S * D ? m->NC0 * 16 : 4 * m->S * D;
+  const int kx = m->W0 > NT * 16 ? m->W0 : NT * 16;
+  m->SX = r4(kx) + 4;
   m->SY = c.use_deep ? NT * 16 + 4 : 0;
+  // one wave per SIMD; DFWFM_KSPLIT=2 runs two per SIMD splitting K (measured slower, kept for A/B)
+  m->KS = 1;
+  if (const char* ks = getenv("DFWFM_KSPLIT")) m->KS = atoi(ks) == 2 ? 2 : 1;
   const bool second = c.use_fwfm || c.use_fm;
   m->flags = (second ? kHasSecond : 0) | (c.use_deep ? kHasDeep : 0) |
-             (c.use_fwlw ? kFoFwlw : kFoTables) | ((second && c.use_lw) ? kFoLw : 0);
-  m->lds_bytes = sizeof(float) * ((size_t)kBM * m->SX + (size_t)kBM * m->SY + (size_t)kBM * F +
-                                  (size_t)kBM * D + 4 * kBM + kBM);
+             (c.use_fwlw ? kFoFwlw : kFoTables) | ((second && c.use_lw) ? kFoLw : 0) |
+             ((second || c.use_deep) ? kNeedE : 0);
+  const LdsLayout L = lds_layout(F, D, m->MT, m->S, m->SX, m->SY, TPW > 0 ? TPW : 1, m->KS, c.use_deep != 0);
+  m->lds_bytes = sizeof(float) * (size_t)L.total;
   if (m->lds_bytes > 160 * 1024) {
     free_model(m);
     return fail(DFWFM_ERR_UNSUPPORTED, "LDS tile of %zu bytes exceeds 160 KiB", m->lds_bytes);
   }
 
   int rc = DFWFM_OK;
-  const int max_pairs = F * (F - 1) / 2;
-  if ((rc = dev_alloc(&m->d_fields, F)) || (rc = dev_alloc(&m->d_pairs, max_pairs)) ||
-      (rc = dev_alloc(&m->d_npairs, 1)) || (rc = dev_alloc(&m->d_err, 1)) ||
+  if ((rc = dev_alloc(&m->d_fields, F)) || (rc = dev_alloc(&m->d_upack, (size_t)m->MT * m->S * 64)) ||
+      (rc = dev_alloc(&m->d_err, 1)) ||
       (rc = dev_alloc(&m->d_fwlw, (size_t)F * D)) || (rc = dev_alloc(&m->d_lw, F)) ||
       (rc = dev_alloc(&m->d_bias, 1))) {
     free_model(m);
@@ -157,6 +164,10 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   }
   if (c.use_deep) {
     m->wpack_elems = (size_t)NT * m->NC0 * 64 + (size_t)(H - 1) * NT * NT * 64;
+    if (m->wpack_elems * sizeof(float4) >= (size_t)1 << 31) {
+      free_model(m);
+      return fail(DFWFM_ERR_UNSUPPORTED, "packed MLP weights exceed the 2 GiB buffer-descriptor range");
+    }
     if ((rc = dev_alloc(&m->d_wpack, m->wpack_elems)) ||
         (rc = dev_alloc(&m->d_mlp_b, (size_t)H * NT * 16)) || (rc = dev_alloc(&m->d_fc, (size_t)NT * 16))) {
       free_model(m);
@@ -164,7 +175,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     }
   }
   e = hipMemset(m->d_err, 0, sizeof(int32_t));
-  if (e == hipSuccess) e = hipMemset(m->d_npairs, 0, sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemset(m->d_upack, 0, sizeof(float) * (size_t)m->MT * m->S * 64);
   if (e != hipSuccess) {
     free_model(m);
     return hip_fail(e, "hipMemset");
@@ -179,15 +190,16 @@ int dfwfm_model_set_tables(dfwfm_model* m, const dfwfm_field_tables* t, int32_t 
   if (!m || !t) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
   if (n != m->F) return fail(DFWFM_ERR_INVALID_ARG, "%d tables for %d fields", n, m->F);
   const bool need_fo = (m->flags & kFoTables) != 0;
+  const bool need_e = (m->flags & kNeedE) != 0;
   for (int f = 0; f < n; ++f) {
     const dfwfm_field_tables& x = t[f];
-    if (!x.emb2) return fail(DFWFM_ERR_INVALID_ARG, "field %d: emb2 is null", f);
+    if (need_e && !x.emb2) return fail(DFWFM_ERR_INVALID_ARG, "field %d: emb2 is null", f);
     if (need_fo && !x.emb1) return fail(DFWFM_ERR_INVALID_ARG, "field %d: emb1 is null", f);
     if (x.num_categories < 1) return fail(DFWFM_ERR_INVALID_ARG, "field %d: num_categories < 1", f);
     if (x.qr_collisions < 0) return fail(DFWFM_ERR_INVALID_ARG, "field %d: qr_collisions < 0", f);
     if (x.qr_collisions > 0) {
       if (f < m->num) return fail(DFWFM_ERR_INVALID_ARG, "field %d: numerical field cannot be QR", f);
-      if (!x.emb2_r || (need_fo && !x.emb1_r))
+      if ((need_e && !x.emb2_r) || (need_fo && !x.emb1_r))
         return fail(DFWFM_ERR_INVALID_ARG, "field %d: QR remainder table is null", f);
       if (x.qr_operation != 0 && x.qr_operation != 1)
         return fail(DFWFM_ERR_UNSUPPORTED, "field %d: QR operation %d (only mult=0, add=1)", f,
@@ -220,8 +232,8 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
   if ((m->flags & kFoLw) && !fm_1st) return fail(DFWFM_ERR_INVALID_ARG, "use_lw needs fm_1st");
   if (!bias) return fail(DFWFM_ERR_INVALID_ARG, "bias is required");
   if (c.use_fwfm || c.use_fm) {
-    hipError_t e = launch_build_pairs(field_cov, m->F, c.use_fm ? 1 : 0, m->d_pairs, m->d_npairs, s);
-    if (e != hipSuccess) return hip_fail(e, "build_pairs");
+    hipError_t e = launch_pack_fwfm(field_cov, m->F, c.use_fm ? 1 : 0, m->MT, m->S, m->d_upack, s);
+    if (e != hipSuccess) return hip_fail(e, "pack_fwfm");
   }
   hipError_t e = hipSuccess;
   if (m->flags & kFoFwlw) e = launch_pad_copy(fwfm_lin, m->F * m->D, m->F * m->D, m->d_fwlw, s);
@@ -271,12 +283,12 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   a.batch = batch;
   a.out = out;
   a.err = m->d_err;
-  a.pairs = m->d_pairs;
-  a.npairs = m->d_npairs;
+  a.upack = m->d_upack;
   a.fwlw = m->d_fwlw;
   a.lw = m->d_lw;
   a.bias = m->d_bias;
   a.wpack = m->d_wpack;
+  a.wpack_bytes = (int32_t)(m->wpack_elems * sizeof(float4));
   a.mlp_b = m->d_mlp_b;
   a.fc = m->d_fc;
   a.F = m->F;
@@ -285,10 +297,15 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   a.N = m->N;
   a.NT = m->NT;
   a.NC0 = m->NC0;
+  a.MT = m->MT;
+  a.S = m->S;
+  a.W0 = m->W0;
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
-  hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, m->lds_bytes, (hipStream_t)stream);
+  // diagnostics only (phase timing): DFWFM_DIAG_DROP_FLAGS clears flag bits, results become invalid
+  if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
+  hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, m->KS, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
 }

@@ -1,26 +1,30 @@
 // dfwfm_kernels.hip -- CDNA4 (gfx950) kernels for the DeepFwFM forward.
 //
 // One fused launch computes the whole forward of reference
-// model/DeepFMs.py:285-469 for a tile of BM = 16 samples:
+// model/DeepFMs.py:285-469 for a tile of kBM = 16 samples:
 //
+//   phase 0  stage the 39 field descriptors, lw, fwlw and the FwFM operand
+//            fragments in LDS; issue the tile's Xi / Xv loads;
 //   phase G  gather: 26 categorical rows (plain nn.Embedding / EmbeddingBag,
-//            or QR quotient x remainder, model/QREmbeddingBag.py:156-174) and
-//            13 numerical rows v_f[0] * Xv (model/DeepFMs.py:297-299,334) into
-//            an LDS tile E[16][F*D] -- this IS deep_emb (field-major `cat`,
-//            model/DeepFMs.py:398) and the `stack` of :337;
-//   phase S  shallow part from LDS: first order (per-field tables :304, or
-//            fwlw :338-347) projected by lw (:445-450) or summed, and the
-//            FwFM second order sum_{k<l} r_kl <E_k, E_l> (:352-367) over a
-//            compact list of non-zero symmetric pairs (pruned R => fewer pairs);
+//            or QR quotient (*|+) remainder, model/QREmbeddingBag.py:156-174)
+//            and 13 numerical rows v_f[0] * Xv (model/DeepFMs.py:297-299,334)
+//            into an LDS tile E[16][F*D] -- this IS deep_emb (the field-major
+//            `cat` of :398) and the `stack` of :337; all of a thread's row
+//            loads are issued before any is consumed;
+//   phase S  first order (per-field tables :304, or fwlw :338-347) projected
+//            by lw (:445-450) or summed; FwFM second order (:352-367) on f32
+//            MFMA as  second[b] = sum_{k,d} E[b,k,d] * (U E_b)[k,d]  with U the
+//            strictly upper triangle of (R + R^T)/2 -- no [39,39,B,10]
+//            intermediates, and R's zero blocks skipped;
 //   phase M  the h_depth x N ReLU MLP (:412-428) on f32 MFMA
 //            (v_mfma_f32_16x16x4_f32, exact f32 fma chain): activations stay
 //            in LDS, weights stream from L2 in a pre-packed fragment order
-//            (one 1 KiB dwordx4 load per wave per 16-deep K chunk per tile),
-//            bias+ReLU fused into the epilogue, net_1_fc fused into the last
-//            layer's epilogue;
+//            (one 1 KiB dwordx4 load per wave per 16-deep K chunk per output
+//            tile), next chunk's loads pinned ahead of the current chunk's
+//            MFMAs; with KS = 2 two waves per SIMD split K (even / odd chunks)
+//            and reduce through LDS; bias+ReLU fused into the epilogue,
+//            net_1_fc fused into the last layer's epilogue;
 //   combine  total = ((first + second) + deep) + bias   (:458 order).
-//
-// Nothing of the reference's [39,39,B,10] outer-product intermediates exists.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,239 +36,380 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float relu_keep_nan(float v) { return v < 0.f ? 0.f : v; }
 
-// ---------------------------------------------------------------------------
-// phase G helpers
-// ---------------------------------------------------------------------------
 template <int D>
-__device__ __forceinline__ void copy_row(float* __restrict__ dst, const float* __restrict__ src) {
+__device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict__ src) {
   if constexpr (D % 4 == 0) {
 #pragma unroll
-    for (int d = 0; d < D; d += 4) *reinterpret_cast<float4*>(dst + d) = *reinterpret_cast<const float4*>(src + d);
+    for (int d = 0; d < D; d += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(src + d);
+      v[d] = x.x; v[d + 1] = x.y; v[d + 2] = x.z; v[d + 3] = x.w;
+    }
   } else if constexpr (D % 2 == 0) {
 #pragma unroll
-    for (int d = 0; d < D; d += 2) *reinterpret_cast<float2*>(dst + d) = *reinterpret_cast<const float2*>(src + d);
+    for (int d = 0; d < D; d += 2) {
+      const float2 x = *reinterpret_cast<const float2*>(src + d);
+      v[d] = x.x; v[d + 1] = x.y;
+    }
   } else {
 #pragma unroll
-    for (int d = 0; d < D; ++d) dst[d] = src[d];
+    for (int d = 0; d < D; ++d) v[d] = src[d];
   }
 }
 
 template <int D>
-__device__ __forceinline__ void combine_rows(float* __restrict__ dst, const float* __restrict__ q,
-                                             const float* __restrict__ r, int op) {
-  float a[D], b[D];
-  if constexpr (D % 2 == 0) {
+__device__ __forceinline__ void store_row(float* dst, const float (&v)[D]) {
+  if constexpr (D % 4 == 0) {
 #pragma unroll
-    for (int d = 0; d < D; d += 2) {
-      float2 x = *reinterpret_cast<const float2*>(q + d);
-      float2 y = *reinterpret_cast<const float2*>(r + d);
-      a[d] = x.x; a[d + 1] = x.y; b[d] = y.x; b[d + 1] = y.y;
-    }
+    for (int d = 0; d < D; d += 4) *reinterpret_cast<float4*>(dst + d) = make_float4(v[d], v[d + 1], v[d + 2], v[d + 3]);
+  } else if constexpr (D % 2 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 2) *reinterpret_cast<float2*>(dst + d) = make_float2(v[d], v[d + 1]);
   } else {
 #pragma unroll
-    for (int d = 0; d < D; ++d) { a[d] = q[d]; b[d] = r[d]; }
+    for (int d = 0; d < D; ++d) dst[d] = v[d];
   }
-  // QREmbeddingBag: embed_q * embed_r ('mult') or embed_q + embed_r ('add')
-#pragma unroll
-  for (int d = 0; d < D; ++d) dst[d] = (op == 0) ? a[d] * b[d] : a[d] + b[d];
+}
+
+// row combine modes: 0 = a * scale (numerical / plain, scale 1), 1 = a * b (QR mult), 2 = a + b (QR add)
+__device__ __forceinline__ float combine(int mode, float a, float b, float scale) {
+  return mode == 1 ? a * b : (mode == 2 ? a + b : a * scale);
 }
 
 // ---------------------------------------------------------------------------
-// phase M: one MLP layer for the workgroup's 16 rows.
-//   act   : LDS [16][SA] input activations (K padded with zeros to NC*16)
-//   wl    : packed weights of this layer, [NT][NC][64 lanes] float4
-//   wave w owns output tiles w, w+4, ... (TPW of them; tiles past NT are
-//   clamped duplicates whose results are discarded -- they ride on a SIMD
-//   that would otherwise idle at the layer barrier).
+// phase M: one MLP layer for the workgroup's 16 rows, one wave's share.
+//   act : LDS [16][SA] input activations (K zero-padded to NC*16)
+//   wl  : packed weights of this layer, [NT][NC][64 lanes] float4
+//   the wave group g (0..3) owns output tiles g, g+4, ... (TPW of them; tiles
+//   past NT are clamped duplicates whose results are discarded); it walks K
+//   chunks c0, c0+KS, ...
 // Fragment algebra (16x16x4 f32): in sub-step s of chunk c lane l supplies
-//   A = act[l&15][16c + 4(l>>4) + s],  B = W[n0 + (l&15)][16c + 4(l>>4) + s],
-// so one ds_read_b128 (A) and one dwordx4 per tile (B) feed 4 MFMAs.
+//   A = act[l&15][16c + 4(l>>4) + s],  B = W[n0 + (l&15)][16c + 4(l>>4) + s].
 // ---------------------------------------------------------------------------
 template <int TPW>
-__device__ __forceinline__ void mlp_layer(const float* __restrict__ act, int SA, int NC,
-                                          const float4* __restrict__ wl, int NT, int N,
-                                          const float* __restrict__ bias, float* __restrict__ out_act,
-                                          int SO, const float* __restrict__ fc, float (&dpart)[4],
-                                          bool last, int wave, int lane) {
-  const float4* wp[TPW];
+__device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[TPW], const float4& a, const f32x4 (&b)[TPW]) {
+  // sub-step-major: consecutive MFMAs hit different accumulators (16x16x4 f32 has a 40-cycle
+  // dependent latency against a 32-cycle issue interval)
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    int t = wave + 4 * j;
-    t = t < NT ? t : NT - 1;
-    wp[j] = wl + (size_t)t * NC * 64 + lane;
-  }
-  f32x4 acc[TPW];
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[j].x, acc[j], 0, 0, 0);
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[j].y, acc[j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[j].z, acc[j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[j].w, acc[j], 0, 0, 0);
+}
 
-  const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
-
-  // two chunks of weight fragments in flight ahead of the MFMAs
-  float4 b0[TPW], b1[TPW];
-  const int c1 = NC > 1 ? 1 : 0;
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) b0[j] = wp[j][0];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) b1[j] = wp[j][(size_t)c1 * 64];
-
-  for (int c = 0; c < NC; ++c) {
-    const float4 a = *reinterpret_cast<const float4*>(arow + 16 * c);
-    int cn = c + 2;
-    cn = cn < NC ? cn : NC - 1;  // clamped: the tail re-loads a resident chunk, never branches
-    float4 b2[TPW];
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) b2[j] = wp[j][(size_t)cn * 64];
+// One layer's weight stream for one wave: output tiles g, g+4, ... (clamped to NT-1) and K chunks
+// c0, c0+KS, ... of the packed [NT][NC][64] float4 layout.  Loads are buffer loads: the per-tile
+// base and the chunk offset are scalar (SALU), the only vector operand is lane*16 -- flat loads
+// spent a 64-bit VALU add per load in front of the MFMAs.
+template <int TPW, int KS>
+struct LayerStream {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int sbase[TPW];  // byte offset of each owned tile's [NC][64] block (wave-uniform)
+  int n, c0;
+  __device__ __forceinline__ void init(__amdgpu_buffer_rsrc_t r, int layer_off, int NC, int NT, int g, int c0_) {
+    rsrc = r;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b0[j].x, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b0[j].y, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b0[j].z, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b0[j].w, acc[j], 0, 0, 0);
+      int t = g + 4 * j;
+      t = t < NT ? t : NT - 1;
+      sbase[j] = __builtin_amdgcn_readfirstlane((layer_off + t * NC * 64) * 16);
     }
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) { b0[j] = b1[j]; b1[j] = b2[j]; }
+    c0 = c0_;
+    n = c0 < NC ? (NC - c0 + KS - 1) / KS : 0;
   }
+  __device__ __forceinline__ int chunk(int i) const { return c0 + KS * (i < n ? i : n - 1); }
+  __device__ __forceinline__ void load(f32x4 (&b)[TPW], int c, int voff) const {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+      b[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, sbase[j] + c * 1024, 0));
+  }
+  // the first two chunks, issued ahead of time (before the previous phase's epilogue / barrier)
+  __device__ __forceinline__ void preload(f32x4 (&b0)[TPW], f32x4 (&b1)[TPW], int voff) const {
+    if (n == 0) return;
+    load(b0, chunk(0), voff);
+    load(b1, chunk(1), voff);
+  }
+};
 
-  // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r
-  const int row0 = (lane >> 4) * 4;
+// K loop of one layer, entered with chunks 0 and 1 already in b0 / b1.  Weight fragments rotate
+// through three register sets, each refilled two chunks ahead of its MFMAs (the loop is unrolled
+// by 3 so no set is ever copied: a copy makes hipcc wait for the load it copies); the activation
+// fragment is read one chunk ahead.  Within a step the refill loads are interleaved with the first
+// MFMAs (sched_group_barrier: 2 MFMA, 1 load, ...), and a sched_barrier closes the step so hipcc
+// cannot sink them to their use.
+template <int TPW, int KS>
+__device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __restrict__ act, int SA,
+                                           const LayerStream<TPW, KS>& ls, f32x4 (&b0)[TPW],
+                                           f32x4 (&b1)[TPW], f32x4 (&b2)[TPW], int lane) {
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    const int t = wave + 4 * j;
-    if (t < NT) {
-      const int n = t * 16 + (lane & 15);
-      const bool valid = n < N;
-      const float bn = valid ? bias[n] : 0.f;
-      if (!last) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = valid ? relu_keep_nan(acc[j][r] + bn) : 0.f;
-          out_act[(row0 + r) * SO + n] = v;
-        }
-      } else {
-        const float w = valid ? fc[n] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = valid ? relu_keep_nan(acc[j][r] + bn) : 0.f;
-          dpart[r] = fmaf(v, w, dpart[r]);
-        }
-      }
-    }
+  for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int n = ls.n;
+  if (n == 0) return;
+  const int voff = lane * 16;
+  const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
+  float4 a = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(0));
+#define DFWFM_STEP(X, Z, i)                                                             \
+  {                                                                                     \
+    const float4 an = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk((i) + 1));  \
+    ls.load(Z, ls.chunk((i) + 2), voff);                                                \
+    mfma_chunk<TPW>(acc, a, X);                                                         \
+    for (int q = 0; q < TPW; ++q) {                                                     \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                \
+    }                                                                                   \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TPW, 0);                            \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    a = an;                                                                             \
   }
+  int i = 0;
+  for (; i + 3 <= n; i += 3) {
+    DFWFM_STEP(b0, b2, i);
+    DFWFM_STEP(b1, b0, i + 1);
+    DFWFM_STEP(b2, b1, i + 2);
+  }
+  if (i < n) DFWFM_STEP(b0, b2, i);
+  if (i + 1 < n) DFWFM_STEP(b1, b0, i + 1);
+#undef DFWFM_STEP
 }
 
 // ---------------------------------------------------------------------------
 // the fused forward kernel
 // ---------------------------------------------------------------------------
-template <int D, int TPW>
-__global__ void __launch_bounds__(kWG) fwd_kernel(FwdArgs p) {
+template <int D, int TPW, int KS>
+__global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
+  constexpr int NTH = 256 * KS;
+  constexpr int NW = 4 * KS;
+  constexpr int RPT = (kBM * 64 + NTH - 1) / NTH;  // gather rows per thread (F <= 64)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (SGPR)
   const int F = p.F;
   const int num = p.num;
   const int SX = p.SX;
   const int SY = p.SY;
-  const bool deep = (p.flags & kHasDeep) != 0;
-
-  float* bufX = smem;                                   // [BM][SX]  E tile / even-layer input
-  float* bufY = bufX + kBM * SX;                        // [BM][SY]  odd-layer input (deep only)
-  float* fo = bufY + (deep ? kBM * SY : 0);             // [BM][F]   first order per field
-  float* part2 = fo + kBM * F;                          // [BM][D]   second order per dim
-  float* dsum = part2 + kBM * D;                        // [4][BM]   deep partial per wave
-  float* fs = dsum + 4 * kBM;                           // [BM]      first + second
+  const int flags = p.flags;
+  const bool deep = (flags & kHasDeep) != 0;
+  const int Fp = r4(F);
+  const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep);
+  FieldDev* desc = reinterpret_cast<FieldDev*>(smem + L.desc);
+  float* lw_s = smem + L.lw;
+  float* fwlw_s = smem + L.fwlw;
+  float* upk = smem + L.upk;
+  float* bufX = smem + L.bufX;
+  float* bufY = smem + L.bufY;
+  f32x4* red = reinterpret_cast<f32x4*>(smem + L.red);
+  float* fo = smem + L.fo;
+  float* part2 = smem + L.part2;
+  float* dsum = smem + L.dsum;
+  float* fs = smem + L.fs;
 
   const int64_t b0 = (int64_t)blockIdx.x * kBM;
-  const int ncat = F - num;
-  const int kpad0 = p.NC0 * 16;
-  const bool fo_tables = (p.flags & kFoTables) != 0;
+  const int g = wave & 3;   // MLP output-tile group
+  const int kh = wave >> 2; // MLP K half (KS == 2)
 
-  // ---- phase G: gather E (and table first order) into LDS -----------------
-  for (int r = tid; r < kBM * F; r += kWG) {
-    const int b = r / F;
-    const int f = r - b * F;
-    const int64_t gb = b0 + b;
-    float* dst = bufX + b * SX + f * D;
-    float fo_v = 0.f;
-    if (gb >= p.batch) {
+  // layer-0 weights: the first two chunks are in flight during the gather and the shallow part
+  LayerStream<TPW, KS> ls;
+  f32x4 wb0[TPW], wb1[TPW], wb2[TPW];
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float4*>(p.wpack), (short)0, p.wpack_bytes, 0x00020000);
+  if (deep) {
+    ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
+    ls.preload(wb0, wb1, lane * 16);
+  }
+
+  // ---- phase 0: stage parameters, issue this thread's Xi / Xv loads ---------
+  for (int i = tid; i < 7 * F; i += NTH)
+    reinterpret_cast<uint2*>(desc)[i] = reinterpret_cast<const uint2*>(p.fields)[i];
+  if (flags & kFoLw)
+    for (int i = tid; i < F; i += NTH) lw_s[i] = p.lw[i];
+  if (flags & kFoFwlw)
+    for (int i = tid; i < F * D; i += NTH) fwlw_s[i] = p.fwlw[i];
+  if (flags & kHasSecond)
+    for (int i = tid; i < p.MT * p.S * 16; i += NTH)
+      reinterpret_cast<float4*>(upk)[i] = reinterpret_cast<const float4*>(p.upack)[i];
+
+  // gather row r -> field f = r / 16, sample b = r % 16 (a wave spans 4 fields)
+  int64_t key[RPT];  // categorical index, or the bits of the numerical value
 #pragma unroll
-      for (int d = 0; d < D; ++d) dst[d] = 0.f;
-    } else {
-      const FieldDev fd = p.fields[f];
-      if (f < num) {
-        const float x = p.xv[gb * p.xv_stride + f];
+  for (int k = 0; k < RPT; ++k) {
+    const int r = tid + k * NTH;
+    const int f = r >> 4;
+    const int64_t gb = b0 + (r & 15);
+    key[k] = 0;
+    if (f < F && gb < p.batch) {
+      if (f < num)
+        key[k] = __float_as_int(p.xv[gb * p.xv_stride + f]);
+      else
+        key[k] = p.xi[gb * p.xi_stride + (f - num)];
+    }
+  }
+  __syncthreads();
+
+  // ---- phase G: gather E rows and table first order --------------------------
+  {
+    const bool needE = (flags & kNeedE) != 0;
+    const bool fo_tab = (flags & kFoTables) != 0;
+    const float* pa[RPT];
+    const float* pb[RPT];
+    const float* qa[RPT];
+    const float* qb[RPT];
+    float scale[RPT];
+    int mode[RPT];
+    bool live[RPT];
 #pragma unroll
-        for (int d = 0; d < D; ++d) dst[d] = fd.emb2[d] * x;
-        if (fo_tables) fo_v = fd.emb1[0] * x;
-      } else {
-        int64_t idx = p.xi[gb * p.xi_stride + (f - num)];
-        if (idx < 0 || idx >= fd.n) {
-          atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
-          idx = 0;
-        }
-        if (fd.c == 0) {
-          copy_row<D>(dst, fd.emb2 + idx * D);
-          if (fo_tables) fo_v = fd.emb1[idx];
+    for (int k = 0; k < RPT; ++k) {
+      const int r = tid + k * NTH;
+      const int f = r >> 4;
+      live[k] = f < F && (b0 + (r & 15)) < p.batch;
+      pa[k] = pb[k] = qa[k] = qb[k] = nullptr;
+      scale[k] = 1.f;
+      mode[k] = 0;
+      if (live[k]) {
+        const FieldDev fd = desc[f];
+        if (f < num) {
+          scale[k] = __int_as_float((int)key[k]);
+          pa[k] = pb[k] = fd.emb2;
+          qa[k] = qb[k] = fd.emb1;
         } else {
-          const int64_t q = idx / fd.c;
-          const int64_t rr = idx - q * fd.c;
-          combine_rows<D>(dst, fd.emb2 + q * D, fd.emb2_r + rr * D, fd.op);
-          if (fo_tables) {
-            const float x = fd.emb1[q], y = fd.emb1_r[rr];
-            fo_v = (fd.op == 0) ? x * y : x + y;
+          int64_t idx = key[k];
+          if (idx < 0 || idx >= fd.n) {
+            atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
+            idx = 0;
+          }
+          if (fd.c == 0) {
+            pa[k] = pb[k] = fd.emb2 + idx * D;
+            if (fo_tab) qa[k] = qb[k] = fd.emb1 + idx;
+          } else {
+            const int64_t q = idx / fd.c;
+            const int64_t rr = idx - q * fd.c;
+            mode[k] = fd.op == 0 ? 1 : 2;
+            pa[k] = fd.emb2 + q * D;
+            pb[k] = fd.emb2_r + rr * D;
+            if (fo_tab) {
+              qa[k] = fd.emb1 + q;
+              qb[k] = fd.emb1_r + rr;
+            }
           }
         }
       }
     }
-    fo[b * F + f] = fo_v;
-  }
-  // zero the K padding of the E tile (layer-0 reads NC0*16 columns)
-  for (int r = tid; r < kBM * (kpad0 - F * D); r += kWG) {
-    const int w = kpad0 - F * D;
-    const int b = r / w;
-    bufX[b * SX + F * D + (r - b * w)] = 0.f;
+    // all loads first ...
+    float va[RPT][D], vb[RPT][D], fa[RPT], fb[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      fa[k] = fb[k] = 0.f;
+      if (live[k] && needE) {
+        load_row<D>(va[k], pa[k]);
+        load_row<D>(vb[k], pb[k]);
+      }
+      if (live[k] && fo_tab) {
+        fa[k] = *qa[k];
+        fb[k] = *qb[k];
+      }
+    }
+    // ... then combine and store
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = tid + k * NTH;
+      const int f = r >> 4;
+      const int b = r & 15;
+      if (f < F) {
+        if (needE) {
+          float e[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(mode[k], va[k][d], vb[k][d], scale[k]) : 0.f;
+          store_row<D>(bufX + b * SX + f * D, e);
+        }
+        fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], fb[k], scale[k]) : 0.f;
+      }
+    }
+    // zero the E-tile padding read by the MLP (NC0*16 columns) and the FwFM (S*4 fields)
+    const int w = p.W0 - F * D;
+    for (int i = tid; i < kBM * w; i += NTH) {
+      const int b = i / w;
+      bufX[b * SX + F * D + (i - b * w)] = 0.f;
+    }
   }
   __syncthreads();
 
   // ---- phase S: shallow part ----------------------------------------------
-  if (p.flags & kFoFwlw) {
+  if (flags & kFoFwlw) {
     // fm_first_order[b, f] = sum_d E[b, f, d] * Wfl[f, d]  (einsum 'ijk,ik->ijk' then 'ijk->ji')
-    for (int r = tid; r < kBM * F; r += kWG) {
-      const int b = r / F;
-      const int f = r - b * F;
+    for (int r = tid; r < kBM * F; r += NTH) {
+      const int f = r >> 4;
+      const int b = r & 15;
       const float* e = bufX + b * SX + f * D;
-      const float* w = p.fwlw + f * D;
+      const float* w = fwlw_s + f * D;
       float s = 0.f;
 #pragma unroll
       for (int d = 0; d < D; ++d) s += e[d] * w[d];
-      fo[r] = s;
+      fo[b * Fp + f] = s;
     }
   }
-  if (p.flags & kHasSecond) {
-    // second[b, d] = sum over pairs k<l with r_kl != 0 of (E_k[d] * E_l[d]) * r_kl
-    const int np = *p.npairs;
-    for (int r = tid; r < kBM * D; r += kWG) {
-      const int b = r / D;
-      const int d = r - b * D;
-      const float* e = bufX + b * SX + d;
-      float acc = 0.f;
-      for (int q = 0; q < np; ++q) {
-        const Pair pr = p.pairs[q];
-        acc = fmaf(e[pr.k * D] * e[pr.l * D], pr.r, acc);
+  if (flags & kHasSecond) {
+    // Y = U * E_b on MFMA: rows k (fields, MT tiles), columns n = b*D + d (D tiles of 16),
+    // contraction over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].
+    const int MT = p.MT, S = p.S;
+    constexpr int NTW = (D + NW - 1) / NW;  // column tiles per wave
+    const float* ecol[NTW];
+    float v[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      int nt = wave + NW * j;
+      nt = nt < D ? nt : D - 1;  // clamped duplicate, discarded below
+      const int n = nt * 16 + (lane & 15);
+      const int b = n / D;
+      ecol[j] = bufX + b * SX + (n - b * D);  // E[b][l][d] = ecol[l * D]
+      v[j] = 0.f;
+    }
+    // one row tile at a time keeps the accumulators in fixed registers (guarded MFMAs make hipcc
+    // shuttle every accumulator between AGPRs and VGPRs); U's rows 16m.. vanish for l <= 16m
+    for (int m = 0; m < MT; ++m) {
+      f32x4 acc[NTW];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = (16 * m + 1) >> 2; s < S; ++s) {
+        const int l = 4 * s + (lane >> 4);
+        const float av = upk[(m * S + s) * 64 + lane];
+        float bv[NTW];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) bv[j] = ecol[j][l * D];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
       }
-      part2[r] = acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * m + 4 * (lane >> 4) + r;
+        const int kk = k < F ? k : 0;
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const float e = ecol[j][kk * D];
+          v[j] = fmaf(k < F ? e : 0.f, acc[j][r], v[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      float x = v[j];
+      x += __shfl_xor(x, 16);
+      x += __shfl_xor(x, 32);
+      const int nt = wave + NW * j;
+      if (lane < 16 && nt < D) part2[nt * 16 + lane] = x;
     }
   }
   __syncthreads();
   if (tid < kBM) {
     float first = 0.f;
-    if (p.flags & kFoLw) {
-      for (int f = 0; f < F; ++f) first = fmaf(fo[tid * F + f], p.lw[f], first);
+    if (flags & kFoLw) {
+      for (int f = 0; f < F; ++f) first = fmaf(fo[tid * Fp + f], lw_s[f], first);
     } else {
-      for (int f = 0; f < F; ++f) first += fo[tid * F + f];
+      for (int f = 0; f < F; ++f) first += fo[tid * Fp + f];
     }
     float second = 0.f;
-    if (p.flags & kHasSecond) {
+    if (flags & kHasSecond) {
 #pragma unroll
       for (int d = 0; d < D; ++d) second += part2[tid * D + d];
     }
@@ -273,51 +418,99 @@ __global__ void __launch_bounds__(kWG) fwd_kernel(FwdArgs p) {
 
   if (!deep) {
     __syncthreads();
-    if (tid < kBM && b0 + tid < p.batch) {
-      float t = fs[tid];
-      if (p.bias) t += p.bias[0];
-      p.out[b0 + tid] = t;
-    }
+    if (tid < kBM && b0 + tid < p.batch) p.out[b0 + tid] = fs[tid] + p.bias[0];
     return;
   }
 
   // ---- phase M: MLP on MFMA -------------------------------------------------
+  const int row0 = (lane >> 4) * 4;
   float dpart[4] = {0.f, 0.f, 0.f, 0.f};
-  const float4* wl = p.wpack;
+  int layer_off = 0;  // float4 offset of layer h in wpack
   for (int h = 0; h < p.H; ++h) {
     const bool even = (h & 1) == 0;
     const float* in = even ? bufX : bufY;
     const int SA = even ? SX : SY;
-    float* out = even ? bufY : bufX;
+    float* outa = even ? bufY : bufX;
     const int SO = even ? SY : SX;
     const int NC = h == 0 ? p.NC0 : p.NT;
     const bool last = h == p.H - 1;
-    mlp_layer<TPW>(in, SA, NC, wl, p.NT, p.N, p.mlp_b + (size_t)h * p.NT * 16, out, SO, p.fc, dpart,
-                   last, wave, lane);
-    wl += (size_t)p.NT * NC * 64;
+    const float* bias = p.mlp_b + (size_t)h * p.NT * 16;
+
+    // epilogue operands, fetched before the K loop so they arrive under it
+    float bn[TPW], wf[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      int t = g + 4 * j;
+      t = t < p.NT ? t : p.NT - 1;
+      const int n = t * 16 + (lane & 15);
+      bn[j] = bias[n];
+      wf[j] = last ? p.fc[n] : 0.f;
+    }
+
+    f32x4 acc[TPW];
+    mlp_k_loop<TPW, KS>(acc, in, SA, ls, wb0, wb1, wb2, lane);
+    // next layer's first chunks go out now, ahead of this layer's epilogue and barrier
+    layer_off += p.NT * NC * 64;
+    if (!last) {
+      ls.init(wrsrc, layer_off, p.NT, p.NT, g, kh);
+      ls.preload(wb0, wb1, lane * 16);
+    }
+    if constexpr (KS == 2) {
+      if (kh == 1) {
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) red[(g * TPW + j) * 64 + lane] = acc[j];
+      }
+      __syncthreads();
+      if (kh == 0) {
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) acc[j] += red[(g * TPW + j) * 64 + lane];
+      }
+    }
+    if (kh == 0) {
+      // C/D layout: col = lane&15 (neuron), row = (lane>>4)*4 + r (sample)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int t = g + 4 * j;
+        if (t < p.NT) {
+          const int n = t * 16 + (lane & 15);
+          const bool valid = n < p.N;  // padded neurons stay exactly 0 (bias/fc pads are 0)
+          if (!last) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              outa[(row0 + r) * SO + n] = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
+              dpart[r] = fmaf(v, wf[j], dpart[r]);
+            }
+          }
+        }
+      }
+    }
     __syncthreads();
   }
 
-  // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the 16 lanes sharing (lane>>4), then the 4 waves
+  // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the 16 lanes sharing (lane>>4), then the 4 groups
+  if (kh == 0) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float v = dpart[r];
-    v += __shfl_xor(v, 8);
-    v += __shfl_xor(v, 4);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 1);
-    dpart[r] = v;
-  }
-  if ((lane & 15) == 0) {
+    for (int r = 0; r < 4; ++r) {
+      float v = dpart[r];
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 1);
+      dpart[r] = v;
+    }
+    if ((lane & 15) == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dsum[wave * kBM + (lane >> 4) * 4 + r] = dpart[r];
+      for (int r = 0; r < 4; ++r) dsum[g * kBM + row0 + r] = dpart[r];
+    }
   }
   __syncthreads();
   if (tid < kBM && b0 + tid < p.batch) {
     const float deepv = ((dsum[tid] + dsum[kBM + tid]) + dsum[2 * kBM + tid]) + dsum[3 * kBM + tid];
-    float t = fs[tid] + deepv;
-    if (p.bias) t += p.bias[0];
-    p.out[b0 + tid] = t;
+    p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
 }
 
@@ -353,99 +546,70 @@ __global__ void pad_copy_kernel(const float* __restrict__ src, int n, int npad, 
     dst[i] = (src && i < n) ? src[i] : 0.f;
 }
 
-// Compact list of the non-zero upper-triangle entries of R_sym = (R^T + R) * 0.5
-// (model/DeepFMs.py:363-364), in (k, l) order.  mode 1 = FM (all ones).
-// One workgroup of 1024 threads; ballot + LDS prefix keeps the order stable.
-__global__ void __launch_bounds__(1024) build_pairs_kernel(const float* __restrict__ R, int F, int mode,
-                                                           Pair* __restrict__ pairs,
-                                                           int32_t* __restrict__ npairs) {
-  __shared__ int wave_cnt[16];
-  __shared__ int base_s;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  if (tid == 0) base_s = 0;
-  __syncthreads();
-  const int total = F * F;
-  for (int start = 0; start < total; start += 1024) {
-    const int i = start + tid;
-    int k = 0, l = 0;
-    float r = 0.f;
-    bool keep = false;
-    if (i < total) {
-      k = i / F;
-      l = i - k * F;
-      if (l > k) {
-        r = (mode == 1) ? 1.f : (R[l * F + k] + R[k * F + l]) * 0.5f;
-        keep = r != 0.f;
-      }
-    }
-    const unsigned long long m = __ballot(keep);
-    const int before = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) wave_cnt[wave] = __popcll(m);
-    __syncthreads();
-    int off = base_s;
-    for (int w = 0; w < wave; ++w) off += wave_cnt[w];
-    if (keep) {
-      Pair pr;
-      pr.k = (int16_t)k;
-      pr.l = (int16_t)l;
-      pr.r = r;
-      pairs[off + before] = pr;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int s = 0;
-      for (int w = 0; w < 16; ++w) s += wave_cnt[w];
-      base_s += s;
-    }
-    __syncthreads();
+// FwFM A operand: U[k][l] = (R[l][k] + R[k][l]) * 0.5 for l > k (model/DeepFMs.py:363-364; the
+// diagonal is removed by :366-367), 0 elsewhere; mode 1 = FM (U = 1 above the diagonal).
+// Fragment order out[(m*S + s)*64 + lane] = U[16m + (lane&15)][4s + (lane>>4)].
+__global__ void pack_fwfm_kernel(const float* __restrict__ R, int F, int mode, int MT, int S,
+                                 float* __restrict__ out) {
+  const int total = MT * S * 64;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int lane = i & 63;
+    const int ms = i >> 6;
+    const int s = ms % S;
+    const int m = ms / S;
+    const int k = 16 * m + (lane & 15);
+    const int l = 4 * s + (lane >> 4);
+    float u = 0.f;
+    if (k < F && l < F && l > k) u = (mode == 1) ? 1.f : (R[l * F + k] + R[k * F + l]) * 0.5f;
+    out[i] = u;
   }
-  if (tid == 0) *npairs = base_s;
 }
 
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <int D, int TPW>
+template <int D, int TPW, int KS>
 static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, hipStream_t s) {
-  auto k = fwd_kernel<D, TPW>;
+  auto k = fwd_kernel<D, TPW, KS>;
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kWG), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256 * KS), lds, s, a);
   return hipGetLastError();
 }
 
-template <int D>
-static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, size_t lds, hipStream_t s) {
+template <int D, int KS>
+static hipError_t launch_fwd_k(const FwdArgs& a, int tpw, size_t lds, hipStream_t s) {
   switch (tpw) {
-    case 1: return launch_fwd_t<D, 1>(a, lds, s);
-    case 2: return launch_fwd_t<D, 2>(a, lds, s);
-    case 3: return launch_fwd_t<D, 3>(a, lds, s);
-    case 4: return launch_fwd_t<D, 4>(a, lds, s);
-    case 5: return launch_fwd_t<D, 5>(a, lds, s);
-    case 6: return launch_fwd_t<D, 6>(a, lds, s);
-    case 7: return launch_fwd_t<D, 7>(a, lds, s);
-    case 8: return launch_fwd_t<D, 8>(a, lds, s);
+    case 1: return launch_fwd_t<D, 1, KS>(a, lds, s);
+    case 2: return launch_fwd_t<D, 2, KS>(a, lds, s);
+    case 3: return launch_fwd_t<D, 3, KS>(a, lds, s);
+    case 4: return launch_fwd_t<D, 4, KS>(a, lds, s);
+    case 5: return launch_fwd_t<D, 5, KS>(a, lds, s);
+    case 6: return launch_fwd_t<D, 6, KS>(a, lds, s);
+    case 7: return launch_fwd_t<D, 7, KS>(a, lds, s);
+    case 8: return launch_fwd_t<D, 8, KS>(a, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-bool supported_embedding_size(int D) {
-  return D == 4 || D == 8 || D == 10 || D == 16 || D == 32;
+template <int D>
+static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, size_t lds, hipStream_t s) {
+  return ks == 2 ? launch_fwd_k<D, 2>(a, tpw, lds, s) : launch_fwd_k<D, 1>(a, tpw, lds, s);
 }
 
-hipError_t launch_forward(const FwdArgs& a, int D, int tpw, size_t lds, hipStream_t s) {
+bool supported_embedding_size(int D) { return D == 4 || D == 8 || D == 10 || D == 16 || D == 32; }
+
+hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, hipStream_t s) {
   switch (D) {
-    case 4: return launch_fwd_d<4>(a, tpw, lds, s);
-    case 8: return launch_fwd_d<8>(a, tpw, lds, s);
-    case 10: return launch_fwd_d<10>(a, tpw, lds, s);
-    case 16: return launch_fwd_d<16>(a, tpw, lds, s);
-    case 32: return launch_fwd_d<32>(a, tpw, lds, s);
+    case 4: return launch_fwd_d<4>(a, tpw, ks, lds, s);
+    case 8: return launch_fwd_d<8>(a, tpw, ks, lds, s);
+    case 10: return launch_fwd_d<10>(a, tpw, ks, lds, s);
+    case 16: return launch_fwd_d<16>(a, tpw, ks, lds, s);
+    case 32: return launch_fwd_d<32>(a, tpw, ks, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -464,8 +628,9 @@ hipError_t launch_pad_copy(const float* src, int n, int npad, float* dst, hipStr
   return hipGetLastError();
 }
 
-hipError_t launch_build_pairs(const float* R, int F, int mode, Pair* pairs, int32_t* npairs, hipStream_t s) {
-  hipLaunchKernelGGL(build_pairs_kernel, dim3(1), dim3(1024), 0, s, R, F, mode, pairs, npairs);
+hipError_t launch_pack_fwfm(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s) {
+  const int total = MT * S * 64;
+  hipLaunchKernelGGL(pack_fwfm_kernel, dim3((total + 255) / 256), dim3(256), 0, s, R, F, mode, MT, S, out);
   return hipGetLastError();
 }
 

@@ -63,9 +63,8 @@ class ForwardEngine:
     # -- parameter sync ----------------------------------------------------
     def sync_tables(self, fields):
         """fields: list of dicts(emb2, emb2_r, emb1, emb1_r, n, c, op) of tensors/ints."""
-        key = tuple((f["emb2"].data_ptr(), None if f["emb2_r"] is None else f["emb2_r"].data_ptr(),
-                     None if f["emb1"] is None else f["emb1"].data_ptr(),
-                     None if f["emb1_r"] is None else f["emb1_r"].data_ptr()) for f in fields)
+        names = ("emb2", "emb2_r", "emb1", "emb1_r")
+        key = tuple(tuple(None if f[nm] is None else f[nm].data_ptr() for nm in names) for f in fields)
         if key == self._tables_key:
             return
         arr = (_lib.dfwfm_field_tables * len(fields))()
@@ -74,10 +73,7 @@ class ForwardEngine:
                 if f[nm] is not None:
                     _require_f32_cuda(f[nm], f"field {i} {nm}", self.device)
             arr[i] = _lib.dfwfm_field_tables(
-                f["emb2"].data_ptr(),
-                None if f["emb2_r"] is None else f["emb2_r"].data_ptr(),
-                None if f["emb1"] is None else f["emb1"].data_ptr(),
-                None if f["emb1_r"] is None else f["emb1_r"].data_ptr(),
+                *[None if f[nm] is None else f[nm].data_ptr() for nm in names],
                 int(f["n"]), int(f["c"]), int(f["op"]), 0)
         _lib.check(_lib.lib().dfwfm_model_set_tables(self.handle, arr, len(fields),
                                                      _stream_handle(self.device)), "dfwfm_model_set_tables")
