@@ -117,6 +117,10 @@ int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream);
 
 /* Diagnostics. */
 const char* dfwfm_last_error(void);
+/* With DFWFM_DIAG_STAMPS=1 in the environment, each forward records 16 shader-clock stamps per
+ * 16-sample workgroup at its phase boundaries; copies up to n of them (synchronising `stream`)
+ * and returns the number of workgroups copied, or a negative status. */
+int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream);
 int dfwfm_abi_version(void);
 
 #ifdef __cplusplus

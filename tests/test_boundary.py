@@ -26,7 +26,8 @@ def header_functions():
 
 def test_header_declares_expected_api():
     assert header_functions() == sorted([
-        "dfwfm_abi_version", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy",
+        "dfwfm_abi_version", "dfwfm_diag_stamps", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create",
+        "dfwfm_model_destroy",
         "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_read_error_flag"])
 
 

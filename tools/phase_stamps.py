@@ -1,0 +1,53 @@
+"""Per-phase cycle breakdown of the fused forward from in-kernel s_memtime stamps (diagnostic).
+
+    DFWFM_DIAG_STAMPS=1 python tools/phase_stamps.py [--batch 4096] [--iters 20]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("DFWFM_DIAG_STAMPS", "1")
+
+from xsdeepfwfm_deprecated_amd import DeepFMs, _lib, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=4096)
+ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--fwlw", action="store_true")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+sizes = synth.CRITEO_FEATURE_SIZES
+m = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1,
+            use_fwlw=a.fwlw, numerical=13, use_cuda=True)
+shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+m.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_state(shapes, 39, 10, 400, True, True).items()})
+m = m.to(dev).eval()
+m.strict_index_check = False
+xi, xv = synth.synth_inputs(sizes, 13, a.batch, seed=5)
+xi, xv = torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)
+with torch.no_grad():
+    for _ in range(a.iters):
+        m(xi, xv)
+torch.cuda.synchronize()
+grid = (a.batch + 15) // 16
+buf = (ctypes.c_uint64 * (grid * 16))()
+n = _lib.lib().dfwfm_diag_stamps(m._engine.handle, buf, grid * 16,
+                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+st = np.frombuffer(buf, dtype=np.uint64).reshape(grid, 16)[:n].astype(np.int64)
+names = ["stage (params, Xi/Xv)", "gather E + table first order", "shallow (fwlw, FwFM MFMA, sums)",
+         "  . fwlw first order", "  . FwFM MFMA (wave 0)", "  . barrier wait", "  . first/second sums",
+         "MLP layer 1", "MLP layer 2", "MLP layer 3", "deep reduce + combine"]
+slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (3, 4), (4, 5), (5, 6), (6, 8)]
+tot = st[:, 8] - st[:, 0]
+print(f"workgroups {n}; total cycles median {np.median(tot):.0f} (p10 {np.percentile(tot, 10):.0f}, "
+      f"p90 {np.percentile(tot, 90):.0f})")
+for nm, sl in zip(names, slots):
+    if sl is None:
+        continue
+    d = st[:, sl[1]] - st[:, sl[0]]
+    print(f"  {nm:34s} median {np.median(d):8.0f} cycles  ({100 * np.median(d) / np.median(tot):5.1f} %)")

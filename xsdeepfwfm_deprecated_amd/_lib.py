@@ -59,6 +59,7 @@ SIGNATURES = {
     "dfwfm_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
     "dfwfm_read_error_flag": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
     "dfwfm_last_error": (ctypes.c_char_p, []),
+    "dfwfm_diag_stamps": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64, _P]),
     "dfwfm_abi_version": (ctypes.c_int, []),
 }
 

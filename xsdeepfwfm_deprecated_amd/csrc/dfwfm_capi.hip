@@ -30,6 +30,8 @@ struct dfwfm_model {
   float* d_fwlw;   // [F*D]
   float* d_lw;     // [F]
   float* d_bias;   // [1]
+  uint64_t* d_stamps;  // diagnostics (DFWFM_DIAG_STAMPS)
+  size_t stamps_cap;   // workgroups the stamp buffer holds
   bool tables_set;
   bool dense_set;
 };
@@ -69,8 +71,8 @@ int dev_alloc(T** p, size_t count) {
 
 void free_model(dfwfm_model* m) {
   if (!m) return;
-  void* ptrs[] = {m->d_fields, m->d_upack, m->d_err, m->d_wpack,
-                  m->d_mlp_b,  m->d_fc,    m->d_fwlw,   m->d_lw,  m->d_bias};
+  void* ptrs[] = {m->d_fields, m->d_upack, m->d_err, m->d_wpack, m->d_mlp_b,
+                  m->d_fc,     m->d_fwlw,  m->d_lw,  m->d_bias,  m->d_stamps};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -305,9 +307,32 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   a.flags = m->flags;
   // diagnostics only (phase timing): DFWFM_DIAG_DROP_FLAGS clears flag bits, results become invalid
   if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
+  // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
+  a.stamps = nullptr;
+  if (getenv("DFWFM_DIAG_STAMPS")) {
+    const size_t grid = (size_t)((batch + kBM - 1) / kBM);
+    if (grid > m->stamps_cap) {
+      if (m->d_stamps) (void)hipFree(m->d_stamps);
+      m->d_stamps = nullptr;
+      m->stamps_cap = 0;
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_stamps), grid * kStampSlots * sizeof(uint64_t)));
+      m->stamps_cap = grid;
+    }
+    a.stamps = m->d_stamps;
+  }
   hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, m->KS, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
+}
+
+int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream) {
+  if (!m || !host || n < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (!m->d_stamps) return fail(DFWFM_ERR_STATE, "no stamps recorded (set DFWFM_DIAG_STAMPS=1)");
+  const size_t cap = m->stamps_cap * kStampSlots;
+  const size_t cnt = (size_t)n < cap ? (size_t)n : cap;
+  HIP_TRY(hipMemcpyAsync(host, m->d_stamps, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return (int)(cnt / kStampSlots);
 }
 
 int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream) {

@@ -10,6 +10,7 @@ namespace dfwfm {
 constexpr int kBM = 16;     // samples per workgroup = one 16-row MFMA tile
 constexpr int kMaxTPW = 8;  // MLP output tiles per wave group => deep_nodes <= 4*8*16 = 512
 constexpr int kMaxMT = 4;   // FwFM row tiles => field_size <= 64
+constexpr int kStampSlots = 16;  // diagnostic phase stamps per workgroup
 
 // flags
 constexpr int kHasSecond = 1;  // FwFM / FM second order
@@ -57,6 +58,7 @@ struct FwdArgs {
   int32_t SX, SY;      // LDS row strides (floats) of the two activation tiles
   int32_t W0;          // E-tile columns that must be valid (zero padded past F*D)
   int32_t flags;
+  uint64_t* stamps;    // diagnostics only: [grid][kStampSlots] shader-clock stamps, normally null
 };
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.

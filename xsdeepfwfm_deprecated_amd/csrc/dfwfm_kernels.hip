@@ -36,6 +36,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float relu_keep_nan(float v) { return v < 0.f ? 0.f : v; }
 
+// Diagnostic phase stamps (p.stamps != nullptr only in DFWFM_DIAG_STAMPS runs; in production the
+// branch is never taken): wave 0 lane 0 records the shader clock at phase boundaries.
+__device__ __forceinline__ void stamp(uint64_t* st, int slot, int tid) {
+  if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
+}
+
 template <int D>
 __device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict__ src) {
   if constexpr (D % 4 == 0) {
@@ -207,32 +213,29 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   float* fs = smem + L.fs;
 
   const int64_t b0 = (int64_t)blockIdx.x * kBM;
+  stamp(p.stamps, 0, tid);
   const int g = wave & 3;   // MLP output-tile group
   const int kh = wave >> 2; // MLP K half (KS == 2)
 
-  // layer-0 weights: the first two chunks are in flight during the gather and the shallow part
   LayerStream<TPW, KS> ls;
   f32x4 wb0[TPW], wb1[TPW], wb2[TPW];
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float4*>(p.wpack), (short)0, p.wpack_bytes, 0x00020000);
-  if (deep) {
-    ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
-    ls.preload(wb0, wb1, lane * 16);
+
+  // ---- phase 0: field descriptors -> LDS; this thread's Xi / Xv; shallow parameters in flight --
+  // Every load is issued before any is consumed (a load-then-store loop waits one round trip per
+  // iteration).  Only the descriptors and the tile's Xi / Xv gate the gather; the FwFM fragments,
+  // lw and fwlw are stored to LDS after the gather's loads are out.
+  constexpr int kDescPT = (7 * 64 + NTH - 1) / NTH;    // uint2 words of descriptors per thread
+  constexpr int kUpkPT = (kMaxMT * 16 * 16 + NTH - 1) / NTH;  // float4 of FwFM fragments per thread
+  constexpr int kFwlwPT = (64 * 32 + NTH - 1) / NTH;   // fwlw floats per thread
+  uint2 dw[kDescPT];
+#pragma unroll
+  for (int k = 0; k < kDescPT; ++k) {
+    const int i = tid + k * NTH;
+    if (i < 7 * F) dw[k] = reinterpret_cast<const uint2*>(p.fields)[i];
   }
-
-  // ---- phase 0: stage parameters, issue this thread's Xi / Xv loads ---------
-  for (int i = tid; i < 7 * F; i += NTH)
-    reinterpret_cast<uint2*>(desc)[i] = reinterpret_cast<const uint2*>(p.fields)[i];
-  if (flags & kFoLw)
-    for (int i = tid; i < F; i += NTH) lw_s[i] = p.lw[i];
-  if (flags & kFoFwlw)
-    for (int i = tid; i < F * D; i += NTH) fwlw_s[i] = p.fwlw[i];
-  if (flags & kHasSecond)
-    for (int i = tid; i < p.MT * p.S * 16; i += NTH)
-      reinterpret_cast<float4*>(upk)[i] = reinterpret_cast<const float4*>(p.upack)[i];
-
-  // gather row r -> field f = r / 16, sample b = r % 16 (a wave spans 4 fields)
-  int64_t key[RPT];  // categorical index, or the bits of the numerical value
+  int64_t key[RPT];  // gather row r -> field f = r / 16, sample b = r % 16: index or Xv bits
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int r = tid + k * NTH;
@@ -246,7 +249,28 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
         key[k] = p.xi[gb * p.xi_stride + (f - num)];
     }
   }
+  float4 uw[kUpkPT];
+  const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
+#pragma unroll
+  for (int k = 0; k < kUpkPT; ++k) {
+    const int i = tid + k * NTH;
+    if (i < n_upk) uw[k] = reinterpret_cast<const float4*>(p.upack)[i];
+  }
+  float fw[kFwlwPT];
+  const int n_fwlw = (flags & kFoFwlw) ? F * D : 0;
+#pragma unroll
+  for (int k = 0; k < kFwlwPT; ++k) {
+    const int i = tid + k * NTH;
+    if (i < n_fwlw) fw[k] = p.fwlw[i];
+  }
+  const float lwv = ((flags & kFoLw) && tid < F) ? p.lw[tid] : 0.f;
+#pragma unroll
+  for (int k = 0; k < kDescPT; ++k) {
+    const int i = tid + k * NTH;
+    if (i < 7 * F) reinterpret_cast<uint2*>(desc)[i] = dw[k];
+  }
   __syncthreads();
+  stamp(p.stamps, 1, tid);
 
   // ---- phase G: gather E rows and table first order --------------------------
   {
@@ -271,8 +295,8 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
         const FieldDev fd = desc[f];
         if (f < num) {
           scale[k] = __int_as_float((int)key[k]);
-          pa[k] = pb[k] = fd.emb2;
-          qa[k] = qb[k] = fd.emb1;
+          pa[k] = fd.emb2;
+          qa[k] = fd.emb1;
         } else {
           int64_t idx = key[k];
           if (idx < 0 || idx >= fd.n) {
@@ -280,8 +304,8 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
             idx = 0;
           }
           if (fd.c == 0) {
-            pa[k] = pb[k] = fd.emb2 + idx * D;
-            if (fo_tab) qa[k] = qb[k] = fd.emb1 + idx;
+            pa[k] = fd.emb2 + idx * D;
+            if (fo_tab) qa[k] = fd.emb1 + idx;
           } else {
             const int64_t q = idx / fd.c;
             const int64_t rr = idx - q * fd.c;
@@ -296,19 +320,46 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
         }
       }
     }
-    // all loads first ...
+    // all loads first (the second operand only for QR rows) ...
     float va[RPT][D], vb[RPT][D], fa[RPT], fb[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       fa[k] = fb[k] = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) va[k][d] = vb[k][d] = 0.f;
       if (live[k] && needE) {
         load_row<D>(va[k], pa[k]);
-        load_row<D>(vb[k], pb[k]);
+        if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
       }
       if (live[k] && fo_tab) {
         fa[k] = *qa[k];
-        fb[k] = *qb[k];
+        if (mode[k] != 0) fb[k] = *qb[k];
       }
+    }
+    // layer-0 weights: the first two chunks go out behind the row loads (vmcnt retires in issue
+    // order, so issuing them earlier would make every gather wait for 56 KB of weights) and land
+    // during the combine, the shallow part and the barriers
+    if (deep) {
+      ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
+      ls.preload(wb0, wb1, lane * 16);
+    }
+    // ... the shallow parameters go to LDS while the row loads are in flight ...
+#pragma unroll
+    for (int k = 0; k < kUpkPT; ++k) {
+      const int i = tid + k * NTH;
+      if (i < n_upk) reinterpret_cast<float4*>(upk)[i] = uw[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kFwlwPT; ++k) {
+      const int i = tid + k * NTH;
+      if (i < n_fwlw) fwlw_s[i] = fw[k];
+    }
+    if ((flags & kFoLw) && tid < F) lw_s[tid] = lwv;
+    // zero the E-tile padding read by the MLP (NC0*16 columns) and the FwFM (S*4 fields)
+    const int w = p.W0 - F * D;
+    for (int i = tid; i < kBM * w; i += NTH) {
+      const int b = i / w;
+      bufX[b * SX + F * D + (i - b * w)] = 0.f;
     }
     // ... then combine and store
 #pragma unroll
@@ -326,14 +377,9 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
         fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], fb[k], scale[k]) : 0.f;
       }
     }
-    // zero the E-tile padding read by the MLP (NC0*16 columns) and the FwFM (S*4 fields)
-    const int w = p.W0 - F * D;
-    for (int i = tid; i < kBM * w; i += NTH) {
-      const int b = i / w;
-      bufX[b * SX + F * D + (i - b * w)] = 0.f;
-    }
   }
   __syncthreads();
+  stamp(p.stamps, 2, tid);
 
   // ---- phase S: shallow part ----------------------------------------------
   if (flags & kFoFwlw) {
@@ -349,6 +395,7 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
       fo[b * Fp + f] = s;
     }
   }
+  stamp(p.stamps, 9, tid);
   if (flags & kHasSecond) {
     // Y = U * E_b on MFMA: rows k (fields, MT tiles), columns n = b*D + d (D tiles of 16),
     // contraction over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].
@@ -366,19 +413,29 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
       v[j] = 0.f;
     }
     // one row tile at a time keeps the accumulators in fixed registers (guarded MFMAs make hipcc
-    // shuttle every accumulator between AGPRs and VGPRs); U's rows 16m.. vanish for l <= 16m
+    // shuttle every accumulator between AGPRs and VGPRs); U's rows 16m.. vanish for l <= 16m.
+    // Steps go in groups of 4 with every operand of the group read from LDS before its MFMAs.
     for (int m = 0; m < MT; ++m) {
       f32x4 acc[NTW];
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int s = (16 * m + 1) >> 2; s < S; ++s) {
-        const int l = 4 * s + (lane >> 4);
-        const float av = upk[(m * S + s) * 64 + lane];
-        float bv[NTW];
+      for (int s0 = (16 * m + 1) >> 2; s0 < S; s0 += 4) {
+        float av[4], bv[4][NTW];
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) bv[j] = ecol[j][l * D];
+        for (int u = 0; u < 4; ++u) {
+          const int s = s0 + u < S ? s0 + u : S - 1;  // clamped reads; the MFMA is skipped below
+          av[u] = upk[(m * S + s) * 64 + lane];
+          const int l = 4 * s + (lane >> 4);
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
+          for (int j = 0; j < NTW; ++j) bv[u][j] = ecol[j][l * D];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // all 16 LDS reads issue before the group's MFMAs
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float a_eff = s0 + u < S ? av[u] : 0.f;  // a zero A fragment adds exactly 0
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_eff, bv[u][j], acc[j], 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -400,20 +457,27 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
       if (lane < 16 && nt < D) part2[nt * 16 + lane] = x;
     }
   }
+  stamp(p.stamps, 10, tid);
   __syncthreads();
-  if (tid < kBM) {
-    float first = 0.f;
-    if (flags & kFoLw) {
-      for (int f = 0; f < F; ++f) first = fmaf(fo[tid * Fp + f], lw_s[f], first);
-    } else {
-      for (int f = 0; f < F; ++f) first += fo[tid * Fp + f];
+  stamp(p.stamps, 11, tid);
+  if (wave < 4) {
+    // first[b] (lw projection or plain sum over fields) and second[b] (sum over d): 16 lanes per
+    // sample each take every 16th term, then a 16-lane butterfly (a serial 39-term LDS chain in 16
+    // threads cost ~5k cycles)
+    const int b = wave * 4 + (lane >> 4);
+    const int q = lane & 15;
+    float first = 0.f, second = 0.f;
+    for (int f = q; f < F; f += 16) {
+      const float x = fo[b * Fp + f];
+      first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
     }
-    float second = 0.f;
-    if (flags & kHasSecond) {
+    if ((flags & kHasSecond) && q < D) second = part2[b * D + q];
 #pragma unroll
-      for (int d = 0; d < D; ++d) second += part2[tid * D + d];
+    for (int o = 8; o >= 1; o >>= 1) {
+      first += __shfl_xor(first, o);
+      second += __shfl_xor(second, o);
     }
-    fs[tid] = first + second;
+    if (q == 0) fs[b] = first + second;
   }
 
   if (!deep) {
@@ -422,6 +486,7 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
     return;
   }
 
+  stamp(p.stamps, 3, tid);
   // ---- phase M: MLP on MFMA -------------------------------------------------
   const int row0 = (lane >> 4) * 4;
   float dpart[4] = {0.f, 0.f, 0.f, 0.f};
@@ -489,6 +554,7 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
       }
     }
     __syncthreads();
+    stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
   }
 
   // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the 16 lanes sharing (lane>>4), then the 4 groups
@@ -512,6 +578,7 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
     const float deepv = ((dsum[tid] + dsum[kBM + tid]) + dsum[2 * kBM + tid]) + dsum[3 * kBM + tid];
     p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
+  stamp(p.stamps, 8, tid);
 }
 
 // ---------------------------------------------------------------------------
