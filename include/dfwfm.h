@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DFWFM_ABI_VERSION 1
+#define DFWFM_ABI_VERSION 2
 
 typedef enum {
   DFWFM_OK = 0,
@@ -111,6 +111,58 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
  * Replaces DeepFMs.forward, model/DeepFMs.py:285-469. */
 int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv,
                   int64_t xv_stride, int64_t batch, float* out, void* stream);
+
+/* ---- training step (reference model/DeepFMs.py:553-637) ---------------------------------- */
+
+/* Forward of a training step: as dfwfm_forward, and additionally keeps (in model-owned device
+ * memory, grown on demand -- so the first call at a new batch size allocates) the activations
+ * the backward needs.  dropout_p is the deep tower's dropout (reference nn.Dropout(0.5) on
+ * deep_emb and after every hidden ReLU, :260-282; 0 = none); masks come from a counter hash of
+ * (seed, layer, row, column), so the backward regenerates them. */
+int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv,
+                        int64_t xv_stride, int64_t batch, float* out, float dropout_p, uint32_t seed,
+                        void* stream);
+
+/* Gradient buffers of one field's tables (device, dense, same shapes as the tables; any may be
+ * NULL to skip it). */
+typedef struct {
+  float* emb2;
+  float* emb2_r;
+  float* emb1;
+  float* emb1_r;
+} dfwfm_field_grads;
+
+/* Dense gradient buffers, accumulated into (+=), like autograd's .grad.  NULL skips a tensor. */
+typedef struct {
+  const dfwfm_field_grads* fields;  /* host array of field_size entries                     */
+  float* field_cov;                 /* [F, F]                                                */
+  float* fwfm_lin;                  /* [F, D]                                                */
+  float* fm_1st;                    /* [F]                                                   */
+  float* bias;                      /* [1]                                                   */
+  float* const* lin_w;              /* host array of h_depth device pointers, [N, K_h] each  */
+  float* const* lin_b;              /* host array of h_depth device pointers, [N] each       */
+  float* fc_w;                      /* [N]                                                   */
+} dfwfm_grads;
+
+/* Backward of the last dfwfm_train_forward: dlogit [batch] = dLoss/dlogit (e.g. (sigmoid(z) - y)
+ * / batch for the reference's BCE-with-logits mean, :634).  Replaces loss.backward() (:636). */
+int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads, void* stream);
+
+/* One tensor of an Adam step (device pointers; grad NULL = tensor skipped, as torch does). */
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+} dfwfm_adam_tensor;
+
+/* torch.optim.Adam(lr, betas, eps, weight_decay) step number `step` (1-based) over n tensors
+ * (replaces optimizer.step(), :637).  The hyper-parameters are doubles, like the Python floats torch
+ * derives its scalars from (bias corrections in double, then rounded to f32 per use).  Tensors must
+ * not alias.  Needs no model: the list travels in the kernel arguments (no host synchronisation). */
+int dfwfm_adam_step(const dfwfm_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,
+                    double eps, double weight_decay, int64_t step, void* stream);
 
 /* Synchronises `stream`, returns the sticky error-flag word and clears it. */
 int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream);

@@ -18,6 +18,7 @@ representative (reference model/DeepFMs.py:297-458):
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -48,6 +49,12 @@ def _field_embeddings(cfg, params, Xi, Xv, prefix):
 @torch.no_grad()
 def forward(cfg, params, Xi, Xv):
     """params: name -> float32 CPU tensor; Xi int64 [B, ncat]; Xv float32 [B, num]. Returns [B] fp32."""
+    return forward_graph(cfg, params, Xi, Xv)
+
+
+def forward_graph(cfg, params, Xi, Xv, masks=None, drop_p=0.0):
+    """forward() with autograd; masks[h] ([B, width] bool, h = 0..H) are the deep tower's dropout keep
+    masks (nn.Dropout: x * keep / (1 - p), reference :411, :417-426)."""
     Xi = Xi.reshape(Xi.shape[0], -1)
     fwfm, fm = bool(cfg.get("use_fwfm")), bool(cfg.get("use_fm"))
     emb2 = _field_embeddings(cfg, params, Xi, Xv, "fm_2nd_embeddings") if (fwfm or fm or cfg.get("use_deep")) else None
@@ -73,7 +80,57 @@ def forward(cfg, params, Xi, Xv):
         total = total + second.sum(1)
     if cfg.get("use_deep"):
         h = torch.cat(emb2, 1)
+        scale = 1.0 / (1.0 - drop_p) if masks is not None else 1.0
+        if masks is not None:
+            h = h * (masks[0].to(h.dtype) * scale)
         for i in range(1, cfg["h_depth"] + 1):
             h = torch.relu(torch.addmm(params[f"net_1_linear_{i}.bias"], h, params[f"net_1_linear_{i}.weight"].t()))
+            if masks is not None:
+                h = h * (masks[i].to(h.dtype) * scale)
         total = total + torch.mm(h, params["net_1_fc.weight"].t()).sum(1)
     return total + params["bias"]
+
+
+# ---- training step (reference model/DeepFMs.py:553-637) -------------------------------------------
+def _mix32(x):
+    x = x.astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    x = (x * np.uint32(0x7FEB352D)).astype(np.uint32)
+    x ^= x >> np.uint32(15)
+    x = (x * np.uint32(0x846CA68B)).astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def dropout_masks(seed, p, B, widths, row0=0):
+    """The HIP kernels' counter-hash dropout keep masks (csrc/dfwfm_device.h dropout_keep), restated:
+    keep (layer, row, col) iff (hash >> 8) / 2^24 >= p.  widths[h] = columns of layer h's output."""
+    out = []
+    with np.errstate(over="ignore"):
+        rows = (np.arange(B, dtype=np.int64) + row0).astype(np.uint32)[:, None]
+        for layer, w in enumerate(widths):
+            cols = np.arange(w, dtype=np.uint32)[None, :]
+            hc = _mix32(cols + np.uint32(0x632BE5AB))
+            hr = _mix32(rows ^ hc)
+            hl = _mix32((np.uint32(layer) * np.uint32(0x9E3779B9)).astype(np.uint32) ^ hr)
+            h = _mix32(np.uint32(seed) ^ hl)
+            u = (h >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+            out.append(torch.from_numpy(u >= np.float32(p)))
+    return out
+
+
+def train_step(cfg, params, Xi, Xv, y, lr, l2, masks=None, drop_p=0.0):
+    """One reference training step: BCE-with-logits mean, backward, torch.optim.Adam(lr, weight_decay=l2)
+    on CPU.  Returns (logits, loss, grads, new_params) as numpy."""
+    leaf = {k: torch.tensor(v, requires_grad=True) for k, v in params.items()}
+    out = forward_graph(cfg, leaf, torch.as_tensor(Xi), torch.as_tensor(Xv), masks, drop_p)
+    loss = F.binary_cross_entropy_with_logits(out, torch.as_tensor(y, dtype=torch.float32))
+    loss.backward()
+    grads = {k: (v.grad.numpy().copy() if v.grad is not None else np.zeros_like(params[k]))
+             for k, v in leaf.items()}
+    for v in leaf.values():
+        if v.grad is None:
+            v.grad = torch.zeros_like(v)
+    opt = torch.optim.Adam(list(leaf.values()), lr=lr, weight_decay=l2)
+    opt.step()
+    return out.detach().numpy(), float(loss.item()), grads, {k: v.detach().numpy() for k, v in leaf.items()}

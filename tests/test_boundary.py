@@ -26,9 +26,9 @@ def header_functions():
 
 def test_header_declares_expected_api():
     assert header_functions() == sorted([
-        "dfwfm_abi_version", "dfwfm_diag_stamps", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create",
-        "dfwfm_model_destroy",
-        "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_read_error_flag"])
+        "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_backward", "dfwfm_diag_stamps", "dfwfm_forward",
+        "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy", "dfwfm_model_set_dense",
+        "dfwfm_model_set_tables", "dfwfm_read_error_flag", "dfwfm_train_forward"])
 
 
 def test_library_exports_every_header_symbol(built):
@@ -40,17 +40,24 @@ def test_library_exports_every_header_symbol(built):
 
 def test_abi_version_and_error_string(built):
     L = built.lib()
-    assert L.dfwfm_abi_version() == 1
+    assert L.dfwfm_abi_version() == 2
     assert isinstance(L.dfwfm_last_error(), bytes)
     # invalid arguments are reported, never abort (no HIP call is reached)
     assert L.dfwfm_model_create(None, None) == -1
     assert b"null" in L.dfwfm_last_error()
     assert L.dfwfm_forward(None, None, 0, None, 0, 0, None, None) == -1
+    assert L.dfwfm_train_forward(None, None, 0, None, 0, 0, None, 0.0, 0, None) == -1
+    assert L.dfwfm_backward(None, None, None, None) == -1
+    assert L.dfwfm_adam_step(None, 3, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, None) == -1
+    assert L.dfwfm_adam_step(None, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None) == -1  # step >= 1
 
 
 def test_struct_layouts_match_header(built):
     assert ctypes.sizeof(built.dfwfm_config) == 11 * 4
     assert ctypes.sizeof(built.dfwfm_field_tables) == 4 * 8 + 2 * 8 + 2 * 4
+    assert ctypes.sizeof(built.dfwfm_field_grads) == 4 * 8
+    assert ctypes.sizeof(built.dfwfm_grads) == 8 * 8
+    assert ctypes.sizeof(built.dfwfm_adam_tensor) == 5 * 8
 
 
 @pytest.mark.parametrize("name", golden_names())

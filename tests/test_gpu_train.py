@@ -1,0 +1,150 @@
+"""GPU: one HIP training step (fused forward in train mode -> HIP backward -> HIP Adam), through the C ABI,
+against the reference's one-step goldens and the training oracle (with the kernels' dropout masks)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import load_train_golden, logit_close, logit_close_scaled, model_kwargs, train_golden_names
+from oracle import torch_port
+from test_train_oracle import compare_step
+
+pytestmark = pytest.mark.gpu
+
+# fp32 with atomically accumulated (order-free) sums: gradients to 2e-5 of each tensor's largest entry;
+# Adam's first step is ~ -lr * sign(g), so the update is checked in lr units where |g + l2*p| is not tiny
+G_TOL, DP_TOL = 2e-5, 2e-3
+
+
+def build(cfg, params, device, **kw):
+    from xsdeepfwfm_deprecated_amd import DeepFMs
+    m = DeepFMs(**model_kwargs(cfg), **kw)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    return m.to(device).train()
+
+
+def hip_step(m, xi, xv, y, device, lr, l2):
+    from xsdeepfwfm_deprecated_amd.training import Adam
+    opt = Adam(m.parameters(), lr=lr, weight_decay=l2)
+    opt.zero_grad()
+    out = m(torch.from_numpy(xi).to(device), torch.from_numpy(xv).to(device))
+    loss = F.binary_cross_entropy_with_logits(out, torch.from_numpy(y).to(device))
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().cpu().numpy() for k, p in m.named_parameters()}
+    opt.step()
+    torch.cuda.synchronize()
+    newp = {k: p.detach().cpu().numpy() for k, p in m.named_parameters()}
+    return out.detach().cpu().numpy(), float(loss.item()), grads, newp
+
+
+def check_dp(cfg, params, grads, newp, ref_grads, ref_newp, lr, l2):
+    """Update error in lr units over entries whose effective Adam gradient is not within noise of 0."""
+    worst = 0.0
+    for k in ref_grads:
+        geff = (ref_grads[k] + l2 * params[k]).reshape(-1)
+        big = np.abs(geff) > 1e-6
+        d = (newp[k] - params[k]).reshape(-1)[big]
+        dr = (ref_newp[k] - params[k]).reshape(-1)[big]
+        if d.size:
+            worst = max(worst, float(np.abs(d - dr).max() / lr))
+    return worst
+
+
+@pytest.mark.parametrize("name", train_golden_names())
+def test_train_step_matches_reference(gpu, name):
+    cfg, params, xi, xv, y, loss_ref, logits_ref, ref = load_train_golden(name)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    out, loss, grads, newp = hip_step(m, xi, xv, y, gpu, cfg["lr"], cfg["l2"])
+    assert logit_close_scaled(out, logits_ref, cfg, params, xi, xv) < 1e-5
+    assert abs(loss - loss_ref) <= 1e-5 * max(1.0, abs(loss_ref))
+    worst_g = 0.0
+    for k, (idx, gr, dp, gn) in ref.items():
+        g = grads[k].reshape(-1).astype(np.float64)
+        assert abs(np.linalg.norm(g) - gn) <= 1e-4 * gn + 1e-12, k
+        gs = g[idx] if idx is not None else g
+        worst_g = max(worst_g, float(np.abs(gs - gr).max() / (np.abs(gr).max() + 1e-30)))
+    assert worst_g <= G_TOL, worst_g
+    # the full update against the oracle's (the goldens store a sample of large tensors)
+    _, _, og, onew = torch_port.train_step(cfg, params, xi, xv, y, cfg["lr"], cfg["l2"])
+    assert check_dp(cfg, params, grads, newp, og, onew, cfg["lr"], cfg["l2"]) <= DP_TOL
+
+
+@pytest.mark.parametrize("B", [1, 15, 17, 100])
+def test_train_step_ragged_batches(gpu, B):
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_fwlw")
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    out, loss, grads, newp = hip_step(m, xi[:B], xv[:B], y[:B], gpu, 1e-3, 3e-7)
+    o_out, o_loss, og, onew = torch_port.train_step(cfg, params, xi[:B], xv[:B], y[:B], 1e-3, 3e-7)
+    assert logit_close(out, o_out) < 1e-5
+    for k in og:
+        sc = np.abs(og[k]).max()
+        assert np.abs(grads[k] - og[k]).max() <= G_TOL * sc + 1e-12, k
+
+
+@pytest.mark.parametrize("name", ["train_small_mlp", "train_deepfwfm_lw"])
+def test_train_step_with_dropout_matches_oracle_masks(gpu, name):
+    """Deep-tower dropout (p = 0.5): the oracle rebuilds the kernels' counter-hash masks."""
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    m = build(cfg, params, gpu, is_deep_dropout=True)
+    torch.manual_seed(99)
+    seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())  # what train_forward draws next
+    torch.manual_seed(99)
+    out, loss, grads, newp = hip_step(m, xi, xv, y, gpu, 1e-3, 0.0)
+    widths = [cfg["field_size"] * cfg["embedding_size"]] + [cfg["deep_nodes"]] * cfg["h_depth"]
+    masks = torch_port.dropout_masks(seed, 0.5, len(xi), widths)
+    o_out, o_loss, og, onew = torch_port.train_step(cfg, params, xi, xv, y, 1e-3, 0.0, masks, 0.5)
+    assert logit_close(out, o_out) < 1e-5
+    for k in og:
+        sc = np.abs(og[k]).max()
+        assert np.abs(grads[k] - og[k]).max() <= G_TOL * sc + 1e-12, k
+    assert check_dp(cfg, params, grads, newp, og, onew, 1e-3, 0.0) <= DP_TOL
+
+
+def test_adam_matches_torch_over_steps(gpu):
+    """Five HIP Adam steps on fixed gradients equal torch.optim.Adam's single-tensor (CPU) updates."""
+    from xsdeepfwfm_deprecated_amd.training import Adam
+    g = torch.Generator().manual_seed(3)
+    shapes = [(1000,), (37, 11), (5000, 10), (1,)]
+    ps = [torch.randn(s, generator=g) for s in shapes]
+    gs = [[torch.randn(s, generator=g) * 10 ** float(torch.randint(-8, 1, (1,), generator=g)) for s in shapes]
+          for _ in range(5)]
+    cpu = [p.clone().requires_grad_(True) for p in ps]
+    dev = [torch.nn.Parameter(p.clone().to(gpu)) for p in ps]
+    o_cpu = torch.optim.Adam(cpu, lr=1e-3, weight_decay=3e-7, foreach=False)
+    o_dev = Adam(dev, lr=1e-3, weight_decay=3e-7)
+    for step in range(5):
+        for p, q, gg in zip(cpu, dev, gs[step]):
+            p.grad = gg.clone()
+            q.grad = gg.clone().to(gpu)
+        o_cpu.step()
+        o_dev.step()
+    for p, q in zip(cpu, dev):
+        # within 2 ulp of the parameter, or 2e-6 lr (sqrt / division rounding of the two implementations)
+        np.testing.assert_allclose(q.detach().cpu().numpy(), p.detach().numpy(), rtol=2.4e-7, atol=2e-9)
+    sd = o_dev.state_dict()
+    assert sd["state"][0]["step"].item() == 5.0 and set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+
+
+def test_backward_of_stale_forward_raises(gpu):
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_small_mlp")
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    a = m(torch.from_numpy(xi[:32]).to(gpu), torch.from_numpy(xv[:32]).to(gpu))
+    m(torch.from_numpy(xi[32:64]).to(gpu), torch.from_numpy(xv[32:64]).to(gpu))
+    with pytest.raises(RuntimeError, match="stale"):
+        a.sum().backward()
+
+
+def test_fit_learns(gpu):
+    """fit(): the reference's loop (init, Adam, shuffle, per-epoch eval) on the HIP kernels; training AUC
+    rises on a learnable synthetic target."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = [1] * 13 + [50, 300, 7, 1000, 20, 5, 64, 9, 100, 3, 11, 17, 250, 4, 6, 30, 8, 2, 40, 12, 90, 5, 15,
+                        300, 7, 60]
+    xi, xv = synth.synth_inputs(sizes, 13, 8192, seed=5)
+    logit = ((xi[:, 0] % 7) - 3) * 0.6 + (xv[:, 0] > 30) * 1.0 - 0.5
+    y = (np.random.default_rng(1).random(8192) < 1 / (1 + np.exp(-logit))).astype(np.float32)
+    m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1, n_epochs=3,
+                batch_size=256, learning_rate=1e-2, weight_decay=3e-7, h_depth=2, deep_nodes=64).to(gpu)
+    train_res, _ = m.fit(xi.reshape(-1, 26, 1), xv, y, [], [], [])
+    assert len(train_res) == 3 and train_res[-1] > 0.6 and train_res[-1] > train_res[0]

@@ -1,0 +1,134 @@
+"""CPU: the training-step oracle (oracle/torch_port.train_step) is pinned to the reference's own one-step
+goldens (tests/golden/train_*.npz, written by gen_golden_train.py from the reference model), and the
+host-side training logic (pruning threshold, DP gradient all-reduce over gloo) behaves as the reference."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_train_golden, train_golden_names
+from oracle import torch_port
+
+
+def compare_step(cfg, params, ref, grads, newp, g_tol=1e-5, dp_tol=1e-4):
+    """Worst relative gradient error (per tensor, vs its max |grad|) and parameter-update error in lr units."""
+    worst_g = worst_dp = 0.0
+    for k, (idx, gr, dp, gn) in ref.items():
+        g = np.asarray(grads[k], np.float64).reshape(-1)
+        d = (np.asarray(newp[k], np.float64) - params[k]).reshape(-1)
+        if idx is not None:
+            g, d = g[idx], d[idx]
+        worst_g = max(worst_g, float(np.abs(g - gr).max() / (np.abs(gr).max() + 1e-30)))
+        worst_dp = max(worst_dp, float(np.abs(d - dp).max() / cfg["lr"]))
+    return worst_g, worst_dp
+
+
+@pytest.mark.parametrize("name", train_golden_names())
+def test_oracle_train_step_matches_reference(name):
+    cfg, params, xi, xv, y, loss, logits, ref = load_train_golden(name)
+    out, l, grads, newp = torch_port.train_step(cfg, params, xi, xv, y, cfg["lr"], cfg["l2"])
+    assert abs(l - loss) <= 1e-6 * max(1.0, abs(loss))
+    assert np.abs(out - logits).max() <= 1e-5
+    wg, wdp = compare_step(cfg, params, ref, grads, newp)
+    assert wg <= 1e-5 and wdp <= 1e-3, (wg, wdp)
+    for k, (_, _, _, gn) in ref.items():
+        assert abs(np.linalg.norm(grads[k].astype(np.float64)) - gn) <= 1e-5 * gn + 1e-12, k
+
+
+def test_dropout_masks_are_bernoulli_and_deterministic():
+    a = torch_port.dropout_masks(1234, 0.5, 512, [390, 400])
+    b = torch_port.dropout_masks(1234, 0.5, 512, [390, 400])
+    c = torch_port.dropout_masks(1235, 0.5, 512, [390, 400])
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    assert not torch.equal(a[0], c[0])
+    for m in a:
+        assert abs(m.float().mean().item() - 0.5) < 0.01
+    assert not torch.equal(a[0][:, :390], a[1][:, :390])  # layers decorrelated
+    # row offsets select the same global rows
+    d = torch_port.dropout_masks(1234, 0.5, 100, [400], row0=17)
+    e = torch_port.dropout_masks(1234, 0.5, 117, [400])
+    assert torch.equal(d[0], e[0][17:])
+
+
+def test_dropout_changes_the_step():
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_small_mlp")
+    widths = [cfg["field_size"] * cfg["embedding_size"]] + [cfg["deep_nodes"]] * cfg["h_depth"]
+    masks = torch_port.dropout_masks(7, 0.5, len(xi), widths)
+    o1, *_ = torch_port.train_step(cfg, params, xi, xv, y, 1e-3, 0.0)
+    o2, *_ = torch_port.train_step(cfg, params, xi, xv, y, 1e-3, 0.0, masks, 0.5)
+    assert not np.allclose(o1, o2)
+
+
+def test_binary_search_threshold_hits_target():
+    from xsdeepfwfm_deprecated_amd.training import binary_search_threshold
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(100000, generator=g) * 0.01
+    thr = binary_search_threshold(w, 0.4, w.numel())
+    assert abs((w.abs() < thr).float().mean().item() - 0.4) < 1e-3
+
+
+def test_prune_step_masks_like_reference():
+    """prune_step zeroes what the reference's loop zeroes (:647-673): emb by a shared threshold, each
+    linear weight to the target rate, R by its symmetric part (so the mask is symmetric)."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs
+    from conftest import model_kwargs
+    cfg, params, *_ = load_train_golden("train_small_mlp")
+    m = DeepFMs(**model_kwargs(cfg))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    from xsdeepfwfm_deprecated_amd.training import prune_step
+    prune_step(m, 0.5, prune_fm=1, prune_r=1, prune_deep=1, emb_r=0.444, emb_corr=1.0)
+    R = m.field_cov.weight.detach()
+    assert torch.equal(R == 0, (R == 0).t())
+    for i in range(1, cfg["h_depth"] + 1):
+        w = getattr(m, f"net_1_linear_{i}").weight
+        assert abs((w == 0).float().mean().item() - 0.5) < 2e-3
+    stacked = torch.cat([p.detach().reshape(-1) for n, p in m.named_parameters() if "fm_2nd_embeddings" in n])
+    assert abs((stacked == 0).float().mean().item() - 0.222) < 2e-3
+
+
+def _dp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from xsdeepfwfm_deprecated_amd.training import allreduce_grads
+        m = torch.nn.Module()
+        m.a = torch.nn.Parameter(torch.zeros(3))
+        m.b = torch.nn.Parameter(torch.zeros(2, 2))
+        flat = torch.arange(7, dtype=torch.float32) * (rank + 1)
+        m.a.grad = flat[:3]
+        m.b.grad = flat[3:].view(2, 2)
+        m._grad_flat = flat
+        allreduce_grads(m)  # the single flat all-reduce
+        r1 = (m.a.grad.clone(), m.b.grad.clone())
+        m._grad_flat = None
+        m.a.grad = torch.ones(3) * (rank + 1)
+        m.b.grad = torch.ones(2, 2) * 10 * (rank + 1)
+        allreduce_grads(m)  # the coalesced fallback
+        q.put((rank, r1, (m.a.grad.clone(), m.b.grad.clone())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_grad_allreduce_gloo_world2():
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    base = torch.arange(7, dtype=torch.float32) * 3
+    for r in range(2):
+        (a1, b1), (a2, b2) = res[r]
+        assert torch.equal(a1, base[:3]) and torch.equal(b1, base[3:].view(2, 2))
+        assert torch.equal(a2, torch.full((3,), 3.0)) and torch.equal(b2, torch.full((2, 2), 30.0))

@@ -1,0 +1,103 @@
+"""Training-step benchmark (BASELINE.json configs[4]: DeepFwFM training, DP over RCCL).
+
+    python tools/bench_train.py [--steps K] [--warmup W] [--batch 4096] [--first-order lw|fwlw]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_train.py
+
+One step = the reference's fit() inner loop body (model/DeepFMs.py:619-637) on a resident synthetic
+Criteo-39 batch: zero_grad, forward (train mode, deep dropout 0.5), BCE-with-logits mean, backward
+(HIP), gradient all-reduce when WORLD_SIZE > 1, HIP Adam step (lr 1e-3, weight_decay 3e-7).
+Prints one JSON line (samples/s over all ranks, ms/step, max over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
+    ap.add_argument("--no-dropout", action="store_true")
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    from xsdeepfwfm_deprecated_amd.training import Adam, allreduce_grads
+    sizes = synth.CRITEO_FEATURE_SIZES
+    fwlw = a.first_order == "fwlw"
+    model = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1,
+                    use_lw=1, use_fwlw=fwlw, numerical=13, is_deep_dropout=not a.no_dropout, use_cuda=True)
+    shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=1234)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    model = model.to(dev).train()
+    opt = Adam(model.parameters(), lr=1e-3, weight_decay=3e-7)
+    B = a.batch
+    batches = []
+    for i in range(4):
+        xi, xv = synth.synth_inputs(sizes, 13, B, seed=1000 * rank + i)
+        y = synth.synth_labels(B, seed=1000 * rank + i)
+        batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev),
+                        torch.from_numpy(y).float().to(dev)))
+
+    def step(i):
+        xi, xv, y = batches[i % 4]
+        opt.zero_grad()
+        out = model(xi, xv)
+        loss = F.binary_cross_entropy_with_logits(out, y)
+        loss.backward()
+        allreduce_grads(model)
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    wall0 = time.perf_counter()
+    t0.record()
+    for i in range(a.steps):
+        loss = step(i)
+    t1.record()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - wall0
+    ms = t0.elapsed_time(t1)
+    if world > 1:
+        t = torch.tensor([ms], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        ms = float(t.item())
+        torch.distributed.barrier()
+    res = {"metric": "DeepFwFM training samples/sec (Criteo-39, Adam, dropout 0.5)",
+           "value": round(world * B * a.steps / (ms / 1e3), 1), "unit": "samples/s", "n_gpus": world,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms / a.steps, 4), "per_gpu_batch": B,
+           "first_order": a.first_order, "dropout": not a.no_dropout, "wall_s": round(wall, 3),
+           "final_loss": round(float(loss.item()), 6)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -231,6 +231,34 @@ class DeepFMs(nn.Module):
                        self.bias.detach(), lin_w, lin_b, w("net_1_fc") if self.use_deep else None)
         return eng
 
+    def _param_layout(self):
+        """The trainable parameters in the C ABI's gradient layout (include/dfwfm.h dfwfm_grads):
+        per field (emb2, emb2_r, emb1, emb1_r) and the dense tensors -- Parameters, not copies."""
+        def parts(mod):
+            if mod is None:
+                return None, None
+            if isinstance(mod, QREmbeddingBag):
+                return mod.weight_q, mod.weight_r
+            return mod.weight, None
+        first = getattr(self, "fm_1st_embeddings", None)
+        second = getattr(self, "fm_2nd_embeddings", None)
+        fields = []
+        for f in range(self.field_size):
+            e2, e2r = parts(None if second is None else second[f])
+            e1, e1r = parts(None if first is None else first[f])
+            fields.append((e2, e2r, e1, e1r))
+
+        def w(name, attr="weight"):
+            m = getattr(self, name, None)
+            return None if m is None else getattr(m, attr)
+        H = self.h_depth if self.use_deep else 0
+        dense = dict(field_cov=w("field_cov"), fwfm_lin=w("fwfm_linear"),
+                     fm_1st=w("fm_1st") if self.use_lw else None, bias=getattr(self, "bias", None),
+                     lin_w=[w(f"net_1_linear_{i}") for i in range(1, H + 1)],
+                     lin_b=[w(f"net_1_linear_{i}", "bias") for i in range(1, H + 1)],
+                     fc_w=w("net_1_fc") if self.use_deep else None)
+        return fields, dense
+
     def _prep_inputs(self, Xi, Xv, device):
         ncat = self.field_size - self.num
         Xi = torch.as_tensor(Xi)

@@ -21,8 +21,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
-SOURCES = ["dfwfm_kernels.hip", "dfwfm_capi.hip"]
-HEADERS = ["dfwfm_internal.h", os.path.join("..", "..", "include", "dfwfm.h")]
+SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_capi.hip"]
+HEADERS = ["dfwfm_internal.h", "dfwfm_device.h", os.path.join("..", "..", "include", "dfwfm.h")]
 ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
 
 DFWFM_OK = 0
@@ -49,6 +49,24 @@ class dfwfm_field_tables(ctypes.Structure):
     ]
 
 
+class dfwfm_field_grads(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("emb2", "emb2_r", "emb1", "emb1_r")]
+
+
+class dfwfm_grads(ctypes.Structure):
+    _fields_ = [
+        ("fields", ctypes.POINTER(dfwfm_field_grads)),
+        ("field_cov", ctypes.c_void_p), ("fwfm_lin", ctypes.c_void_p), ("fm_1st", ctypes.c_void_p),
+        ("bias", ctypes.c_void_p), ("lin_w", ctypes.POINTER(ctypes.c_void_p)),
+        ("lin_b", ctypes.POINTER(ctypes.c_void_p)), ("fc_w", ctypes.c_void_p),
+    ]
+
+
+class dfwfm_adam_tensor(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
 # name -> (restype, argtypes); every symbol include/dfwfm.h declares
 _P = ctypes.c_void_p
 SIGNATURES = {
@@ -57,6 +75,12 @@ SIGNATURES = {
     "dfwfm_model_set_tables": (ctypes.c_int, [_P, ctypes.POINTER(dfwfm_field_tables), ctypes.c_int32, _P]),
     "dfwfm_model_set_dense": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P]),
     "dfwfm_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
+    "dfwfm_train_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P,
+                                           ctypes.c_float, ctypes.c_uint32, _P]),
+    "dfwfm_backward": (ctypes.c_int, [_P, _P, ctypes.POINTER(dfwfm_grads), _P]),
+    "dfwfm_adam_step": (ctypes.c_int, [ctypes.POINTER(dfwfm_adam_tensor), ctypes.c_int32, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_int64, _P]),
     "dfwfm_read_error_flag": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
     "dfwfm_last_error": (ctypes.c_char_p, []),
     "dfwfm_diag_stamps": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64, _P]),
@@ -76,16 +100,27 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile libdfwfm.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    """Compile libdfwfm.so for gfx950 in-tree (hipcc cross-compiles without a GPU): one object per
+    translation unit, compiled in parallel, then linked."""
     if not force and not _stale():
         return LIB_PATH
+    from concurrent.futures import ThreadPoolExecutor
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
+    objs = [os.path.join(CSRC, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+
+    def compile_one(i):
+        cmd = [hipcc] + flags + ["-c", "-o", objs[i], os.path.join(CSRC, SOURCES[i])]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True, cwd=CSRC)
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        list(ex.map(compile_one, range(len(SOURCES))))
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True, cwd=CSRC)
+    subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", tmp] + objs, check=True, cwd=CSRC)
+    for o in objs:
+        os.remove(o)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
@@ -106,7 +141,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.dfwfm_abi_version() != 1:
+        if L.dfwfm_abi_version() != 2:
             raise DfwfmError("libdfwfm ABI mismatch")
         _lib = L
     return _lib

@@ -6,7 +6,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cmath>
 #include <string>
+#include <vector>
 
 #include "dfwfm_internal.h"
 
@@ -32,6 +34,29 @@ struct dfwfm_model {
   float* d_bias;   // [1]
   uint64_t* d_stamps;  // diagnostics (DFWFM_DIAG_STAMPS)
   size_t stamps_cap;   // workgroups the stamp buffer holds
+  // training
+  float4* d_wtpack;    // transposed MLP packs for dX_{l-1} = G_l W_l
+  size_t wtpack_elems;
+  int wt_off[kMaxH + 1];
+  float* d_rsk;        // symmetric off-diagonal (R+R^T)/2 fragments
+  float* d_ws;         // activation workspace (E, fo, X_0..X_H, G_1..G_H)
+  int64_t ws_batch;
+  float* sv_e;
+  float* sv_fo;
+  float* sv_x[kMaxH + 1];
+  float* sv_g[kMaxH + 1];
+  float* sv_de;
+  float* red_part;        // per-16-row-tile partial sums of the shallow reductions
+  FieldDev h_fields[64];  // host copy of the field descriptors (scatter task planning)
+  // the last dfwfm_train_forward, replayed by dfwfm_backward
+  const int64_t* t_xi;
+  int64_t t_xs;
+  const float* t_xv;
+  int64_t t_vs;
+  int64_t t_batch;
+  float t_drop;
+  uint32_t t_seed;
+  bool trained;
   bool tables_set;
   bool dense_set;
 };
@@ -71,8 +96,8 @@ int dev_alloc(T** p, size_t count) {
 
 void free_model(dfwfm_model* m) {
   if (!m) return;
-  void* ptrs[] = {m->d_fields, m->d_upack, m->d_err, m->d_wpack, m->d_mlp_b,
-                  m->d_fc,     m->d_fwlw,  m->d_lw,  m->d_bias,  m->d_stamps};
+  void* ptrs[] = {m->d_fields, m->d_upack, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
+                  m->d_lw,     m->d_bias,  m->d_stamps,  m->d_wtpack, m->d_rsk,   m->d_ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -164,13 +189,21 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     free_model(m);
     return rc;
   }
+  if ((rc = dev_alloc(&m->d_rsk, (size_t)m->MT * m->S * 64))) {
+    free_model(m);
+    return rc;
+  }
   if (c.use_deep) {
     m->wpack_elems = (size_t)NT * m->NC0 * 64 + (size_t)(H - 1) * NT * NT * 64;
     if (m->wpack_elems * sizeof(float4) >= (size_t)1 << 31) {
       free_model(m);
       return fail(DFWFM_ERR_UNSUPPORTED, "packed MLP weights exceed the 2 GiB buffer-descriptor range");
     }
-    if ((rc = dev_alloc(&m->d_wpack, m->wpack_elems)) ||
+    // transposed packs: layer 1 block [NC0 tiles][NT chunks], layers 2..H [NT][NT]; same total
+    m->wtpack_elems = m->wpack_elems;
+    m->wt_off[1] = 0;
+    for (int l = 2; l <= H; ++l) m->wt_off[l] = m->wt_off[l - 1] + (l == 2 ? m->NC0 : NT) * NT * 64;
+    if ((rc = dev_alloc(&m->d_wtpack, m->wtpack_elems)) || (rc = dev_alloc(&m->d_wpack, m->wpack_elems)) ||
         (rc = dev_alloc(&m->d_mlp_b, (size_t)H * NT * 16)) || (rc = dev_alloc(&m->d_fc, (size_t)NT * 16))) {
       free_model(m);
       return rc;
@@ -217,6 +250,7 @@ int dfwfm_model_set_tables(dfwfm_model* m, const dfwfm_field_tables* t, int32_t 
   memcpy(host, t, sizeof(dfwfm_field_tables) * n);
   for (int f = 0; f < n; ++f)
     if (host[f].c > 0) host[f].n = (host[f].n + host[f].c - 1) / host[f].c * host[f].c;
+  memcpy(m->h_fields, host, sizeof(FieldDev) * n);
   HIP_TRY(hipMemcpyAsync(m->d_fields, host, sizeof(FieldDev) * n, hipMemcpyHostToDevice, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // `host` is a stack buffer
   m->tables_set = true;
@@ -235,6 +269,7 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
   if (!bias) return fail(DFWFM_ERR_INVALID_ARG, "bias is required");
   if (c.use_fwfm || c.use_fm) {
     hipError_t e = launch_pack_fwfm(field_cov, m->F, c.use_fm ? 1 : 0, m->MT, m->S, m->d_upack, s);
+    if (e == hipSuccess) e = launch_pack_fwfm_sym(field_cov, m->F, c.use_fm ? 1 : 0, m->MT, m->S, m->d_rsk, s);
     if (e != hipSuccess) return hip_fail(e, "pack_fwfm");
   }
   hipError_t e = hipSuccess;
@@ -250,6 +285,8 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
       const int K = h == 0 ? m->F * m->D : m->N;
       const int NC = h == 0 ? m->NC0 : m->NT;
       e = launch_pack_linear(lin_w[h], m->N, K, m->NT, NC, dst, s);
+      if (e == hipSuccess)
+        e = launch_pack_linear_t(lin_w[h], m->N, K, h == 0 ? m->NC0 : m->NT, m->NT, m->d_wtpack + m->wt_off[h + 1], s);
       if (e == hipSuccess) e = launch_pad_copy(lin_b[h], m->N, m->NT * 16, m->d_mlp_b + (size_t)h * m->NT * 16, s);
       if (e != hipSuccess) return hip_fail(e, "pack_linear");
       dst += (size_t)m->NT * NC * 64;
@@ -261,9 +298,12 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
   return DFWFM_OK;
 }
 
-int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
-                  int64_t batch, float* out, void* stream) {
-  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+}  // extern "C"
+
+namespace {
+
+int check_inputs(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
+                 int64_t batch, const void* out) {
   if (batch < 0) return fail(DFWFM_ERR_INVALID_ARG, "negative batch");
   if (!m->tables_set || !m->dense_set)
     return fail(DFWFM_ERR_STATE, "set_tables and set_dense must precede forward");
@@ -274,8 +314,11 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   if (ncat > 0 && xi_stride < ncat) return fail(DFWFM_ERR_INVALID_ARG, "xi_stride < F - numerical");
   if (m->num > 0 && xv_stride < m->num) return fail(DFWFM_ERR_INVALID_ARG, "xv_stride < numerical");
   if ((batch + kBM - 1) / kBM > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "batch too large");
+  return DFWFM_OK;
+}
 
-  FwdArgs a;
+void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int64_t xi_stride, const float* xv,
+                       int64_t xv_stride, int64_t batch, float* out) {
   memset(&a, 0, sizeof a);
   a.fields = m->d_fields;
   a.xi = xi;
@@ -305,11 +348,55 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
+}
+
+// Activation workspace for `batch` rows: E [B][F*D], fo [B][F], X_0 [B][r4(F*D)], X_h and G_h [B][N].
+int ensure_workspace(dfwfm_model* m, int64_t batch) {
+  if (batch <= m->ws_batch) return DFWFM_OK;
+  const int64_t FD = (int64_t)m->F * m->D;
+  const int64_t per_row = 2 * FD + m->F + (m->H > 0 ? r4((int)FD) + 2 * (int64_t)m->H * m->N : 0);
+  const int64_t red_blocks = (batch + kBM - 1) / kBM;
+  const int64_t red_floats = red_blocks * red_outputs(m->F, m->D, m->N, m->num);
+  if (m->d_ws) (void)hipFree(m->d_ws);
+  m->d_ws = nullptr;
+  m->ws_batch = 0;
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_ws), sizeof(float) * (size_t)(per_row * batch + red_floats + 64)));
+  // every array starts 16-byte aligned: the row counts are multiples of 4 or the offsets are padded
+  auto al = [](int64_t x) { return (x + 3) & ~(int64_t)3; };
+  float* p = m->d_ws;
+  m->sv_e = p;   p += al(FD * batch);
+  m->sv_de = p;  p += al(FD * batch);
+  m->red_part = p;  p += al(red_floats);
+  m->sv_fo = p;  p += al((int64_t)m->F * batch);
+  for (int h = 0; h <= kMaxH; ++h) m->sv_x[h] = m->sv_g[h] = nullptr;
+  if (m->H > 0) {
+    m->sv_x[0] = p;  p += r4((int)FD) * batch;
+    for (int h = 1; h <= m->H; ++h) {
+      m->sv_x[h] = p;  p += (int64_t)m->N * batch;
+      m->sv_g[h] = p;  p += (int64_t)m->N * batch;
+    }
+  }
+  m->ws_batch = batch;
+  return DFWFM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
+                  int64_t batch, float* out, void* stream) {
+  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
+  if (rc != DFWFM_OK || batch == 0) return rc;
+  FwdArgs a;
+  fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, out);
   // diagnostics only (phase timing): DFWFM_DIAG_DROP_FLAGS clears flag bits, results become invalid
   if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   a.stamps = nullptr;
-  if (getenv("DFWFM_DIAG_STAMPS")) {
+  const char* stv = getenv("DFWFM_DIAG_STAMPS");
+  if (stv && atoi(stv) == 1) {
     const size_t grid = (size_t)((batch + kBM - 1) / kBM);
     if (grid > m->stamps_cap) {
       if (m->d_stamps) (void)hipFree(m->d_stamps);
@@ -323,6 +410,300 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, m->KS, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
+}
+
+int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
+                        int64_t batch, float* out, float dropout_p, uint32_t seed, void* stream) {
+  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  m->trained = false;
+  int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
+  if (rc != DFWFM_OK) return rc;
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(DFWFM_ERR_INVALID_ARG, "dropout_p outside [0, 1)");
+  if (m->H > 0 && m->N % 4 != 0)
+    return fail(DFWFM_ERR_UNSUPPORTED, "training needs deep_nodes %% 4 == 0 (got %d)", m->N);
+  if (m->KS != 1) return fail(DFWFM_ERR_UNSUPPORTED, "training runs with DFWFM_KSPLIT=1 only");
+  if (backward_lds_bytes(m->F, m->D, m->MT, m->S, m->SX, m->SY) > 160 * 1024)
+    return fail(DFWFM_ERR_UNSUPPORTED, "backward LDS tile exceeds 160 KiB");
+  if ((rc = ensure_workspace(m, batch)) != DFWFM_OK) return rc;
+  m->t_xi = xi;
+  m->t_xs = xi_stride;
+  m->t_xv = xv;
+  m->t_vs = xv_stride;
+  m->t_batch = batch;
+  m->t_drop = dropout_p;
+  m->t_seed = seed;
+  if (batch == 0) {
+    m->trained = true;
+    return DFWFM_OK;
+  }
+  FwdArgs a;
+  fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, out);
+  a.flags |= kTrain | ((m->H > 0 && dropout_p > 0.f) ? kDrop : 0);
+  a.sv_e = m->sv_e;
+  a.sv_fo = m->sv_fo;
+  for (int h = 0; h <= m->H; ++h) a.sv_x[h] = m->sv_x[h];
+  a.drop_p = dropout_p;
+  a.drop_scale = 1.f / (1.f - dropout_p);
+  a.seed = seed;
+  hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, 1, m->lds_bytes, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "train forward launch");
+  m->trained = true;
+  return DFWFM_OK;
+}
+
+int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, void* stream) {
+  if (!m || !g) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_backward needs a preceding dfwfm_train_forward");
+  const int64_t batch = m->t_batch;
+  if (batch == 0) return DFWFM_OK;
+  if (!dlogit) return fail(DFWFM_ERR_INVALID_ARG, "null dlogit");
+  hipStream_t s = (hipStream_t)stream;
+  const int F = m->F, D = m->D, num = m->num, H = m->H;
+  const bool drop = H > 0 && m->t_drop > 0.f;
+  hipError_t e;
+
+  // 1. per-tile backward: dE and the G chain (no atomics)
+  if (m->flags & kNeedE) {
+    BwdArgs a;
+    memset(&a, 0, sizeof a);
+    a.batch = batch;
+    a.dlogit = dlogit;
+    a.sv_e = m->sv_e;
+    for (int h = 0; h <= H; ++h) {
+      a.sv_x[h] = m->sv_x[h];
+      a.sv_g[h] = m->sv_g[h];
+    }
+    a.sv_de = m->sv_de;
+    a.rsk = m->d_rsk;
+    a.fwlw = m->d_fwlw;
+    a.lw = m->d_lw;
+    a.fc = m->d_fc;
+    a.wtpack = m->d_wtpack;
+    a.wtpack_bytes = (int32_t)(m->wtpack_elems * sizeof(float4));
+    for (int l = 1; l <= H; ++l) a.wt_off[l] = m->wt_off[l];
+    a.F = F;
+    a.H = H;
+    a.N = m->N;
+    a.NT = m->NT;
+    a.NC0 = m->NC0;
+    a.MT = m->MT;
+    a.S = m->S;
+    a.SX = m->SX;
+    a.SY = m->SY;
+    a.W0 = m->W0;
+    a.flags = m->flags | (drop ? kDrop : 0);
+    a.drop_p = m->t_drop;
+    a.drop_scale = 1.f / (1.f - m->t_drop);
+    a.seed = m->t_seed;
+    // diagnostics only: DFWFM_DIAG_STAMPS=2 records the backward's phase clocks instead of the forward's
+    const char* stv = getenv("DFWFM_DIAG_STAMPS");
+    if (stv && atoi(stv) == 2) {
+      const size_t grid = (size_t)((batch + kBM - 1) / kBM);
+      if (grid > m->stamps_cap) {
+        if (m->d_stamps) (void)hipFree(m->d_stamps);
+        m->d_stamps = nullptr;
+        m->stamps_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_stamps), grid * kStampSlots * sizeof(uint64_t)));
+        m->stamps_cap = grid;
+      }
+      a.stamps = m->d_stamps;
+    }
+    const size_t lds = backward_lds_bytes(F, D, m->MT, m->S, m->SX, m->SY);
+    e = launch_backward(a, D, m->TPW > 0 ? m->TPW : 1, lds, s);
+    if (e != hipSuccess) return hip_fail(e, "backward launch");
+  }
+
+  // 2. dense shallow reductions: per 16-row tile, then summed over tiles
+  {
+    RedArgs r;
+    memset(&r, 0, sizeof r);
+    r.batch = batch;
+    r.part = m->red_part;
+    r.dlogit = dlogit;
+    r.sv_e = m->sv_e;
+    r.sv_fo = m->sv_fo;
+    r.sv_de = (m->flags & kNeedE) ? m->sv_de : nullptr;
+    r.x_h = H > 0 ? m->sv_x[H] : nullptr;
+    r.xv = m->t_xv;
+    r.xv_stride = m->t_vs;
+    r.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
+    r.g_bias = g->bias;
+    r.g_lw = (m->flags & kFoLw) ? g->fm_1st : nullptr;
+    r.g_fwlw = (m->flags & kFoFwlw) ? g->fwfm_lin : nullptr;
+    r.g_R = m->cfg.use_fwfm ? g->field_cov : nullptr;
+    r.g_fc = H > 0 ? g->fc_w : nullptr;
+    for (int f = 0; f < num && g->fields; ++f) {
+      r.g_num2[f] = (m->flags & kNeedE) ? g->fields[f].emb2 : nullptr;
+      r.g_num1[f] = (m->flags & kFoTables) ? g->fields[f].emb1 : nullptr;
+    }
+    r.F = F;
+    r.D = D;
+    r.num = num;
+    r.N = m->N;
+    r.MT = m->MT;
+    r.flags = m->flags;
+    e = launch_reduce(r, s);
+    if (e != hipSuccess) return hip_fail(e, "reduce launch");
+  }
+
+  // 3. categorical tables: privatised (LDS) tasks for small tables, atomic tasks for large ones
+  if (g->fields) {
+    ScatterArgs priv, atom;
+    memset(&priv, 0, sizeof priv);
+    priv.D = D;
+    priv.F = F;
+    priv.num = num;
+    priv.fields = m->d_fields;
+    priv.xi = m->t_xi;
+    priv.xi_stride = m->t_xs;
+    priv.batch = batch;
+    priv.sv_de = m->sv_de;
+    priv.dlogit = dlogit;
+    priv.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
+    memcpy(&atom, &priv, sizeof priv);
+    priv.chunk = 1024;  // 4 samples per lane
+    atom.chunk = 256;
+    const int64_t pchunks = (batch + priv.chunk - 1) / priv.chunk;
+    const int64_t achunks = (batch + atom.chunk - 1) / atom.chunk;
+    int blocks[2] = {0, 0};  // [atomic, priv]
+    auto flush = [&](bool is_priv) -> int {
+      ScatterArgs& L = is_priv ? priv : atom;
+      if (L.ntasks == 0) return DFWFM_OK;
+      hipError_t er = is_priv ? launch_scatter_priv(L, blocks[1], s) : launch_scatter(L, blocks[0], s);
+      L.ntasks = 0;
+      blocks[is_priv] = 0;
+      return er == hipSuccess ? DFWFM_OK : hip_fail(er, "scatter launch");
+    };
+    auto add = [&](float* gt, const float* other, int64_t c, int f, int kind, int src, int64_t rows) -> int {
+      if (!gt || rows <= 0) return DFWFM_OK;
+      const int w = src == 0 ? D : 1;
+      const bool is_priv = rows * (w + 1) <= kPrivFloats;
+      ScatterArgs& L = is_priv ? priv : atom;
+      const int64_t nb = is_priv ? pchunks : achunks;
+      if (L.ntasks == kScatterList || blocks[is_priv] + nb > 0x7fffffff) {
+        int rc = flush(is_priv);
+        if (rc != DFWFM_OK) return rc;
+      }
+      ScatterTask& t = L.t[L.ntasks];
+      t.g = gt;
+      t.other = other;
+      t.c = (int32_t)c;
+      t.field = (int16_t)f;
+      t.kind = (int8_t)kind;
+      t.src = (int8_t)src;
+      t.rows = (int32_t)(rows < 0x7fffffff ? rows : 0x7fffffff);
+      t.block0 = blocks[is_priv];
+      blocks[is_priv] += (int)nb;
+      L.ntasks++;
+      return DFWFM_OK;
+    };
+    int rc = DFWFM_OK;
+    for (int f = num; f < F && rc == DFWFM_OK; ++f) {
+      const FieldDev& fd = m->h_fields[f];
+      const dfwfm_field_grads& fg = g->fields[f];
+      if (fd.c > 0 && fd.c > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: QR collisions too large", f);
+      for (int src = 0; src < 2 && rc == DFWFM_OK; ++src) {
+        if (src == 0 && !(m->flags & kNeedE)) continue;
+        if (src == 1 && !(m->flags & kFoTables)) continue;
+        float* gq = src == 0 ? fg.emb2 : fg.emb1;
+        float* gr = src == 0 ? fg.emb2_r : fg.emb1_r;
+        if (fd.c == 0) {
+          rc = add(gq, nullptr, 0, f, 0, src, fd.n);
+        } else {
+          const bool mult = fd.op == 0;
+          const float* tq = src == 0 ? fd.emb2 : fd.emb1;
+          const float* tr = src == 0 ? fd.emb2_r : fd.emb1_r;
+          rc = add(gq, mult ? tr : nullptr, fd.c, f, 1, src, fd.n / fd.c);
+          if (rc == DFWFM_OK) rc = add(gr, mult ? tq : nullptr, fd.c, f, 2, src, fd.c);
+        }
+      }
+    }
+    if (rc == DFWFM_OK) rc = flush(true);
+    if (rc == DFWFM_OK) rc = flush(false);
+    if (rc != DFWFM_OK) return rc;
+  }
+
+  // 4. dW_l += G_l^T X_{l-1}, db_l += sum_b G_l
+  if (H > 0 && (g->lin_w || g->lin_b)) {
+    DwArgs d;
+    memset(&d, 0, sizeof d);
+    d.H = H;
+    d.N = m->N;
+    d.nnb = (m->N + 63) / 64;
+    d.batch = batch;
+    int per_split = 0;
+    for (int l = 1; l <= H; ++l) {
+      d.G[l] = m->sv_g[l];
+      d.X[l] = m->sv_x[l - 1];
+      d.gW[l] = g->lin_w ? g->lin_w[l - 1] : nullptr;
+      d.gB[l] = g->lin_b ? g->lin_b[l - 1] : nullptr;
+      d.K[l] = l == 1 ? F * D : m->N;
+      d.ldx[l] = l == 1 ? r4(F * D) : m->N;
+      d.nkb[l] = d.gW[l] ? (d.K[l] + 63) / 64 : (d.gB[l] ? 1 : 0);
+      per_split += d.nnb * d.nkb[l];
+    }
+    if (per_split > 0) {
+      // split the batch so the launch holds ~4 workgroups per CU, each over >= 128 rows
+      int64_t splits = (1024 + per_split - 1) / per_split;
+      if (const char* ds = getenv("DFWFM_DW_SPLITS")) splits = atoi(ds);  // tuning only
+      const int64_t max_splits = (batch + 127) / 128;
+      if (splits > max_splits) splits = max_splits;
+      if (splits < 1) splits = 1;
+      int64_t rows = (batch + splits - 1) / splits;
+      rows = (rows + 31) / 32 * 32;
+      splits = (batch + rows - 1) / rows;
+      d.splits = (int32_t)splits;
+      d.rows_per_split = rows;
+      d.blk0[1] = 0;
+      for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
+      e = launch_dw(d, d.blk0[H + 1], s);
+      if (e != hipSuccess) return hip_fail(e, "dw launch");
+    }
+  }
+  return DFWFM_OK;
+}
+
+int dfwfm_adam_step(const dfwfm_adam_tensor* t, int32_t n, double lr, double beta1, double beta2, double eps,
+                    double weight_decay, int64_t step, void* stream) {
+  if (n > 0 && !t) return fail(DFWFM_ERR_INVALID_ARG, "null tensor list");
+  if (n < 0) return fail(DFWFM_ERR_INVALID_ARG, "negative tensor count");
+  if (step < 1) return fail(DFWFM_ERR_INVALID_ARG, "step must be >= 1");
+  for (int i = 0; i < n; ++i)
+    if (t[i].grad && t[i].numel > 0 && (!t[i].param || !t[i].exp_avg || !t[i].exp_avg_sq))
+      return fail(DFWFM_ERR_INVALID_ARG, "adam tensor %d: null state pointer", i);
+  // torch.optim.Adam: bias corrections and step size in double (Python floats), rounded to f32 per use
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  const float step_size = (float)(lr / bc1), omb1 = (float)(1.0 - beta1), b2 = (float)beta2,
+              omb2 = (float)(1.0 - beta2), epsf = (float)eps, wd = (float)weight_decay, bc2s = (float)sqrt(bc2);
+  AdamList list;
+  memset(&list, 0, sizeof list);
+  int64_t blocks = 0;
+  auto flush = [&]() -> int {
+    if (list.n == 0) return DFWFM_OK;
+    hipError_t e = launch_adam(list, (int)blocks, step_size, omb1, b2, omb2, epsf, wd, bc2s, (hipStream_t)stream);
+    list.n = 0;
+    blocks = 0;
+    return e == hipSuccess ? DFWFM_OK : hip_fail(e, "adam launch");
+  };
+  for (int i = 0; i < n; ++i) {
+    if (!t[i].grad || t[i].numel <= 0) continue;  // torch skips parameters without a grad
+    const int64_t nb = (t[i].numel + 1023) / 1024;
+    if (nb > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "adam tensor %d too large", i);
+    if (list.n == kAdamList || blocks + nb > 0x7fffffff) {
+      int rc = flush();
+      if (rc != DFWFM_OK) return rc;
+    }
+    AdamTensor& a = list.t[list.n++];
+    a.p = t[i].param;
+    a.g = t[i].grad;
+    a.m = t[i].exp_avg;
+    a.v = t[i].exp_avg_sq;
+    a.n = t[i].numel;
+    a.block0 = blocks;
+    blocks += nb;
+  }
+  return flush();
 }
 
 int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream) {

@@ -1,0 +1,180 @@
+// dfwfm_device.h -- device helpers shared by the forward and training kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dfwfm_internal.h"
+
+namespace dfwfm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float relu_keep_nan(float v) { return v < 0.f ? 0.f : v; }
+
+// Diagnostic phase stamps (p.stamps != nullptr only in DFWFM_DIAG_STAMPS runs; in production the
+// branch is never taken): wave 0 lane 0 records the shader clock at phase boundaries.
+__device__ __forceinline__ void stamp(uint64_t* st, int slot, int tid) {
+  if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
+}
+
+// constant-rate (100 MHz) clock, comparable across XCDs: workgroup start/end spread
+__device__ __forceinline__ void stamp_rt(uint64_t* st, int slot, int tid) {
+  if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <int D>
+__device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict__ src) {
+  if constexpr (D % 4 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(src + d);
+      v[d] = x.x; v[d + 1] = x.y; v[d + 2] = x.z; v[d + 3] = x.w;
+    }
+  } else if constexpr (D % 2 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 2) {
+      const float2 x = *reinterpret_cast<const float2*>(src + d);
+      v[d] = x.x; v[d + 1] = x.y;
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = src[d];
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void store_row(float* dst, const float (&v)[D]) {
+  if constexpr (D % 4 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 4) *reinterpret_cast<float4*>(dst + d) = make_float4(v[d], v[d + 1], v[d + 2], v[d + 3]);
+  } else if constexpr (D % 2 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 2) *reinterpret_cast<float2*>(dst + d) = make_float2(v[d], v[d + 1]);
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) dst[d] = v[d];
+  }
+}
+
+// row combine modes: 0 = a * scale (numerical / plain, scale 1), 1 = a * b (QR mult), 2 = a + b (QR add)
+__device__ __forceinline__ float combine(int mode, float a, float b, float scale) {
+  return mode == 1 ? a * b : (mode == 2 ? a + b : a * scale);
+}
+
+// ---------------------------------------------------------------------------
+// phase M: one MLP layer for the workgroup's 16 rows, one wave's share.
+//   act : LDS [16][SA] input activations (K zero-padded to NC*16)
+//   wl  : packed weights of this layer, [NT][NC][64 lanes] float4
+//   the wave group g (0..3) owns output tiles g, g+4, ... (TPW of them; tiles
+//   past NT are clamped duplicates whose results are discarded); it walks K
+//   chunks c0, c0+KS, ...
+// Fragment algebra (16x16x4 f32): in sub-step s of chunk c lane l supplies
+//   A = act[l&15][16c + 4(l>>4) + s],  B = W[n0 + (l&15)][16c + 4(l>>4) + s].
+// ---------------------------------------------------------------------------
+template <int TPW>
+__device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[TPW], const float4& a, const f32x4 (&b)[TPW]) {
+  // sub-step-major: consecutive MFMAs hit different accumulators (16x16x4 f32 has a 40-cycle
+  // dependent latency against a 32-cycle issue interval)
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[j].x, acc[j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[j].y, acc[j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[j].z, acc[j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[j].w, acc[j], 0, 0, 0);
+}
+
+// One layer's weight stream for one wave: output tiles g, g+4, ... (clamped to NT-1) and K chunks
+// c0, c0+KS, ... of the packed [NT][NC][64] float4 layout.  Loads are buffer loads: the per-tile
+// base and the chunk offset are scalar (SALU), the only vector operand is lane*16 -- flat loads
+// spent a 64-bit VALU add per load in front of the MFMAs.
+template <int TPW, int KS>
+struct LayerStream {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int sbase[TPW];  // byte offset of each owned tile's [NC][64] block (wave-uniform)
+  int n, c0;
+  __device__ __forceinline__ void init(__amdgpu_buffer_rsrc_t r, int layer_off, int NC, int NT, int g, int c0_) {
+    rsrc = r;
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      int t = g + 4 * j;
+      t = t < NT ? t : NT - 1;
+      sbase[j] = __builtin_amdgcn_readfirstlane((layer_off + t * NC * 64) * 16);
+    }
+    c0 = c0_;
+    n = c0 < NC ? (NC - c0 + KS - 1) / KS : 0;
+  }
+  __device__ __forceinline__ int chunk(int i) const { return c0 + KS * (i < n ? i : n - 1); }
+  __device__ __forceinline__ void load(f32x4 (&b)[TPW], int c, int voff) const {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+      b[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, sbase[j] + c * 1024, 0));
+  }
+  // the first two chunks, issued ahead of time (before the previous phase's epilogue / barrier)
+  __device__ __forceinline__ void preload(f32x4 (&b0)[TPW], f32x4 (&b1)[TPW], int voff) const {
+    if (n == 0) return;
+    load(b0, chunk(0), voff);
+    load(b1, chunk(1), voff);
+  }
+};
+
+// K loop of one layer, entered with chunks 0 and 1 already in b0 / b1.  Weight fragments rotate
+// through three register sets, each refilled two chunks ahead of its MFMAs (the loop is unrolled
+// by 3 so no set is ever copied: a copy makes hipcc wait for the load it copies); the activation
+// fragment is read one chunk ahead.  Within a step the refill loads are interleaved with the first
+// MFMAs (sched_group_barrier: 2 MFMA, 1 load, ...), and a sched_barrier closes the step so hipcc
+// cannot sink them to their use.
+template <int TPW, int KS>
+__device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __restrict__ act, int SA,
+                                           const LayerStream<TPW, KS>& ls, f32x4 (&b0)[TPW],
+                                           f32x4 (&b1)[TPW], f32x4 (&b2)[TPW], int lane) {
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int n = ls.n;
+  if (n == 0) return;
+  const int voff = lane * 16;
+  const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
+  float4 a = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(0));
+#define DFWFM_STEP(X, Z, i)                                                             \
+  {                                                                                     \
+    const float4 an = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk((i) + 1));  \
+    ls.load(Z, ls.chunk((i) + 2), voff);                                                \
+    mfma_chunk<TPW>(acc, a, X);                                                         \
+    for (int q = 0; q < TPW; ++q) {                                                     \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                \
+    }                                                                                   \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TPW, 0);                            \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    a = an;                                                                             \
+  }
+  int i = 0;
+  for (; i + 3 <= n; i += 3) {
+    DFWFM_STEP(b0, b2, i);
+    DFWFM_STEP(b1, b0, i + 1);
+    DFWFM_STEP(b2, b1, i + 2);
+  }
+  if (i < n) DFWFM_STEP(b0, b2, i);
+  if (i + 1 < n) DFWFM_STEP(b1, b0, i + 1);
+#undef DFWFM_STEP
+}
+
+
+// Counter-based dropout mask (deep tower; reference nn.Dropout(0.5), model/DeepFMs.py:260-282):
+// keep element (layer, row, col) of a step iff a 24-bit hash of (seed, layer, row, col) >= p.
+// The same function regenerates the mask in the backward.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ bool dropout_keep(uint32_t seed, int layer, int64_t row, int col, float p) {
+  const uint32_t h = mix32(seed ^ mix32((uint32_t)layer * 0x9E3779B9U ^ mix32((uint32_t)row ^ mix32((uint32_t)col + 0x632BE5ABU))));
+  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
+}  // namespace dfwfm

@@ -19,6 +19,9 @@ constexpr int kFoTables = 4;   // first order from fm_1st_embeddings
 constexpr int kFoFwlw = 8;     // first order from fwfm_linear
 constexpr int kFoLw = 16;      // project first order with fm_1st.weight
 constexpr int kNeedE = 32;     // second-order / deep embeddings are gathered
+constexpr int kTrain = 64;     // save the activations the backward needs (FwdArgs::sv_*)
+constexpr int kDrop = 128;     // dropout on the deep tower (train only)
+constexpr int kMaxH = 16;      // hidden layers
 
 // Device copy of dfwfm_field_tables (same field order and sizes); for QR fields
 // n holds the accepted index bound ceil(n/c)*c.
@@ -59,6 +62,14 @@ struct FwdArgs {
   int32_t W0;          // E-tile columns that must be valid (zero padded past F*D)
   int32_t flags;
   uint64_t* stamps;    // diagnostics only: [grid][kStampSlots] shader-clock stamps, normally null
+  // training (flags & kTrain): activations kept for the backward
+  float* sv_e;              // [B][F*D] E before dropout
+  float* sv_fo;             // [B][F]   first order per field
+  float* sv_x[kMaxH + 1];   // X_0 [B][F*D] (deep_emb after dropout), X_h [B][N] (layer h output after
+                            // ReLU and dropout), h = 1..H
+  float drop_p;             // dropout probability of the deep tower (kDrop)
+  float drop_scale;         // 1 / (1 - p)
+  uint32_t seed;            // dropout hash seed of this step
 };
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.
@@ -87,10 +98,134 @@ __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int
   return L;
 }
 
+// Backward, per 16-sample tile (no atomics): dE of the shallow terms and of the MLP input (the
+// dX_{l-1} = G_l W_l chain on MFMA), G_l saved for the weight-gradient GEMM, dE saved for the
+// reductions and the table scatter.
+struct BwdArgs {
+  int64_t batch;
+  const float* dlogit;           // [B] dL/dlogit
+  const float* sv_e;             // [B][F*D]
+  const float* sv_x[kMaxH + 1];  // X_0 .. X_H
+  float* sv_g[kMaxH + 1];        // G_1 .. G_H written here ([B][N], dL/dz of each layer)
+  float* sv_de;                  // [B][F*D] dL/dE written here
+  const float* rsk;              // [MT][S][64] symmetric off-diagonal (R + R^T)/2 fragments (FM: ones)
+  const float* fwlw;             // [F*D]
+  const float* lw;               // [F]
+  const float* fc;               // [NT*16]
+  const float4* wtpack;          // transposed MLP packs: layer l block [KT_l][NT][64] float4
+  int32_t wtpack_bytes;
+  int32_t wt_off[kMaxH + 1];     // float4 offset of layer l's block (l = 1..H)
+  int32_t F, H, N;
+  int32_t NT, NC0, MT, S;
+  int32_t SX, SY, W0;
+  int32_t flags;
+  float drop_p, drop_scale;
+  uint32_t seed;
+  uint64_t* stamps;              // diagnostics only (DFWFM_DIAG_STAMPS=2): phase clocks per workgroup
+};
+
+// Batch reductions of the dense shallow parameters, per 16-row tile then summed over tiles:
+// bias, fm_1st (lw), fwfm_linear, field_cov (Gram on MFMA), net_1_fc, numerical-field tables.
+struct RedArgs {
+  int64_t batch;
+  const float* dlogit;
+  const float* sv_e;             // [B][F*D]
+  const float* sv_fo;            // [B][F]
+  const float* sv_de;            // [B][F*D]
+  const float* x_h;              // [B][N] last hidden layer output (net_1_fc input) or null
+  const float* xv;               // numerical values
+  int64_t xv_stride;
+  const float* lw;               // [F] (kFoLw)
+  float* g_bias;
+  float* g_lw;
+  float* g_fwlw;
+  float* g_R;
+  float* g_fc;
+  float* g_num2[64];             // numerical field f: d v_f [D]
+  float* g_num1[64];             // numerical field f: d w1_f [1]
+  float* part;                   // [ceil(B/16)][red_outputs] per-tile partial sums (no atomics)
+  int32_t F, D, num, N, MT;
+  int32_t flags;
+};
+// packed per-block outputs of the reduction: bias | lw[F] | fwlw[F*D] | R[F*F] | fc[N] | num2[num*D] | num1[num]
+__host__ __device__ inline int red_outputs(int F, int D, int N, int num) {
+  return 1 + F + F * D + F * F + N + num * D + num;
+}
+
+// Embedding-table scatter: one task per (categorical field, table) with dense grads.  Tables of at
+// most kPrivRows*w floats accumulate in LDS inside one workgroup (no global contention: a field
+// with 4 categories receives every sample); larger tables take global atomics, one sample per lane.
+constexpr int kPrivFloats = 24 * 1024;  // LDS of a privatised task: rows * (w + 1) (sums + row flags)
+struct ScatterTask {
+  float* g;             // grad of this table
+  const float* other;   // QR mult: the partner table whose row multiplies the gradient (else null)
+  int32_t c;            // QR collisions (kind 1, 2)
+  int16_t field;        // model field index
+  int8_t kind;          // 0 plain row idx, 1 quotient row idx / c, 2 remainder row idx % c
+  int8_t src;           // 0: dE[b, f, :] (row width D), 1: dfo[b, f] = dlogit * (lw[f] or 1) (width 1)
+  int32_t rows;         // table rows
+  int32_t block0;       // first workgroup of the task in its launch
+};
+static_assert(sizeof(ScatterTask) == 32, "scatter task layout");
+constexpr int kScatterList = 96;  // tasks per launch: the list is a kernel argument (< 4 KiB)
+struct ScatterArgs {
+  ScatterTask t[kScatterList];
+  int32_t ntasks;
+  int32_t D, F, num;
+  const FieldDev* fields;
+  const int64_t* xi;
+  int64_t xi_stride;
+  int64_t batch;
+  const float* sv_de;
+  const float* dlogit;
+  const float* lw;      // [F] or null (dfo = dlogit)
+  int32_t chunk;        // samples per workgroup of a non-privatised task
+};
+
+// dW_l += G_l^T X_{l-1} and db_l += sum_b G_l for every layer in one launch.
+struct DwArgs {
+  const float* G[kMaxH + 1];
+  const float* X[kMaxH + 1];
+  float* gW[kMaxH + 1];
+  float* gB[kMaxH + 1];
+  int32_t K[kMaxH + 1];          // input width of layer l
+  int32_t ldx[kMaxH + 1];        // row stride of X_{l-1} (multiple of 4)
+  int32_t blk0[kMaxH + 2];       // first workgroup of layer l (prefix over layers)
+  int32_t nkb[kMaxH + 1];        // 64-wide K blocks of layer l
+  int32_t H, N, nnb, splits;
+  int64_t batch;
+  int64_t rows_per_split;
+};
+
+// One tensor of a fused Adam step.
+struct AdamTensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+  int64_t block0;                // first workgroup of this tensor
+};
+constexpr int kAdamList = 40;    // tensors per Adam launch (the list is a kernel argument, < 4 KiB)
+struct AdamList {
+  AdamTensor t[kAdamList];
+  int32_t n;
+};
+
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, hipStream_t s);
 hipError_t launch_pack_linear(const float* w, int N, int K, int NT, int NC, float4* out, hipStream_t s);
 hipError_t launch_pad_copy(const float* src, int n, int npad, float* dst, hipStream_t s);
 hipError_t launch_pack_fwfm(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s);
+hipError_t launch_pack_linear_t(const float* w, int N, int K, int KT, int NTc, float4* out, hipStream_t s);
+hipError_t launch_pack_fwfm_sym(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s);
+hipError_t launch_backward(const BwdArgs& a, int D, int tpw, size_t lds, hipStream_t s);
+size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
+hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s);
+hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages
+hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s);
+hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s);
+hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
+                       float eps, float wd, float bc2_sqrt, hipStream_t s);
 
 }  // namespace dfwfm

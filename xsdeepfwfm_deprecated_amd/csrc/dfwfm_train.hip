@@ -1,0 +1,809 @@
+// dfwfm_train.hip -- CDNA4 (gfx950) kernels of the DeepFwFM training step
+// (reference model/DeepFMs.py:553-637: loss.backward() and Adam(weight_decay=l2).step()).
+//
+// Every gradient is a sum over the batch; the kernels are split by how that sum is formed, so that
+// no address receives more than a few dozen atomic adds (256-way contended device atomics cost more
+// than the rest of the step together):
+//   bwd_kernel      per 16-sample tile, no atomics: dE of the FwFM term ((R+R^T)/2 * E on MFMA)
+//                   and of fwlw, the MLP input-gradient chain dX_{l-1} = G_l W_l on MFMA (the
+//                   forward's weight-streaming loop over transposed packs) with ReLU / dropout masks
+//                   from the saved layer outputs; G_l and dE go to the workspace.
+//   reduce_kernel   dense shallow grads over 64-row blocks: bias, fm_1st, fwfm_linear, field_cov (a
+//                   dlogit-weighted Gram matrix on MFMA), net_1_fc, the numerical fields' tables.
+//   scatter_kernel  dE / dfo into the categorical tables' dense grads (nn.Embedding(sparse=False)):
+//                   small tables accumulate privately in LDS, large ones take global atomics.
+//   dw_kernel       dW_l += G_l^T X_{l-1} and db_l += sum G_l for all layers in one launch.
+//   adam_kernel     torch.optim.Adam's update (coupled L2, bias correction) over a tensor list.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dfwfm_device.h"
+#include "dfwfm_internal.h"
+
+namespace dfwfm {
+
+struct BwdLds {
+  int lw, fwlw, rsk, bufE, bufD, bufA, dl, total;
+};
+
+__host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX, int SY) {
+  BwdLds L;
+  int o = 0;
+  L.lw = o;    o += r4(F);
+  L.fwlw = o;  o += r4(F * D);
+  L.rsk = o;   o += MT * S * 64;
+  L.bufE = o;  o += kBM * (SX > SY ? SX : SY);  // E tile; reused as the second G buffer
+  L.bufD = o;  o += kBM * SX;                   // dE tile
+  L.bufA = o;  o += kBM * SY;                   // G buffer
+  L.dl = o;    o += kBM;
+  L.total = r4(o);
+  return L;
+}
+
+size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY) {
+  return sizeof(float) * (size_t)bwd_layout(F, D, MT, S, SX, SY).total;
+}
+
+// sum over the 16 lanes of an aligned 16-lane group
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 8);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 1);
+  return v;
+}
+
+template <int D, int TPW>
+__global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
+  constexpr int NTH = 256;
+  constexpr int NW = 4;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int F = p.F, SX = p.SX, SY = p.SY, FD = F * D;
+  const int flags = p.flags;
+  const bool deep = (flags & kHasDeep) != 0;
+  const bool second = (flags & kHasSecond) != 0;
+  const bool fwlw = (flags & kFoFwlw) != 0;
+  const bool lwp = (flags & kFoLw) != 0;
+  const bool drop = (flags & kDrop) != 0;
+  const BwdLds L = bwd_layout(F, D, p.MT, p.S, SX, SY);
+  float* lw_s = smem + L.lw;
+  float* fwlw_s = smem + L.fwlw;
+  float* rsk = smem + L.rsk;
+  float* bufE = smem + L.bufE;
+  float* bufD = smem + L.bufD;
+  float* bufA = smem + L.bufA;
+  float* bufB = bufE;  // the E tile is dead once the shallow dE is formed
+  float* dl = smem + L.dl;
+  const int64_t b0 = (int64_t)blockIdx.x * kBM;
+  const int row0 = (lane >> 4) * 4;
+
+  // ---- P0: stage --------------------------------------------------------------
+  stamp(p.stamps, 0, tid);
+  stamp_rt(p.stamps, 10, tid);
+  if (lwp)
+    for (int i = tid; i < F; i += NTH) lw_s[i] = p.lw[i];
+  if (fwlw)
+    for (int i = tid; i < FD; i += NTH) fwlw_s[i] = p.fwlw[i];
+  if (second)
+    for (int i = tid; i < p.MT * p.S * 16; i += NTH)
+      reinterpret_cast<float4*>(rsk)[i] = reinterpret_cast<const float4*>(p.rsk)[i];
+  if (tid < kBM) dl[tid] = (b0 + tid < p.batch) ? p.dlogit[b0 + tid] : 0.f;
+  for (int i = tid; i < kBM * p.W0; i += NTH) {
+    const int b = i / p.W0;
+    const int c = i - b * p.W0;
+    const int64_t row = b0 + b;
+    bufE[b * SX + c] = (second && c < FD && row < p.batch) ? p.sv_e[row * FD + c] : 0.f;
+    bufD[b * SX + c] = 0.f;
+  }
+  __syncthreads();
+  stamp(p.stamps, 1, tid);
+
+  // ---- P1: dE of the shallow part ---------------------------------------------
+  if (second) {
+    // dE[b,k,d] = dlogit_b * sum_{l != k} Rs[k,l] E[b,l,d]  (+ dfo[b,k] * Wfl[k,d] with fwlw, :344-345)
+    const int MT = p.MT, S = p.S;
+    constexpr int NTW = (D + NW - 1) / NW;
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int nt = wave + NW * j;
+        if (nt >= D) continue;  // wave-uniform
+        const int n = nt * 16 + (lane & 15);
+        const int b = n / D;
+        const int d = n - b * D;
+        const float* ecol = bufE + b * SX + d;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < S; ++s) {
+          const float av = rsk[(m * S + s) * 64 + lane];
+          const float bv = ecol[(4 * s + (lane >> 4)) * D];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * m + row0 + r;
+          if (k < F) {
+            float v = dl[b] * acc[r];
+            if (fwlw) v = fmaf(lwp ? dl[b] * lw_s[k] : dl[b], fwlw_s[k * D + d], v);
+            bufD[b * SX + k * D + d] = v;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  stamp(p.stamps, 2, tid);
+
+  // ---- P2: MLP backward (net_1_fc then net_1_linear_H .. 1, :412-428) ---------------
+  if (deep) {
+    const int H = p.H, N = p.N, NT = p.NT, NP = NT * 16;
+    const float scale = drop ? p.drop_scale : 1.f;
+    // G_H = dlogit * fc * (X_H > 0) * scale -> bufA and global
+    for (int i = tid; i < kBM * NP; i += NTH) {
+      const int b = i / NP;
+      const int n = i - b * NP;
+      const int64_t row = b0 + b;
+      const bool ok = n < N && row < p.batch;
+      const float x = ok ? p.sv_x[H][row * N + n] : 0.f;
+      const float gv = (ok && x > 0.f) ? dl[b] * p.fc[n] * scale : 0.f;
+      bufA[b * SY + n] = gv;
+      if (ok) p.sv_g[H][row * N + n] = gv;
+    }
+    __syncthreads();
+    stamp(p.stamps, 3, tid);
+
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float4*>(p.wtpack), (short)0, p.wtpack_bytes, 0x00020000);
+    LayerStream<TPW, 1> ls;
+    f32x4 wb0[TPW], wb1[TPW], wb2[TPW];
+    for (int l = H; l >= 1; --l) {
+      const bool fromA = ((H - l) & 1) == 0;
+      const float* in = fromA ? bufA : bufB;
+      float* outg = fromA ? bufB : bufA;
+      const int K = l == 1 ? FD : N;
+      const int KT = l == 1 ? p.NC0 : NT;
+      // output tiles (the layer's inputs k) in passes of 4*TPW: layer 1 may have more tiles
+      // (ceil(F*D/16)) than the hidden width the kernel's TPW was sized for
+      for (int t0 = 0; t0 < KT; t0 += 4 * TPW) {
+        ls.init(wrsrc, p.wt_off[l] + t0 * NT * 64, NT, KT - t0, wave, 0);
+        ls.preload(wb0, wb1, lane * 16);
+        // epilogue operands: the ReLU/dropout mask source X_{l-1} for this lane's outputs
+        float xm[TPW][4];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          const int t = t0 + wave + 4 * j;
+          const int k = t * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t row = b0 + row0 + r;
+            xm[j][r] = (l > 1 && t < KT && k < K && row < p.batch) ? p.sv_x[l - 1][row * N + k] : 0.f;
+          }
+        }
+        f32x4 acc[TPW];
+        mlp_k_loop<TPW, 1>(acc, in, SY, ls, wb0, wb1, wb2, lane);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          const int t = t0 + wave + 4 * j;
+          if (t >= KT) continue;  // wave-uniform
+          const int k = t * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int b = row0 + r;
+            const int64_t row = b0 + b;
+            if (l > 1) {
+              const float gv = (k < K && xm[j][r] > 0.f) ? acc[j][r] * scale : 0.f;
+              outg[b * SY + k] = gv;
+              if (k < K && row < p.batch) p.sv_g[l - 1][row * N + k] = gv;
+            } else if (k < FD) {
+              float gv = acc[j][r];
+              if (drop) gv = dropout_keep(p.seed, 0, row, k, p.drop_p) ? gv * scale : 0.f;
+              bufD[b * SX + k] += gv;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      stamp(p.stamps, 4 + (H - l < 3 ? H - l : 3), tid);
+    }
+  }
+  stamp(p.stamps, 8, tid);
+
+  // ---- P3: dE -> workspace (coalesced rows) ---------------------------------------
+  for (int i = tid; i < kBM * FD; i += NTH) {
+    const int b = i / FD;
+    const int c = i - b * FD;
+    if (b0 + b < p.batch) p.sv_de[(b0 + b) * FD + c] = bufD[b * SX + c];
+  }
+  stamp(p.stamps, 9, tid);
+  stamp_rt(p.stamps, 11, tid);
+}
+
+// ---------------------------------------------------------------------------
+// Dense shallow gradients, one 16-row tile per workgroup: the tile's rows of E, fo and X_H are
+// contiguous in the workspace, so they are staged with linear float4 loads (all in flight at once);
+// each block writes its partial sums (no atomics) and reduce_final_kernel adds the blocks.
+// ---------------------------------------------------------------------------
+constexpr int kRedMaxFD = 2048;  // F*D (64 x 32)
+constexpr int kRedMaxN = 512;
+
+struct RedLds {
+  int e, fo, xh, xv, de, total;
+};
+__host__ __device__ inline RedLds red_layout(int F, int D, int N, int num) {
+  RedLds L;
+  int o = 0;
+  L.e = o;   o += r4(kBM * F * D);  // rows packed (stride F*D), as in the workspace
+  L.fo = o;  o += r4(kBM * F);
+  L.xh = o;  o += r4(kBM * N);
+  L.xv = o;  o += r4(kBM * (num > 0 ? num : 1));
+  L.de = o;  o += r4(kBM * (num > 0 ? num * D : 1));
+  L.total = r4(o);
+  return L;
+}
+
+// copy n contiguous floats (16-byte aligned source and destination offsets) global -> LDS, zero-filling
+// [n, ncap); U float4 per thread in flight
+template <int U>
+__device__ __forceinline__ void stage_linear(float* __restrict__ dst, const float* __restrict__ src, int n, int ncap,
+                                             int tid) {
+  const int n4 = ncap >> 2;
+  for (int q0 = tid; q0 < n4; q0 += 256 * U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * 256;
+      const int e = q * 4;
+      if (q < n4 && e + 3 < n) {
+        v[u] = *reinterpret_cast<const float4*>(src + e);
+      } else {
+        v[u].x = (q < n4 && e < n) ? src[e] : 0.f;
+        v[u].y = (q < n4 && e + 1 < n) ? src[e + 1] : 0.f;
+        v[u].z = (q < n4 && e + 2 < n) ? src[e + 2] : 0.f;
+        v[u].w = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * 256;
+      if (q < n4) *reinterpret_cast<float4*>(dst + q * 4) = v[u];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
+  constexpr int NTH = 256;
+  constexpr int KF = kRedMaxFD / NTH;  // per-thread E columns
+  constexpr int KN = kRedMaxN / NTH;   // per-thread hidden units
+  __shared__ float dl[kBM];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int F = a.F, D = a.D, FD = F * D, num = a.num, N = a.N, numD = num * D;
+  const RedLds L = red_layout(F, D, N, num);
+  float* es = sm + L.e;
+  float* fos = sm + L.fo;
+  float* xhs = sm + L.xh;
+  float* xvs = sm + L.xv;
+  float* des = sm + L.de;
+  const int64_t rb = (int64_t)blockIdx.x * kBM;
+  const int nt = (int)((a.batch - rb) < kBM ? (a.batch - rb) : kBM);
+  const bool lwp = (a.flags & kFoLw) != 0;
+  const bool need_e = a.g_fwlw || a.g_R;
+  const bool need_num2 = numD > 0 && a.sv_de != nullptr;
+  if (tid < kBM) dl[tid] = tid < nt ? a.dlogit[rb + tid] : 0.f;
+  if (need_e) stage_linear<8>(es, a.sv_e + rb * FD, nt * FD, r4(kBM * FD), tid);
+  if (a.g_lw) stage_linear<2>(fos, a.sv_fo + rb * F, nt * F, r4(kBM * F), tid);
+  if (a.g_fc) stage_linear<8>(xhs, a.x_h + rb * N, nt * N, r4(kBM * N), tid);
+  if (num > 0)
+    for (int i = tid; i < kBM * num; i += NTH) {
+      const int b = i / num, c = i - b * num;
+      xvs[i] = b < nt ? a.xv[(rb + b) * a.xv_stride + c] : 0.f;
+    }
+  if (need_num2)
+#pragma unroll 4
+    for (int i = tid; i < kBM * numD; i += NTH) {
+      const int b = i / numD, c = i - b * numD;
+      des[i] = b < nt ? a.sv_de[(rb + b) * FD + c] : 0.f;
+    }
+  __syncthreads();
+
+  float* out = a.part + (size_t)blockIdx.x * red_outputs(F, D, N, num);
+  float* o_lw = out + 1;
+  float* o_fw = o_lw + F;
+  float* o_R = o_fw + FD;
+  float* o_fc = o_R + F * F;
+  float* o_n2 = o_fc + N;
+  float* o_n1 = o_n2 + numD;
+  // bias (total_sum += self.bias, :458)
+  if (tid < kBM) {
+    const float v = sum16(dl[tid]);
+    if (tid == 0) out[0] = v;
+  }
+  // fm_1st: first = fo . w_lw (:450)
+  if (tid < F) {
+    float s = 0.f;
+    if (a.g_lw)
+#pragma unroll
+      for (int b = 0; b < kBM; ++b) s = fmaf(dl[b], fos[b * F + tid], s);
+    o_lw[tid] = s;
+  }
+  // fwfm_linear: fo[b,f] = <E[b,f,:], Wfl[f,:]> (:344-345); dfo's lw[f] factor is applied by the final sum
+#pragma unroll
+  for (int j = 0; j < KF; ++j) {
+    const int i = tid + j * NTH;
+    if (i < FD) {
+      float s = 0.f;
+      if (a.g_fwlw)
+#pragma unroll
+        for (int b = 0; b < kBM; ++b) s = fmaf(dl[b], es[b * FD + i], s);
+      o_fw[i] = s;
+    }
+  }
+  // numerical fields: E_f = v_f * Xv_f, fo_f = w1_f * Xv_f (:297-299, :304, :334)
+  for (int i = tid; i < numD; i += NTH) {
+    const int f = i / D;
+    float s = 0.f;
+    if (need_num2)
+#pragma unroll
+      for (int b = 0; b < kBM; ++b) s = fmaf(des[b * numD + i], xvs[b * num + f], s);
+    o_n2[i] = s;
+  }
+  if (tid < num) {
+    float s = 0.f;
+#pragma unroll
+    for (int b = 0; b < kBM; ++b) s = fmaf(dl[b], xvs[b * num + tid], s);
+    o_n1[tid] = s;
+  }
+  // net_1_fc: deep = X_H . w_fc (:428-436)
+#pragma unroll
+  for (int j = 0; j < KN; ++j) {
+    const int n = tid + j * NTH;
+    if (n < N) {
+      float s = 0.f;
+      if (a.g_fc)
+#pragma unroll
+        for (int b = 0; b < kBM; ++b) s = fmaf(dl[b], xhs[b * N + n], s);
+      o_fc[n] = s;
+    }
+  }
+  // field_cov: d W[k,l] = 0.5 * sum_b dlogit_b <E_bk, E_bl>, k != l (:363-367): a Gram matrix on MFMA,
+  // contraction over (b, d)
+  if (a.g_R) {
+    const int MT = a.MT, ntile = MT * MT;
+    const int steps = (kBM * D) / 4;
+    for (int t = wave; t < ntile; t += 4) {
+      const int mk = t / MT, ml = t - mk * MT;
+      const int kA = 16 * mk + (lane & 15);
+      const int lB = 16 * ml + (lane & 15);
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < steps; ++s) {
+        const int n = 4 * s + (lane >> 4);
+        const int b = n / D;
+        const int d = n - b * D;
+        const float av = kA < F ? dl[b] * es[b * FD + kA * D + d] : 0.f;
+        const float bv = lB < F ? es[b * FD + lB * D + d] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * mk + (lane >> 4) * 4 + r;
+        if (k < F && lB < F) o_R[k * F + lB] = k != lB ? 0.5f * acc[r] : 0.f;
+      }
+    }
+  }
+}
+
+// Sum of the per-block partials, added into the grads (accumulate, like autograd): 64 outputs per
+// workgroup, each wave sums a quarter of the blocks (8 loads in flight per lane), then the four
+// quarters are combined in a fixed order (deterministic).
+__global__ void __launch_bounds__(256) reduce_final_kernel(RedArgs a, int nblk) {
+  __shared__ float q4[4][64];
+  const int F = a.F, D = a.D, N = a.N, num = a.num, FD = F * D, numD = num * D;
+  const int P = red_outputs(F, D, N, num);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lane;
+  const int per = (nblk + 3) / 4;
+  const int b0 = wave * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+  float s = 0.f;
+  if (o < P) {
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = a.part[(size_t)(b + u) * P + o];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < b1; ++b) s += a.part[(size_t)b * P + o];
+  }
+  q4[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || o >= P) return;
+  s = ((q4[0][lane] + q4[1][lane]) + q4[2][lane]) + q4[3][lane];
+  const bool lwp = (a.flags & kFoLw) != 0;
+  float* dst = nullptr;
+  float scale = 1.f;
+  int i = o;
+  if (i < 1) {
+    dst = a.g_bias;
+  } else if ((i -= 1) < F) {
+    dst = a.g_lw ? a.g_lw + i : nullptr;
+  } else if ((i -= F) < FD) {
+    dst = a.g_fwlw ? a.g_fwlw + i : nullptr;
+    if (lwp) scale = a.lw[i / D];
+  } else if ((i -= FD) < F * F) {
+    dst = a.g_R ? a.g_R + i : nullptr;
+  } else if ((i -= F * F) < N) {
+    dst = a.g_fc ? a.g_fc + i : nullptr;
+  } else if ((i -= N) < numD) {
+    dst = a.g_num2[i / D] ? a.g_num2[i / D] + i % D : nullptr;
+  } else {
+    i -= numD;
+    dst = a.g_num1[i];
+    if (lwp) scale = a.lw[i];
+  }
+  if (dst) *dst += s * scale;
+}
+
+// ---------------------------------------------------------------------------
+// Categorical-table scatter (reference nn.Embedding / EmbeddingBag / QREmbeddingBag backward with
+// dense grads).  Each workgroup takes a.chunk samples of one task.  PRIV (small tables): the chunk
+// accumulates in an LDS copy of the table, then each touched row is added to the grad once (so an
+// address sees at most one atomic per chunk even when every sample hits it); else one sample per
+// lane with global atomics.
+// ---------------------------------------------------------------------------
+template <bool PRIV>
+__global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
+  constexpr int SPT = 4;  // samples per thread
+  extern __shared__ __attribute__((aligned(16))) float acc[];
+  const int tid = threadIdx.x;
+  int lo = 0, hi = a.ntasks - 1;
+  const int bid = blockIdx.x;
+  while (lo < hi) {  // last task whose block0 <= bid
+    const int mid = (lo + hi + 1) >> 1;
+    if (a.t[mid].block0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const ScatterTask T = a.t[lo];
+  const FieldDev fd = a.fields[T.field];
+  const int f = T.field, D = a.D, FD = a.F * D, w = T.src == 0 ? D : 1;
+  const int col = f - a.num;
+  const float lwf = a.lw ? a.lw[f] : 1.f;
+  const int64_t s0 = (int64_t)(bid - T.block0) * a.chunk;
+  // row of sample b in this task's table, and the partner-table row (QR)
+  auto locate = [&](int64_t b, int64_t& row, int64_t& part) {
+    int64_t idx = a.xi[b * a.xi_stride + col];
+    if (idx < 0 || idx >= fd.n) idx = 0;  // the forward clamped (and flagged) it the same way
+    row = idx;
+    part = 0;
+    if (T.kind == 1) {
+      row = idx / T.c;
+      part = idx - row * T.c;
+    } else if (T.kind == 2) {
+      part = idx / T.c;
+      row = idx - part * T.c;
+    }
+  };
+  auto value = [&](int64_t b, int64_t part, int d) -> float {
+    float v = T.src == 1 ? a.dlogit[b] * lwf : a.sv_de[b * FD + f * D + d];
+    if (T.other) v *= T.other[T.src == 1 ? part : part * D + d];
+    return v;
+  };
+  if constexpr (PRIV) {
+    int* flag = reinterpret_cast<int*>(acc + T.rows * w);
+    const int n = T.rows * (w + 1);
+    for (int i = tid; i < n; i += 256) acc[i] = 0.f;  // acc and flags
+    int64_t rows[SPT];
+    int64_t parts[SPT];
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      const int64_t b = s0 + tid + k * 256;
+      rows[k] = -1;
+      if (tid + k * 256 < a.chunk && b < a.batch) locate(b, rows[k], parts[k]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      if (rows[k] < 0) continue;
+      const int64_t b = s0 + tid + k * 256;
+      for (int d = 0; d < w; ++d) atomicAdd(&acc[rows[k] * w + d], value(b, parts[k], d));
+      flag[rows[k]] = 1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      if (rows[k] < 0) continue;
+      if (atomicExch(&flag[rows[k]], 0) == 1)  // first sample of this row in the chunk flushes it
+        for (int d = 0; d < w; ++d) atomicAdd(T.g + rows[k] * w + d, acc[rows[k] * w + d]);
+    }
+  } else {
+    const int64_t b = s0 + tid;
+    if (tid < a.chunk && b < a.batch) {
+      int64_t row, part;
+      locate(b, row, part);
+      for (int d = 0; d < w; ++d) atomicAdd(T.g + row * w + d, value(b, part, d));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dW_l += G_l^T X_{l-1}: workgroup = 64 (n) x 64 (k) block of one layer over one batch split;
+// wave w owns n rows 16w..16w+15 and the 4 k tiles.  32-row chunks of G and X are staged in LDS,
+// the next chunk's global loads in registers while the current chunk's MFMAs run.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
+  __shared__ __attribute__((aligned(16))) float gs[32][64 + 4];
+  __shared__ __attribute__((aligned(16))) float xs[32][64 + 4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  int bid = blockIdx.x;
+  int l = 1;
+  while (l < a.H && bid >= a.blk0[l + 1]) ++l;
+  bid -= a.blk0[l];
+  const int per_layer_blocks = a.nnb * a.nkb[l];
+  const int split = bid / per_layer_blocks;
+  const int rem = bid - split * per_layer_blocks;
+  const int nb = rem / a.nkb[l];
+  const int kb = rem - nb * a.nkb[l];
+  const int N = a.N, K = a.K[l];
+  const int n0 = nb * 64, k0 = kb * 64;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > a.batch) r_end = a.batch;
+  const float* G = a.G[l];
+  const float* X = a.X[l];
+  const int ldx = a.ldx[l];
+
+  // staging map: 32 rows x 64 cols = 512 float4 per operand, 2 per thread
+  float4 pg[2], px[2];
+  auto fetch = [&](int64_t rbase) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 256;
+      const int rr = i >> 4;
+      const int c4 = (i & 15) * 4;
+      const int64_t row = rbase + rr;
+      float4 vg = make_float4(0.f, 0.f, 0.f, 0.f), vx = vg;
+      if (row < r_end) {
+        const float* gp = G + row * N + n0 + c4;
+        const float* xp = X + row * ldx + k0 + c4;
+        if (n0 + c4 + 3 < N) vg = *reinterpret_cast<const float4*>(gp);
+        else {
+          vg.x = n0 + c4 < N ? gp[0] : 0.f; vg.y = n0 + c4 + 1 < N ? gp[1] : 0.f;
+          vg.z = n0 + c4 + 2 < N ? gp[2] : 0.f; vg.w = 0.f;
+        }
+        if (k0 + c4 + 3 < K) vx = *reinterpret_cast<const float4*>(xp);
+        else {
+          vx.x = k0 + c4 < K ? xp[0] : 0.f; vx.y = k0 + c4 + 1 < K ? xp[1] : 0.f;
+          vx.z = k0 + c4 + 2 < K ? xp[2] : 0.f; vx.w = 0.f;
+        }
+      }
+      pg[u] = vg;
+      px[u] = vx;
+    }
+  };
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float* gB = kb == 0 ? a.gB[l] : nullptr;  // db_l = sum_b G_l[b, :] rides on the k-block-0 workgroups
+  float bsum = 0.f;
+  fetch(r_begin);
+  for (int64_t rb = r_begin; rb < r_end; rb += 32) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 256;
+      *reinterpret_cast<float4*>(&gs[i >> 4][(i & 15) * 4]) = pg[u];
+      *reinterpret_cast<float4*>(&xs[i >> 4][(i & 15) * 4]) = px[u];
+    }
+    __syncthreads();
+    if (rb + 32 < r_end) fetch(rb + 32);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int rr = 4 * s + (lane >> 4);
+      const float av = gs[rr][16 * wave + (lane & 15)];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xs[rr][16 * t + (lane & 15)], acc[t], 0, 0, 0);
+    }
+    if (gB && tid < 64)
+#pragma unroll 8
+      for (int rr = 0; rr < 32; ++rr) bsum += gs[rr][tid];
+    __syncthreads();
+  }
+  if (gB && tid < 64 && n0 + tid < N) atomicAdd(gB + n0 + tid, bsum);
+  float* gW = a.gW[l];
+  if (!gW) return;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int k = k0 + 16 * t + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 16 * wave + (lane >> 4) * 4 + r;
+      if (n < N && k < K) atomicAdd(gW + (int64_t)n * K + k, acc[t][r]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Adam (torch.optim.Adam, single-tensor form, torch/optim/adam.py _single_tensor_adam):
+// g += wd * p; m = lerp(m, g, 1 - b1);
+// v = v * b2 + (1 - b2) * g * g; p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) adam_kernel(const AdamList list, float step_size, float omb1, float b2,
+                                                   float omb2, float eps, float wd, float bc2_sqrt) {
+  int lo = 0, hi = list.n - 1;
+  const int bid = blockIdx.x;
+  while (lo < hi) {  // last tensor whose block0 <= bid
+    const int mid = (lo + hi + 1) >> 1;
+    if (list.t[mid].block0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const AdamTensor T = list.t[lo];
+  const int64_t i0 = (int64_t)(bid - T.block0) * 1024;
+  // torch's CPU kernels' evaluation order: fmadd where ATen's vector path uses one, every other
+  // product / sum rounded on its own
+  for (int64_t i = i0 + threadIdx.x; i < i0 + 1024 && i < T.n; i += 256) {
+    const float pv = T.p[i];
+    float g = T.g[i];
+    if (wd != 0.f) g = fmaf(wd, pv, g);                        // grad.add(param, alpha=wd): ATen's fmadd
+    float m = T.m[i];
+    m = fmaf(omb1, __fsub_rn(g, m), m);                         // exp_avg.lerp_(grad, 1-b1): fmadd, w < 0.5
+    float v = __fmul_rn(T.v[i], b2);                                             // exp_avg_sq.mul_(b2)
+    v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));                         //   .addcmul_(g, g, 1-b2)
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), eps);     // sqrt(v)/sqrt(bc2) + eps
+    T.m[i] = m;
+    T.v[i] = v;
+    T.p[i] = __fadd_rn(pv, __fdiv_rn(__fmul_rn(-step_size, m), denom));          // addcdiv_(m, denom, -lr/bc1)
+  }
+}
+
+// transposed fragment pack for the backward: outputs = the layer's inputs k, contraction = n
+// out[(t*NTc + c)*64 + lane][s] = W[n = 16c + 4(lane>>4) + s][k = 16t + (lane&15)]
+__global__ void pack_linear_t_kernel(const float* __restrict__ w, int N, int K, int KT, int NTc,
+                                     float4* __restrict__ out) {
+  const int64_t total = (int64_t)KT * NTc * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    const int64_t tc = i >> 6;
+    const int c = (int)(tc % NTc);
+    const int t = (int)(tc / NTc);
+    const int k = t * 16 + (lane & 15);
+    const int n0 = 16 * c + 4 * (lane >> 4);
+    float v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int n = n0 + s;
+      v[s] = (n < N && k < K) ? w[(int64_t)n * K + k] : 0.f;
+    }
+    out[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// symmetric off-diagonal (R + R^T)/2 (FM: ones) in the FwFM A-fragment order
+__global__ void pack_fwfm_sym_kernel(const float* __restrict__ R, int F, int mode, int MT, int S,
+                                     float* __restrict__ out) {
+  const int total = MT * S * 64;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int lane = i & 63;
+    const int ms = i >> 6;
+    const int s = ms % S;
+    const int m = ms / S;
+    const int k = 16 * m + (lane & 15);
+    const int l = 4 * s + (lane >> 4);
+    float u = 0.f;
+    if (k < F && l < F && l != k) u = (mode == 1) ? 1.f : (R[l * F + k] + R[k * F + l]) * 0.5f;
+    out[i] = u;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <int D, int TPW>
+static hipError_t launch_bwd_t(const BwdArgs& a, size_t lds, hipStream_t s) {
+  auto k = bwd_kernel<D, TPW>;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+template <int D>
+static hipError_t launch_bwd_d(const BwdArgs& a, int tpw, size_t lds, hipStream_t s) {
+  switch (tpw) {
+    case 1: return launch_bwd_t<D, 1>(a, lds, s);
+    case 2: return launch_bwd_t<D, 2>(a, lds, s);
+    case 3: return launch_bwd_t<D, 3>(a, lds, s);
+    case 4: return launch_bwd_t<D, 4>(a, lds, s);
+    case 5: return launch_bwd_t<D, 5>(a, lds, s);
+    case 6: return launch_bwd_t<D, 6>(a, lds, s);
+    case 7: return launch_bwd_t<D, 7>(a, lds, s);
+    case 8: return launch_bwd_t<D, 8>(a, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_backward(const BwdArgs& a, int D, int tpw, size_t lds, hipStream_t s) {
+  switch (D) {
+    case 4: return launch_bwd_d<4>(a, tpw, lds, s);
+    case 8: return launch_bwd_d<8>(a, tpw, lds, s);
+    case 10: return launch_bwd_d<10>(a, tpw, lds, s);
+    case 16: return launch_bwd_d<16>(a, tpw, lds, s);
+    case 32: return launch_bwd_d<32>(a, tpw, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_reduce(const RedArgs& a, hipStream_t s) {
+  if (a.batch <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
+  if (a.F * a.D > kRedMaxFD || a.N > kRedMaxN || a.num * a.D > 512) return hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * (size_t)red_layout(a.F, a.D, a.N, a.num).total;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(reduce_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(reduce_kernel, dim3(grid), dim3(256), lds, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int P = red_outputs(a.F, a.D, a.N, a.num);
+  hipLaunchKernelGGL(reduce_final_kernel, dim3((P + 63) / 64), dim3(256), 0, s, a, (int)grid);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s) {
+  if (total_blocks <= 0 || a.ntasks <= 0) return hipSuccess;
+  if (a.chunk > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scatter_kernel<false>, dim3(total_blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s) {
+  if (total_blocks <= 0 || a.ntasks <= 0) return hipSuccess;
+  if (a.chunk > 4 * 256) return hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * kPrivFloats;
+  auto k = scatter_kernel<true>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3(total_blocks), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
+  if (total_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dw_kernel, dim3(total_blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
+                       float eps, float wd, float bc2_sqrt, hipStream_t s) {
+  if (total_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(adam_kernel, dim3(total_blocks), dim3(256), 0, s, list, step_size, omb1, b2, omb2, eps, wd,
+                     bc2_sqrt);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_linear_t(const float* w, int N, int K, int KT, int NTc, float4* out, hipStream_t s) {
+  const int64_t total = (int64_t)KT * NTc * 64;
+  const unsigned grid = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(pack_linear_t_kernel, dim3(grid), dim3(256), 0, s, w, N, K, KT, NTc, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_fwfm_sym(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s) {
+  const int total = MT * S * 64;
+  hipLaunchKernelGGL(pack_fwfm_sym_kernel, dim3((total + 255) / 256), dim3(256), 0, s, R, F, mode, MT, S, out);
+  return hipGetLastError();
+}
+
+}  // namespace dfwfm

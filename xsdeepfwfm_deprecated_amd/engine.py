@@ -8,6 +8,9 @@ it in sync with a DeepFMs module's parameters.
   fragment layout on the current stream whenever any of them changes
   (tracked with the tensors' in-place version counters), e.g. after every
   optimizer step -- never per forward otherwise.
+* Training: ``train_forward`` keeps the activations in engine-owned device
+  memory and ``backward`` consumes them; every train forward gets a token and a
+  backward for a stale token raises (one forward/backward pair at a time).
 """
 from __future__ import annotations
 
@@ -112,8 +115,53 @@ class ForwardEngine:
         _lib.check(rc, "dfwfm_forward")
         return out
 
+    # -- training step -------------------------------------------------------
+    def train_forward(self, xi, xv, out, dropout_p: float, seed: int) -> int:
+        """Forward of a training step; returns the token the matching backward must present."""
+        B = xi.shape[0]
+        ncat = self.cfg["field_size"] - self.cfg["numerical"]
+        xs = xi.stride(0) if ncat > 0 else 0
+        vs = xv.stride(0) if self.cfg["numerical"] > 0 else 0
+        rc = _lib.lib().dfwfm_train_forward(self.handle, ctypes.c_void_p(xi.data_ptr()), xs,
+                                            ctypes.c_void_p(xv.data_ptr()), vs, B, ctypes.c_void_p(out.data_ptr()),
+                                            float(dropout_p), int(seed) & 0xFFFFFFFF, _stream_handle(self.device))
+        _lib.check(rc, "dfwfm_train_forward")
+        self._token = getattr(self, "_token", 0) + 1
+        return self._token
+
+    def backward(self, token: int, dlogit, field_grads, dense):
+        """field_grads: per field (emb2, emb2_r, emb1, emb1_r) grad tensors or None; dense: dict of
+        field_cov, fwfm_lin, fm_1st, bias, fc_w (tensor or None), lin_w / lin_b (lists)."""
+        if token != getattr(self, "_token", None):
+            raise RuntimeError("dfwfm: backward of a stale training forward (another train forward ran in "
+                               "between; one forward/backward pair at a time)")
+        fg = (_lib.dfwfm_field_grads * len(field_grads))()
+        for i, tup in enumerate(field_grads):
+            fg[i] = _lib.dfwfm_field_grads(*[None if t is None else t.data_ptr() for t in tup])
+        lw, lb = dense.get("lin_w") or [], dense.get("lin_b") or []
+        W = (ctypes.c_void_p * max(len(lw), 1))(*[None if t is None else t.data_ptr() for t in lw])
+        Bv = (ctypes.c_void_p * max(len(lb), 1))(*[None if t is None else t.data_ptr() for t in lb])
+        g = _lib.dfwfm_grads(fg, *[None if dense.get(k) is None else dense[k].data_ptr()
+                                   for k in ("field_cov", "fwfm_lin", "fm_1st", "bias")],
+                             W if lw else None, Bv if lb else None,
+                             None if dense.get("fc_w") is None else dense["fc_w"].data_ptr())
+        _lib.check(_lib.lib().dfwfm_backward(self.handle, ctypes.c_void_p(dlogit.data_ptr()), ctypes.byref(g),
+                                             _stream_handle(self.device)), "dfwfm_backward")
+
     def read_error_flag(self) -> int:
         v = ctypes.c_int32(0)
         _lib.check(_lib.lib().dfwfm_read_error_flag(self.handle, ctypes.byref(v), _stream_handle(self.device)),
                    "dfwfm_read_error_flag")
         return int(v.value)
+
+
+def adam_step(entries, lr, beta1, beta2, eps, weight_decay, step, device):
+    """One torch.optim.Adam step over [(param, grad, exp_avg, exp_avg_sq)] (float32, contiguous, on
+    `device`) on the current stream; no model handle needed."""
+    arr = (_lib.dfwfm_adam_tensor * max(len(entries), 1))()
+    for i, (p, g, m, v) in enumerate(entries):
+        arr[i] = _lib.dfwfm_adam_tensor(p.data_ptr(), None if g is None else g.data_ptr(), m.data_ptr(),
+                                        v.data_ptr(), p.numel())
+    _lib.check(_lib.lib().dfwfm_adam_step(arr, len(entries), float(lr), float(beta1), float(beta2), float(eps),
+                                          float(weight_decay), int(step), _stream_handle(device)),
+               "dfwfm_adam_step")

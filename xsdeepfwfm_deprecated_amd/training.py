@@ -1,30 +1,135 @@
-"""Training path of DeepFMs (reference model/DeepFMs.py:497-748, 807-823).
+"""Training path of DeepFMs (reference model/DeepFMs.py:497-748, 807-823) on the HIP kernels.
 
-The forward of a training step is the same fused HIP kernel; gradients come
-from the HIP backward kernels (see csrc/).  Until those land, requesting a
-gradient raises instead of silently falling back to PyTorch ops.
+* ``train_forward``: an autograd Function whose forward is the fused HIP forward in training mode
+  (activations kept, deep-tower dropout from a counter hash) and whose backward is the fused HIP
+  backward (csrc/dfwfm_train.hip) writing every parameter's gradient -- dense, like the
+  reference's ``nn.Embedding(sparse=False)`` -- into one flat per-step buffer.
+* ``Adam``: ``torch.optim.Adam`` (coupled L2, bias correction) as one HIP kernel per <= 40 tensors,
+  same defaults and ``state_dict`` layout.
+* ``fit``: the reference's epoch loop -- init_weights, optimizer, BCE-with-logits (or the KD loss),
+  magnitude pruning, per-epoch eval, shuffle, save, early stopping -- with the training set
+  resident in HBM and, under ``torch.distributed``, data parallelism: each rank takes its slice of
+  every global batch and the flat gradient buffer is all-reduced (RCCL) before the step.
+
+Nothing here computes on the CPU: without the HIP library every entry point raises.
 """
 from __future__ import annotations
 
+import logging
+import math
+from time import time
+
+import numpy as np
 import torch
+import torch.nn.functional as F
+
+from . import engine as _engine
 
 
-class _FusedForward(torch.autograd.Function):
+# --------------------------------------------------------------------------------------- autograd
+class _TrainForward(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, eng, xi, xv, *params):
-        return eng.forward(xi, xv)
+    def forward(ctx, model, eng, xi, xv, dropout_p, seed, *params):
+        out = torch.empty(xi.shape[0], dtype=torch.float32, device=eng.device)
+        ctx.token = eng.train_forward(xi, xv, out, dropout_p, seed)
+        ctx.model, ctx.eng = model, eng
+        ctx.inputs = (xi, xv)  # the backward kernel re-reads the indices
+        ctx.params = params
+        return out
 
     @staticmethod
     def backward(ctx, grad_out):
-        raise NotImplementedError("dfwfm: the HIP backward kernels are not built yet; run the forward "
-                                  "under torch.no_grad()")
+        model, eng, params = ctx.model, ctx.eng, ctx.params
+        need = ctx.needs_input_grad[6:]
+        flat, views = _grad_buffer(params, need, eng.device)
+        by_id = {id(p): g for p, g in zip(params, views)}
+        fields, dense = model._param_layout()
+        fg = [tuple(None if t is None else by_id.get(id(t)) for t in tup) for tup in fields]
+        dg = {k: (None if v is None else by_id.get(id(v))) for k, v in dense.items() if not isinstance(v, list)}
+        dg["lin_w"] = [by_id.get(id(t)) for t in dense["lin_w"]]
+        dg["lin_b"] = [by_id.get(id(t)) for t in dense["lin_b"]]
+        eng.backward(ctx.token, grad_out.contiguous(), fg, dg)
+        model._grad_flat = flat
+        return (None,) * 6 + tuple(views)
+
+
+def _grad_buffer(params, need, device):
+    """One zeroed flat buffer holding every needed gradient (a single memset and, under data
+    parallelism, a single all-reduce); returns it and per-parameter views (None where not needed)."""
+    sizes = [p.numel() if n else 0 for p, n in zip(params, need)]
+    flat = torch.zeros(sum(sizes), dtype=torch.float32, device=device)
+    views, off = [], 0
+    for p, n, sz in zip(params, need, sizes):
+        views.append(flat[off:off + sz].view_as(p) if n else None)
+        off += sz
+    return flat, views
 
 
 def train_forward(model, eng, xi, xv):
-    params = [p for p in model.parameters() if p.requires_grad]
-    return _FusedForward.apply(eng, xi, xv, *params)
+    """Logits with a HIP backward attached (reference forward in training mode, :285-469)."""
+    if model.training and model.is_shallow_dropout and model.dropout_shallow and \
+            any(float(p) != 0.0 for p in model.dropout_shallow[:2]):
+        raise NotImplementedError("dfwfm: shallow dropout p > 0 is not supported (the reference default is 0)")
+    p = 0.0
+    if model.training and model.use_deep and model.is_deep_dropout:
+        p = float(model.dropout_deep[0])
+        if any(float(d) != p for d in model.dropout_deep):
+            raise NotImplementedError("dfwfm: per-layer dropout rates must be equal")
+    seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+    params = [q for q in model.parameters() if q.requires_grad]
+    return _TrainForward.apply(model, eng, xi, xv, p, seed, *params)
 
 
+# --------------------------------------------------------------------------------------- Adam
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False, maximize=False) with the update on the HIP kernel.
+
+    Same hyper-parameters, same per-parameter state (``step``, ``exp_avg``, ``exp_avg_sq``), so a
+    ``state_dict`` moves between this and torch's Adam.  Parameters must be float32 HIP tensors."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if lr < 0.0 or eps < 0.0 or weight_decay < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError("invalid Adam hyper-parameter")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                                      amsgrad=False, maximize=False, foreach=None, capturable=False,
+                                      differentiable=False, fused=None))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            if group.get("amsgrad") or group.get("maximize"):
+                raise NotImplementedError("dfwfm Adam: amsgrad / maximize")
+            by_step = {}
+            device = None
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("dfwfm Adam: sparse gradients are not supported")
+                if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous():
+                    raise RuntimeError("dfwfm Adam: parameters must be contiguous float32 HIP tensors")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                by_step.setdefault(int(st["step"].item()), []).append((p, g, st["exp_avg"], st["exp_avg_sq"]))
+                device = p.device
+            b1, b2 = group["betas"]
+            for step, entries in by_step.items():
+                _engine.adam_step(entries, group["lr"], b1, b2, group["eps"], group["weight_decay"], step, device)
+                for p, *_ in entries:
+                    torch.autograd.graph.increment_version(p)  # in-place update behind torch's back
+        return loss
+
+
+# --------------------------------------------------------------------------------------- pruning
 def binary_search_threshold(param, target_percent, total_no):
     """Magnitude threshold hitting a target sparsity by bisection (reference :807-823)."""
     lo, hi = 0.0, 1e2
@@ -43,5 +148,219 @@ def binary_search_threshold(param, target_percent, total_no):
     return mid
 
 
-def fit(model, *args, **kwargs):
-    raise NotImplementedError("dfwfm: training (fit) needs the HIP backward kernels (next milestone)")
+def prune_step(model, adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb_corr):
+    """The reference's in-loop magnitude pruning (:647-673)."""
+    with torch.no_grad():
+        emb_threshold = None
+        if prune_fm != 0:
+            stacked = torch.cat([p.data for n, p in model.named_parameters() if "fm_2nd_embeddings" in n], 0)
+            emb_threshold = model.binary_search_threshold(stacked, adaptive_sparse * emb_r, stacked.numel())
+        for name, param in model.named_parameters():
+            if "fm_2nd_embeddings" in name and prune_fm != 0:
+                param.data[param.data.abs() < emb_threshold] = 0
+            if "linear" in name and "weight" in name and prune_deep != 0:
+                thr = model.binary_search_threshold(param.data, adaptive_sparse, param.numel())
+                param.data[param.data.abs() < thr] = 0
+            if name == "field_cov.weight" and prune_r != 0:
+                symm = 0.5 * (param.data + param.data.t())
+                thr = model.binary_search_threshold(symm, adaptive_sparse * emb_corr, param.numel())
+                param.data[symm.abs() < thr] = 0
+
+
+# --------------------------------------------------------------------------------------- fit
+def _dist():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist
+    return None
+
+
+def allreduce_grads(model):
+    """Sum the gradients over ranks (the loss is already normalised by the global batch): one
+    all-reduce of the flat buffer the backward filled when every grad still lives in it."""
+    dist = _dist()
+    if dist is None:
+        return
+    params = [p for p in model.parameters() if p.grad is not None]
+    flat = getattr(model, "_grad_flat", None)
+    if flat is not None and params:
+        lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * 4
+        if all(lo <= p.grad.data_ptr() < hi for p in params):
+            dist.all_reduce(flat)
+            return
+    grads = [p.grad for p in params]
+    buf = torch._utils._flatten_dense_tensors(grads)
+    dist.all_reduce(buf)
+    for g, r in zip(grads, torch._utils._unflatten_dense_tensors(buf, grads)):
+        g.copy_(r)
+
+
+def make_optimizer(model):
+    """Reference :553-561: SGD(momentum) unless adam / rmsp / adag; adam runs on the HIP kernel."""
+    if model.optimizer_type == "adam":
+        return Adam(model.parameters(), lr=model.learning_rate, weight_decay=model.weight_decay)
+    if model.optimizer_type == "rmsp":
+        return torch.optim.RMSprop(model.parameters(), lr=model.learning_rate, weight_decay=model.weight_decay)
+    if model.optimizer_type == "adag":
+        return torch.optim.Adagrad(model.parameters(), lr=model.learning_rate, weight_decay=model.weight_decay)
+    return torch.optim.SGD(model.parameters(), lr=model.learning_rate, momentum=model.momentum,
+                           weight_decay=model.weight_decay)
+
+
+def _param_summary(model, log, nonzero=False):
+    tot = e1 = e2 = dnn = 0
+    nz_r = 0
+    for name, p in model.named_parameters():
+        c = int((p != 0).sum().item()) if nonzero else p.numel()
+        tot += c
+        if "1st_embeddings" in name:
+            e1 += c
+        if "2nd_embeddings" in name:
+            e2 += c
+        if "linear_" in name:
+            dnn += c
+        if name == "field_cov.weight":
+            nz_r = int((0.5 * (p.data + p.data.t()) != 0).sum().item())
+    return tot, e1, e2, dnn, nz_r
+
+
+def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_valid=None, early_stopping=False,
+        refit=False, save_path=None, prune=0, prune_fm=0, prune_r=0, prune_deep=0, emb_r=1., emb_corr=1.,
+        teacher_model=None):
+    """Reference DeepFMs.fit (:497-748).  ``model.batch_size`` is the per-rank batch; under
+    torch.distributed every global batch of world * batch_size rows is split over the ranks."""
+    log = model.logger
+    device = model._device()
+    if device.type != "cuda":
+        from ._lib import DfwfmError
+        raise DfwfmError("fit runs only on a HIP device (no CPU fallback): move the module with .cuda() first")
+    dist = _dist()
+    rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+    ncat = model.field_size - model.num
+    Xi_train = np.asarray(Xi_train).reshape((-1, ncat, 1))
+    Xv_train = np.asarray(Xv_train)
+    y_train = np.asarray(y_train)
+    x_size = Xi_train.shape[0]
+    is_valid = Xi_valid is not None and len(Xi_valid) > 0
+    if is_valid:
+        Xi_valid = np.asarray(Xi_valid).reshape((-1, ncat, 1))
+        Xv_valid = np.asarray(Xv_valid)
+        y_valid = np.asarray(y_valid)
+        x_valid_size = Xi_valid.shape[0]
+
+    log.info("init_weights")
+    model.init_weights()
+    if dist:  # every rank starts from rank 0's weights
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    model.train()
+    optimizer = make_optimizer(model)
+    num_total, e1, e2, dnn, nz_r = _param_summary(model, log)
+    log.info("========")
+    log.info(f"Summation of feature sizes: {sum(model.feature_sizes):,}")
+    log.info(f"Number of 1st order embeddings: {e1:,}")
+    log.info(f"Number of 2nd order embeddings: {e2:,}")
+    if model.use_fwfm:
+        log.info(f"Number of 2nd order interactions: {nz_r:,}")
+    if model.use_deep:
+        log.info(f"Number of DNN parameters: {dnn:,}")
+    log.info(f"Number of total parameters: {num_total:,}")
+    log.info("========")
+    num_total_original = num_total
+
+    # the training set lives in HBM; each epoch's shuffle is a device gather by the reference's
+    # numpy permutation (same order as the reference's host-side shuffle)
+    Xi_d = torch.as_tensor(Xi_train.reshape(x_size, ncat), dtype=torch.int64).to(device)
+    Xv_d = torch.as_tensor(Xv_train, dtype=torch.float32).to(device)
+    y_d = torch.as_tensor(y_train, dtype=torch.float32).to(device)
+    train_result, valid_result = [], []
+    n_iter = 0
+    bs = model.batch_size
+    gbs = bs * world
+    for epoch in range(model.n_epochs):
+        total_loss = 0.0
+        batch_iter = x_size // gbs
+        epoch_begin = batch_begin = time()
+        teacher_outputs = None
+        if teacher_model:
+            t0 = time()
+            teacher_model.eval()
+            teacher_outputs = model.fetch_teacher_outputs(teacher_model, Xi_train, Xv_train, x_size)
+            logging.info("- Finished computing teacher outputs after {} secs..".format(math.ceil(time() - t0)))
+        for i in range(batch_iter + 1):
+            if epoch >= model.warm:
+                n_iter += 1
+            offset = i * gbs
+            end = min(x_size, offset + gbs)
+            if offset == end:
+                break
+            lo = min(end, offset + rank * bs)
+            hi = min(end, lo + bs)
+            n_global = end - offset
+            optimizer.zero_grad()
+            if hi > lo:
+                xi, xv, yb = Xi_d[lo:hi], Xv_d[lo:hi], y_d[lo:hi]
+                outputs = model(xi, xv)
+                if teacher_model:
+                    tb = torch.as_tensor(teacher_outputs[i]).to(device)
+                    loss = model.loss_fn_kd(outputs, tb, yb)
+                else:
+                    # mean over the global batch: the rank's sum / n_global, summed over ranks below
+                    loss = F.binary_cross_entropy_with_logits(outputs, yb, reduction="sum") / n_global \
+                        if dist else F.binary_cross_entropy_with_logits(outputs, yb)
+                loss.backward()
+            else:
+                loss = torch.zeros((), device=device)
+                for p in model.parameters():
+                    p.grad = torch.zeros_like(p)
+            allreduce_grads(model)
+            optimizer.step()
+            total_loss += loss.item()
+            if model.verbose and i % 100 == 99:
+                ev = model.evaluate(xi, xv, yb)
+                log.info("[%d, %5d] loss: %.6f metric: %.6f time: %.1f s" %
+                         (epoch + 1, i + 1, total_loss / 100.0, ev, time() - batch_begin))
+                total_loss = 0.0
+                batch_begin = time()
+            if prune and (i == batch_iter or i % 10 == 9) and epoch >= model.warm:
+                model.adaptive_sparse = model.target_sparse * (1 - 0.99 ** (n_iter / 100.))
+                prune_step(model, model.adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb_corr)
+
+        no_non_sparse = sum(int((p != 0).sum().item()) for p in model.parameters())
+        log.info("Model parameters %d, sparse rate %.2f%%" % (no_non_sparse, 100 - no_non_sparse * 100. / num_total))
+        train_loss, train_eval, train_prauc, train_rce = model.eval_by_batch(Xi_train, Xv_train, y_train, x_size)
+        train_result.append(train_eval)
+        log.info("Training [%d] loss: %.6f metric: %.6f prauc: %.4f rce: %.2f sparse %.2f%% time: %.1f s" %
+                 (epoch + 1, train_loss, train_eval, train_prauc, train_rce,
+                  100 - no_non_sparse * 100. / num_total, time() - epoch_begin))
+        if is_valid:
+            valid_loss, valid_eval, valid_prauc, valid_rce = model.eval_by_batch(Xi_valid, Xv_valid, y_valid,
+                                                                                 x_valid_size)
+            valid_result.append(valid_eval)
+            log.info("Validation [%d] loss: %.6f metric: %.6f prauc: %.4f rce: %.2f sparse %.2f%% time: %.1f s" %
+                     (epoch + 1, valid_loss, valid_eval, valid_prauc, valid_rce,
+                      100 - no_non_sparse * 100. / num_total, time() - epoch_begin))
+        log.info("*" * 50)
+        model.train()
+        perm = np.random.permutation(x_size)
+        Xi_train, Xv_train, y_train = Xi_train[perm], Xv_train[perm], y_train[perm]
+        pd = torch.as_tensor(perm).to(device)
+        Xi_d, Xv_d, y_d = Xi_d[pd], Xv_d[pd], y_d[pd]
+        if save_path and rank == 0:
+            torch.save(model.state_dict(), save_path)
+        if is_valid and early_stopping and model.training_termination(valid_result):
+            log.info("early stop at [%d] epoch!" % (epoch + 1))
+            break
+
+    if prune:
+        tot, e1, e2, dnn, nz_r = _param_summary(model, log, nonzero=True)
+        log.info("========")
+        log.info(f"Number of pruned 1st order embeddings: {e1:,}")
+        log.info(f"Number of pruned 2nd order embeddings: {e2:,}")
+        log.info(f"Number of pruned 2nd order interactions: {nz_r:,}")
+        log.info(f"Number of pruned DNN parameters: {dnn:,}")
+        log.info(f"Number of pruned total parameters: {tot:,}")
+        log.info(f"Non pruned model parameters: \t{num_total_original:,}")
+        log.info(f"Pruned Parameters: \t{num_total_original - tot:,}")
+        log.info("========")
+    return train_result, valid_result
