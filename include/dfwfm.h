@@ -164,6 +164,29 @@ typedef struct {
 int dfwfm_adam_step(const dfwfm_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,
                     double eps, double weight_decay, int64_t step, void* stream);
 
+/* ---- graph-replayable training step -------------------------------------------------------
+ * A training step whose every launch reads its per-step scalars from device memory can be captured
+ * once into a HIP graph and replayed (no host work per step).  The per-step state is one
+ * caller-allocated, zero-initialised device block of DFWFM_ADAM_STATE_BYTES: an int64 step counter
+ * followed by the step's Adam scalars. */
+#define DFWFM_ADAM_STATE_BYTES 48
+
+/* From now on the dropout masks of dfwfm_train_forward / dfwfm_backward mix the device step counter
+ * at `step_dev` (an int64 in such a state block; NULL restores host-only seeds) into their seed,
+ * read when the kernels run -- so a replayed step draws fresh masks. */
+int dfwfm_set_step_source(dfwfm_model* m, const int64_t* step_dev);
+
+/* dfwfm_adam_step with the step counter and bias corrections on the device: increments the counter
+ * in `state_dev`, derives the scalars there (double, then f32) and updates every tensor. */
+int dfwfm_adam_step_dev(const dfwfm_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,
+                        double eps, double weight_decay, void* state_dev, void* stream);
+
+/* Gradient of binary_cross_entropy_with_logits (reference criterion, model/DeepFMs.py:561, :634) with
+ * the summed loss divided by `denom` (the batch for reduction='mean'): dlogit[i] = (sigmoid(z_i) - y_i)
+ * / denom.  When loss_sum is non-NULL the per-sample losses are added to *loss_sum. */
+int dfwfm_bce_grad(const float* logits, const float* labels, int64_t n, double denom, float* dlogit,
+                   float* loss_sum, void* stream);
+
 /* Synchronises `stream`, returns the sticky error-flag word and clears it. */
 int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream);
 

@@ -134,3 +134,31 @@ def train_step(cfg, params, Xi, Xv, y, lr, l2, masks=None, drop_p=0.0):
     opt = torch.optim.Adam(list(leaf.values()), lr=lr, weight_decay=l2)
     opt.step()
     return out.detach().numpy(), float(loss.item()), grads, {k: v.detach().numpy() for k, v in leaf.items()}
+
+
+def step_seed(base, step):
+    """Seed of a graph-replayed step (csrc/dfwfm_device.h step_seed): base ^ mix32(step * 0x9E3779B9 + 0x7F4A7C15),
+    with `step` the device counter's value when the step's kernels run (0 for the first step)."""
+    with np.errstate(over="ignore"):
+        x = np.array([(step * 0x9E3779B9 + 0x7F4A7C15) & 0xFFFFFFFF], dtype=np.uint32)
+        return int(np.uint32(base) ^ _mix32(x)[0])
+
+
+def train_steps(cfg, params, batches, lr, l2, mask_fn=None, drop_p=0.0):
+    """Several reference training steps with one persistent torch.optim.Adam (CPU).  batches: list of
+    (Xi, Xv, y); mask_fn(k, B) -> dropout masks of step k (or None).  Returns (per-step logits, params)."""
+    leaf = {k: torch.tensor(v, requires_grad=True) for k, v in params.items()}
+    opt = torch.optim.Adam(list(leaf.values()), lr=lr, weight_decay=l2)
+    outs = []
+    for k, (Xi, Xv, y) in enumerate(batches):
+        opt.zero_grad()
+        masks = mask_fn(k, len(Xi)) if mask_fn else None
+        out = forward_graph(cfg, leaf, torch.as_tensor(Xi), torch.as_tensor(Xv), masks, drop_p)
+        loss = F.binary_cross_entropy_with_logits(out, torch.as_tensor(y, dtype=torch.float32))
+        loss.backward()
+        for v in leaf.values():
+            if v.grad is None:
+                v.grad = torch.zeros_like(v)
+        opt.step()
+        outs.append(out.detach().numpy())
+    return outs, {k: v.detach().numpy() for k, v in leaf.items()}

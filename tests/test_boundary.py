@@ -26,9 +26,10 @@ def header_functions():
 
 def test_header_declares_expected_api():
     assert header_functions() == sorted([
-        "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_backward", "dfwfm_diag_stamps", "dfwfm_forward",
-        "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy", "dfwfm_model_set_dense",
-        "dfwfm_model_set_tables", "dfwfm_read_error_flag", "dfwfm_train_forward"])
+        "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_bce_grad",
+        "dfwfm_diag_stamps", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy",
+        "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_read_error_flag", "dfwfm_set_step_source",
+        "dfwfm_train_forward"])
 
 
 def test_library_exports_every_header_symbol(built):
@@ -50,6 +51,10 @@ def test_abi_version_and_error_string(built):
     assert L.dfwfm_backward(None, None, None, None) == -1
     assert L.dfwfm_adam_step(None, 3, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, None) == -1
     assert L.dfwfm_adam_step(None, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None) == -1  # step >= 1
+    assert L.dfwfm_adam_step_dev(None, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, None, None) == -1
+    assert L.dfwfm_bce_grad(None, None, 4, 4.0, None, None, None) == -1
+    assert L.dfwfm_bce_grad(None, None, 0, 0.0, None, None, None) == -1  # denom > 0
+    assert L.dfwfm_set_step_source(None, None) == -1
 
 
 def test_struct_layouts_match_header(built):

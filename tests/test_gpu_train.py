@@ -148,3 +148,82 @@ def test_fit_learns(gpu):
                 batch_size=256, learning_rate=1e-2, weight_decay=3e-7, h_depth=2, deep_nodes=64).to(gpu)
     train_res, _ = m.fit(xi.reshape(-1, 26, 1), xv, y, [], [], [])
     assert len(train_res) == 3 and train_res[-1] > 0.6 and train_res[-1] > train_res[0]
+
+
+def _batches(cfg, xi, xv, y, B, k):
+    return [(xi[i * B:(i + 1) * B], xv[i * B:(i + 1) * B], y[i * B:(i + 1) * B]) for i in range(k)]
+
+
+def _param_err(m, onew, lr):
+    worst = 0.0
+    for k, p in m.named_parameters():
+        worst = max(worst, float(np.abs(p.detach().cpu().numpy() - onew[k]).max() / lr))
+    return worst
+
+
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult"])
+def test_fused_graph_steps_match_oracle(gpu, name):
+    """FusedTrainStep: step 1 eager, steps 2-4 replayed from the captured HIP graph; parameters after
+    4 steps equal 4 reference steps (torch.optim.Adam carried across steps) within a fraction of lr."""
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    B, K = 64, 4
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7)
+    logits = []
+    for xb, vb, yb in _batches(cfg, xi, xv, y, B, K):
+        t.step(torch.from_numpy(xb).to(gpu), torch.from_numpy(vb).to(gpu), torch.from_numpy(yb).to(gpu))
+        logits.append(t.out[:B].detach().cpu().numpy().copy())
+    torch.cuda.synchronize()
+    assert t.graphs is not None  # steps 2.. replayed
+    outs, onew = torch_port.train_steps(cfg, params, _batches(cfg, xi, xv, y, B, K), 1e-3, 3e-7)
+    for k in range(K):
+        assert logit_close(logits[k], outs[k]) < 1e-4, k
+    # Adam's early steps move by ~lr * sign(g): near-zero gradients may flip, so the bar is 1% of lr
+    # over all entries and a tight one on the median
+    errs = [np.abs(p.detach().cpu().numpy() - onew[k]).reshape(-1) / 1e-3 for k, p in m.named_parameters()]
+    e = np.concatenate(errs)
+    assert np.median(e) < 1e-3 and np.quantile(e, 0.999) < 0.05, (np.median(e), np.quantile(e, 0.999))
+    # the loss sum the kernels accumulated equals the oracle's
+    ref_loss = sum(float(torch.nn.functional.binary_cross_entropy_with_logits(
+        torch.from_numpy(o), torch.from_numpy(yb), reduction="sum")) for o, (_, _, yb) in
+        zip(outs, _batches(cfg, xi, xv, y, B, K)))
+    assert abs(t.loss_sum.item() - ref_loss) <= 1e-4 * abs(ref_loss)
+
+
+def test_fused_step_dropout_uses_device_step_seed(gpu):
+    """Graph-replayable dropout: step k draws masks from seed ^ mix(k - 1) (device counter)."""
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_small_mlp")
+    B, K = 32, 3
+    m = build(cfg, params, gpu, is_deep_dropout=True)
+    t = FusedTrainStep(m, B, lr=1e-3, weight_decay=0.0)
+    for xb, vb, yb in _batches(cfg, xi, xv, y, B, K):
+        t.step(torch.from_numpy(xb).to(gpu), torch.from_numpy(vb).to(gpu), torch.from_numpy(yb).to(gpu))
+    torch.cuda.synchronize()
+    widths = [cfg["field_size"] * cfg["embedding_size"]] + [cfg["deep_nodes"]] * cfg["h_depth"]
+    mask_fn = lambda k, n: torch_port.dropout_masks(torch_port.step_seed(t.seed, k), 0.5, n, widths)  # noqa: E731
+    outs, onew = torch_port.train_steps(cfg, params, _batches(cfg, xi, xv, y, B, K), 1e-3, 0.0, mask_fn, 0.5)
+    e = np.concatenate([np.abs(p.detach().cpu().numpy() - onew[k]).reshape(-1) / 1e-3
+                        for k, p in m.named_parameters()])
+    assert np.median(e) < 1e-3 and np.quantile(e, 0.999) < 0.05
+
+
+def test_fit_fused_matches_autograd_fit(gpu):
+    """fit() with the fused graph step and with the autograd path (fused_fit=False) train the same
+    model to the same AUC (same init seed, same shuffles; no dropout so the paths are comparable)."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = [1] * 13 + [50, 300, 7, 1000, 20, 5, 64, 9, 100, 3, 11, 17, 250, 4, 6, 30, 8, 2, 40, 12, 90, 5, 15,
+                        300, 7, 60]
+    xi, xv = synth.synth_inputs(sizes, 13, 4096, seed=5)
+    logit = ((xi[:, 0] % 7) - 3) * 0.6 + (xv[:, 0] > 30) * 1.0 - 0.5
+    y = (np.random.default_rng(1).random(4096) < 1 / (1 + np.exp(-logit))).astype(np.float32)
+    res = []
+    for fused in (True, False):
+        m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1, n_epochs=2,
+                    batch_size=512, learning_rate=1e-2, weight_decay=3e-7, h_depth=2, deep_nodes=64,
+                    is_deep_dropout=False, random_seed=3).to(gpu)
+        m.fused_fit = fused
+        tr, _ = m.fit(xi.reshape(-1, 26, 1), xv, y, [], [], [])
+        res.append(tr)
+    assert abs(res[0][-1] - res[1][-1]) < 2e-3, res

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
     ap.add_argument("--no-dropout", action="store_true")
+    ap.add_argument("--mode", choices=["fused", "autograd"], default="fused",
+                    help="fused: FusedTrainStep (HIP-graph replay, what fit() runs); autograd: model() + "
+                         "loss.backward() + HIP Adam")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -40,7 +43,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
-    from xsdeepfwfm_deprecated_amd.training import Adam, allreduce_grads
+    from xsdeepfwfm_deprecated_amd.training import Adam, FusedTrainStep, allreduce_grads
     sizes = synth.CRITEO_FEATURE_SIZES
     fwlw = a.first_order == "fwlw"
     model = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1,
@@ -58,8 +61,15 @@ def main():
         batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev),
                         torch.from_numpy(y).float().to(dev)))
 
+    trainer = None
+    if a.mode == "fused":
+        dist = torch.distributed if world > 1 else None
+        trainer = FusedTrainStep(model, B, lr=1e-3, weight_decay=3e-7, dist=dist)
+
     def step(i):
         xi, xv, y = batches[i % 4]
+        if trainer is not None:
+            return trainer.step(xi, xv, y, B * world if world > 1 else None)
         opt.zero_grad()
         out = model(xi, xv)
         loss = F.binary_cross_entropy_with_logits(out, y)
@@ -92,7 +102,7 @@ def main():
            "value": round(world * B * a.steps / (ms / 1e3), 1), "unit": "samples/s", "n_gpus": world,
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms / a.steps, 4), "per_gpu_batch": B,
            "first_order": a.first_order, "dropout": not a.no_dropout, "wall_s": round(wall, 3),
-           "final_loss": round(float(loss.item()), 6)}
+           "mode": a.mode, "final_loss_sum": round(float(loss.item()), 4)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

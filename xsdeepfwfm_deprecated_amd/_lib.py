@@ -28,6 +28,7 @@ ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
 DFWFM_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported", -3: "HIP error", -4: "bad state"}
 FLAG_INDEX_OUT_OF_RANGE = 1
+ADAM_STATE_BYTES = 48
 
 
 class DfwfmError(RuntimeError):
@@ -81,6 +82,11 @@ SIGNATURES = {
     "dfwfm_adam_step": (ctypes.c_int, [ctypes.POINTER(dfwfm_adam_tensor), ctypes.c_int32, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int64, _P]),
+    "dfwfm_set_step_source": (ctypes.c_int, [_P, _P]),
+    "dfwfm_adam_step_dev": (ctypes.c_int, [ctypes.POINTER(dfwfm_adam_tensor), ctypes.c_int32, ctypes.c_double,
+                                           ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                           _P, _P]),
+    "dfwfm_bce_grad": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_double, _P, _P, _P]),
     "dfwfm_read_error_flag": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
     "dfwfm_last_error": (ctypes.c_char_p, []),
     "dfwfm_diag_stamps": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64, _P]),

@@ -56,6 +56,7 @@ struct dfwfm_model {
   int64_t t_batch;
   float t_drop;
   uint32_t t_seed;
+  const int64_t* step_src;  // dfwfm_set_step_source
   bool trained;
   bool tables_set;
   bool dense_set;
@@ -267,33 +268,46 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
   if ((m->flags & kFoFwlw) && !fwfm_lin) return fail(DFWFM_ERR_INVALID_ARG, "use_fwlw needs fwfm_linear");
   if ((m->flags & kFoLw) && !fm_1st) return fail(DFWFM_ERR_INVALID_ARG, "use_lw needs fm_1st");
   if (!bias) return fail(DFWFM_ERR_INVALID_ARG, "bias is required");
+  PackList L;
+  memset(&L, 0, sizeof L);
+  int blocks = 0;
+  auto job = [&](int type, const float* src, void* dst, int64_t total, int a, int b, int d) {
+    PackJob& j = L.j[L.n++];
+    j.src = src;
+    j.dst = reinterpret_cast<float*>(dst);
+    j.total = total;
+    j.type = type;
+    j.a = a;
+    j.b = b;
+    j.d = d;
+    j.block0 = blocks;
+    blocks += (int)((total + 255) / 256);
+  };
   if (c.use_fwfm || c.use_fm) {
-    hipError_t e = launch_pack_fwfm(field_cov, m->F, c.use_fm ? 1 : 0, m->MT, m->S, m->d_upack, s);
-    if (e == hipSuccess) e = launch_pack_fwfm_sym(field_cov, m->F, c.use_fm ? 1 : 0, m->MT, m->S, m->d_rsk, s);
-    if (e != hipSuccess) return hip_fail(e, "pack_fwfm");
+    const int64_t tot = (int64_t)m->MT * m->S * 64;
+    job(kPackFwfm, field_cov, m->d_upack, tot, m->F, c.use_fm ? 1 : 0, m->S);
+    job(kPackFwfmSym, field_cov, m->d_rsk, tot, m->F, c.use_fm ? 1 : 0, m->S);
   }
-  hipError_t e = hipSuccess;
-  if (m->flags & kFoFwlw) e = launch_pad_copy(fwfm_lin, m->F * m->D, m->F * m->D, m->d_fwlw, s);
-  if (e == hipSuccess && (m->flags & kFoLw)) e = launch_pad_copy(fm_1st, m->F, m->F, m->d_lw, s);
-  if (e == hipSuccess) e = launch_pad_copy(bias, 1, 1, m->d_bias, s);
-  if (e != hipSuccess) return hip_fail(e, "pad_copy");
+  if (m->flags & kFoFwlw) job(kPackPad, fwfm_lin, m->d_fwlw, m->F * m->D, m->F * m->D, 0, 0);
+  if (m->flags & kFoLw) job(kPackPad, fm_1st, m->d_lw, m->F, m->F, 0, 0);
+  job(kPackPad, bias, m->d_bias, 1, 1, 0, 0);
   if (c.use_deep) {
     if (!lin_w || !lin_b || !fc_w) return fail(DFWFM_ERR_INVALID_ARG, "use_deep needs MLP weights");
-    float4* dst = m->d_wpack;
+    size_t off = 0;
     for (int h = 0; h < m->H; ++h) {
       if (!lin_w[h] || !lin_b[h]) return fail(DFWFM_ERR_INVALID_ARG, "layer %d weight/bias is null", h);
       const int K = h == 0 ? m->F * m->D : m->N;
       const int NC = h == 0 ? m->NC0 : m->NT;
-      e = launch_pack_linear(lin_w[h], m->N, K, m->NT, NC, dst, s);
-      if (e == hipSuccess)
-        e = launch_pack_linear_t(lin_w[h], m->N, K, h == 0 ? m->NC0 : m->NT, m->NT, m->d_wtpack + m->wt_off[h + 1], s);
-      if (e == hipSuccess) e = launch_pad_copy(lin_b[h], m->N, m->NT * 16, m->d_mlp_b + (size_t)h * m->NT * 16, s);
-      if (e != hipSuccess) return hip_fail(e, "pack_linear");
-      dst += (size_t)m->NT * NC * 64;
+      const int64_t tot = (int64_t)m->NT * NC * 64;
+      job(kPackLinear, lin_w[h], m->d_wpack + off, tot, m->N, K, NC);
+      job(kPackLinearT, lin_w[h], m->d_wtpack + m->wt_off[h + 1], tot, m->N, K, m->NT);
+      job(kPackPad, lin_b[h], m->d_mlp_b + (size_t)h * m->NT * 16, m->NT * 16, m->N, 0, 0);
+      off += (size_t)tot;
     }
-    e = launch_pad_copy(fc_w, m->N, m->NT * 16, m->d_fc, s);
-    if (e != hipSuccess) return hip_fail(e, "pad_copy fc");
+    job(kPackPad, fc_w, m->d_fc, m->NT * 16, m->N, 0, 0);
   }
+  hipError_t e = launch_pack_list(L, blocks, s);
+  if (e != hipSuccess) return hip_fail(e, "pack launch");
   m->dense_set = true;
   return DFWFM_OK;
 }
@@ -445,6 +459,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   a.drop_p = dropout_p;
   a.drop_scale = 1.f / (1.f - dropout_p);
   a.seed = seed;
+  a.seed_src = m->step_src;
   hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, 1, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
   m->trained = true;
@@ -495,6 +510,7 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
     a.drop_p = m->t_drop;
     a.drop_scale = 1.f / (1.f - m->t_drop);
     a.seed = m->t_seed;
+    a.seed_src = m->step_src;
     // diagnostics only: DFWFM_DIAG_STAMPS=2 records the backward's phase clocks instead of the forward's
     const char* stv = getenv("DFWFM_DIAG_STAMPS");
     if (stv && atoi(stv) == 2) {
@@ -704,6 +720,59 @@ int dfwfm_adam_step(const dfwfm_adam_tensor* t, int32_t n, double lr, double bet
     blocks += nb;
   }
   return flush();
+}
+
+int dfwfm_set_step_source(dfwfm_model* m, const int64_t* step_dev) {
+  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  m->step_src = step_dev;
+  return DFWFM_OK;
+}
+
+int dfwfm_adam_step_dev(const dfwfm_adam_tensor* t, int32_t n, double lr, double beta1, double beta2, double eps,
+                        double weight_decay, void* state_dev, void* stream) {
+  if ((n > 0 && !t) || !state_dev) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (n < 0) return fail(DFWFM_ERR_INVALID_ARG, "negative tensor count");
+  static_assert(sizeof(AdamDevState) == DFWFM_ADAM_STATE_BYTES, "state block size");
+  for (int i = 0; i < n; ++i)
+    if (t[i].grad && t[i].numel > 0 && (!t[i].param || !t[i].exp_avg || !t[i].exp_avg_sq))
+      return fail(DFWFM_ERR_INVALID_ARG, "adam tensor %d: null state pointer", i);
+  AdamDevState* st = reinterpret_cast<AdamDevState*>(state_dev);
+  hipError_t e = launch_adam_prep(st, lr, beta1, beta2, eps, weight_decay, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "adam prep launch");
+  AdamList list;
+  memset(&list, 0, sizeof list);
+  int64_t blocks = 0;
+  for (int i = 0; i <= n; ++i) {
+    const bool last = i == n;
+    if (!last && (!t[i].grad || t[i].numel <= 0)) continue;
+    const int64_t nb = last ? 0 : (t[i].numel + 1023) / 1024;
+    if (nb > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "adam tensor %d too large", i);
+    if (list.n > 0 && (last || list.n == kAdamList || blocks + nb > 0x7fffffff)) {
+      e = launch_adam_dev(list, (int)blocks, st, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(e, "adam launch");
+      list.n = 0;
+      blocks = 0;
+    }
+    if (last) break;
+    AdamTensor& a = list.t[list.n++];
+    a.p = t[i].param;
+    a.g = t[i].grad;
+    a.m = t[i].exp_avg;
+    a.v = t[i].exp_avg_sq;
+    a.n = t[i].numel;
+    a.block0 = blocks;
+    blocks += nb;
+  }
+  return DFWFM_OK;
+}
+
+int dfwfm_bce_grad(const float* z, const float* y, int64_t n, double denom, float* dz, float* loss_sum,
+                   void* stream) {
+  if (n < 0) return fail(DFWFM_ERR_INVALID_ARG, "negative count");
+  if (n > 0 && (!z || !y || !dz)) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (!(denom > 0.0)) return fail(DFWFM_ERR_INVALID_ARG, "denom must be > 0");
+  hipError_t e = launch_bce_grad(z, y, n, (float)denom, dz, loss_sum, (hipStream_t)stream);
+  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "bce launch");
 }
 
 int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream) {

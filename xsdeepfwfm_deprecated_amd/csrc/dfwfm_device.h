@@ -177,4 +177,12 @@ __device__ __forceinline__ bool dropout_keep(uint32_t seed, int layer, int64_t r
   return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
 }
 
+// Dropout seed of a step: the host's seed, or -- for graph-replayed steps -- that seed mixed with a
+// device step counter (read at kernel time, so every replay draws fresh masks).
+__device__ __forceinline__ uint32_t step_seed(uint32_t base, const int64_t* src) {
+  if (src == nullptr) return base;
+  const uint32_t step = (uint32_t)*src;
+  return base ^ mix32(step * 0x9E3779B9U + 0x7F4A7C15U);
+}
+
 }  // namespace dfwfm

@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "../../include/dfwfm.h"
 
 namespace dfwfm {
@@ -70,6 +73,7 @@ struct FwdArgs {
   float drop_p;             // dropout probability of the deep tower (kDrop)
   float drop_scale;         // 1 / (1 - p)
   uint32_t seed;            // dropout hash seed of this step
+  const int64_t* seed_src;  // device step counter mixed into the seed (graph replay), or null
 };
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.
@@ -121,6 +125,7 @@ struct BwdArgs {
   int32_t flags;
   float drop_p, drop_scale;
   uint32_t seed;
+  const int64_t* seed_src;       // as FwdArgs::seed_src
   uint64_t* stamps;              // diagnostics only (DFWFM_DIAG_STAMPS=2): phase clocks per workgroup
 };
 
@@ -212,13 +217,40 @@ struct AdamList {
   int32_t n;
 };
 
+// Raises a kernel's dynamic-LDS limit when a launch needs more than previously granted.  Done once
+// per kernel and size, not per launch, so launches recorded into a HIP graph make no attribute calls.
+inline hipError_t ensure_lds_limit(const void* fn, size_t lds) {
+  if (lds <= 65536) return hipSuccess;
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> granted;
+  std::lock_guard<std::mutex> g(mu);
+  size_t& cur = granted[fn];
+  if (lds <= cur) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) cur = lds;
+  return e;
+}
+
+// One packing job of set_dense (see pack_dense_kernel).
+enum PackType : int32_t { kPackPad = 0, kPackLinear = 1, kPackLinearT = 2, kPackFwfm = 3, kPackFwfmSym = 4 };
+struct PackJob {
+  const float* src;
+  float* dst;
+  int64_t total;    // elements (float or float4) written
+  int32_t type;
+  int32_t a, b, d;  // pad: n (valid), -, -; linear: N, K, NC; fwfm: F, mode, S
+  int32_t block0;
+  int32_t pad_;
+};
+constexpr int kPackList = 56;  // 3 per hidden layer (kMaxH = 16) + 6; the list is a kernel argument (< 4 KiB)
+struct PackList {
+  PackJob j[kPackList];
+  int32_t n;
+};
+
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, hipStream_t s);
-hipError_t launch_pack_linear(const float* w, int N, int K, int NT, int NC, float4* out, hipStream_t s);
-hipError_t launch_pad_copy(const float* src, int n, int npad, float* dst, hipStream_t s);
-hipError_t launch_pack_fwfm(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s);
-hipError_t launch_pack_linear_t(const float* w, int N, int K, int KT, int NTc, float4* out, hipStream_t s);
-hipError_t launch_pack_fwfm_sym(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s);
+hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 hipError_t launch_backward(const BwdArgs& a, int D, int tpw, size_t lds, hipStream_t s);
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
 hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s);
@@ -227,5 +259,14 @@ hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s)
 hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
                        float eps, float wd, float bc2_sqrt, hipStream_t s);
+// device-side step: state = {int64 step; float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt}
+struct AdamDevState {
+  int64_t step;
+  float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt, pad[3];
+};
+hipError_t launch_adam_prep(AdamDevState* st, double lr, double b1, double b2, double eps, double wd, hipStream_t s);
+hipError_t launch_adam_dev(const AdamList& list, int total_blocks, const AdamDevState* st, hipStream_t s);
+hipError_t launch_bce_grad(const float* z, const float* y, int64_t n, float denom, float* dz, float* loss_sum,
+                           hipStream_t s);
 
 }  // namespace dfwfm

@@ -36,7 +36,9 @@ namespace dfwfm {
 // ---------------------------------------------------------------------------
 // the fused forward kernel
 // ---------------------------------------------------------------------------
-template <int D, int TPW, int KS>
+// TRAIN: the training-step variant (activations saved, dropout); compiled separately so the inference
+// kernel carries none of it
+template <int D, int TPW, int KS, bool TRAIN>
 __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   constexpr int NTH = 256 * KS;
   constexpr int NW = 4 * KS;
@@ -233,9 +235,9 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   }
   __syncthreads();
   stamp(p.stamps, 2, tid);
-  const bool train = (flags & kTrain) != 0;
+  constexpr bool train = TRAIN;
   const int FD = F * D;
-  if (train) {  // E, before dropout, for the shallow backward
+  if constexpr (train) {  // E, before dropout, for the shallow backward
     for (int i = tid; i < kBM * FD; i += NTH) {
       const int b = i / FD;
       const int c = i - b * FD;
@@ -322,19 +324,20 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   stamp(p.stamps, 10, tid);
   __syncthreads();
   stamp(p.stamps, 11, tid);
-  if (train) {
+  if constexpr (train) {
     for (int i = tid; i < kBM * F; i += NTH) {
       const int b = i / F;
       if (b0 + b < p.batch) p.sv_fo[(b0 + b) * F + (i - b * F)] = fo[b * Fp + (i - b * F)];
     }
     if (deep) {  // deep_emb dropout (net_1_linear_0_dropout, model/DeepFMs.py:411) and X_0
       const bool drop = (flags & kDrop) != 0;
+      const uint32_t dseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
       for (int i = tid; i < kBM * FD; i += NTH) {
         const int b = i / FD;
         const int c = i - b * FD;
         const int64_t row = b0 + b;
         float v = bufX[b * SX + c];
-        if (drop) v = dropout_keep(p.seed, 0, row, c, p.drop_p) ? v * p.drop_scale : 0.f;
+        if (drop) v = dropout_keep(dseed, 0, row, c, p.drop_p) ? v * p.drop_scale : 0.f;
         bufX[b * SX + c] = v;
         if (row < p.batch) p.sv_x[0][row * r4(FD) + c] = v;  // rows 16-byte aligned for dw_kernel
       }
@@ -367,10 +370,11 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   }
 
   stamp(p.stamps, 3, tid);
-  if (train) __syncthreads();  // the dropped X_0 tile is complete before layer 1 reads it
+  if constexpr (train) __syncthreads();  // the dropped X_0 tile is complete before layer 1 reads it
   // ---- phase M: MLP on MFMA -------------------------------------------------
   const int row0 = (lane >> 4) * 4;
-  const bool drop = (flags & kDrop) != 0;
+  const bool drop = train && (flags & kDrop) != 0;
+  const uint32_t hseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
   float dpart[4] = {0.f, 0.f, 0.f, 0.f};
   int layer_off = 0;  // float4 offset of layer h in wpack
   for (int h = 0; h < p.H; ++h) {
@@ -421,18 +425,28 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
         if (t < p.NT) {
           const int n = t * 16 + (lane & 15);
           const bool valid = n < p.N;  // padded neurons stay exactly 0 (bias/fc pads are 0)
+          if constexpr (train) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
-            if (train) {  // dropout after the ReLU (net_1_linear_{h}_dropout, :416-426), X_h kept
+            for (int r = 0; r < 4; ++r) {
+              // dropout after the ReLU (net_1_linear_{h}_dropout, :416-426), X_h kept for the backward
+              float v = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
               const int64_t row = b0 + row0 + r;
-              if (drop) v = dropout_keep(p.seed, h + 1, row, n, p.drop_p) ? v * p.drop_scale : 0.f;
+              if (drop) v = dropout_keep(hseed, h + 1, row, n, p.drop_p) ? v * p.drop_scale : 0.f;
               if (valid && row < p.batch) p.sv_x[h + 1][row * p.N + n] = v;
+              if (!last)
+                outa[(row0 + r) * SO + n] = v;
+              else
+                dpart[r] = fmaf(v, wf[j], dpart[r]);
             }
-            if (!last)
-              outa[(row0 + r) * SO + n] = v;
-            else
+          } else if (!last) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) outa[(row0 + r) * SO + n] = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
               dpart[r] = fmaf(v, wf[j], dpart[r]);
+            }
           }
         }
       }
@@ -469,62 +483,82 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
 // dense-parameter packing (run on weight updates, not per forward)
 // ---------------------------------------------------------------------------
 
-// W [N][K] row-major (nn.Linear.weight) -> [NT][NC][64][4] fragment order
-__global__ void pack_linear_kernel(const float* __restrict__ w, int N, int K, int NT, int NC,
-                                   float4* __restrict__ out) {
-  const int64_t total = (int64_t)NT * NC * 64;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(i & 63);
-    const int64_t tc = i >> 6;
-    const int c = (int)(tc % NC);
-    const int t = (int)(tc / NC);
-    const int n = t * 16 + (lane & 15);
-    const int k0 = 16 * c + 4 * (lane >> 4);
-    float v[4];
+// ---------------------------------------------------------------------------
+// Dense-parameter packing, one launch for every job of a set_dense (re-run after each optimizer step):
+//   kPackPad       dst[i] = i < n ? src[i] : 0, i < npad
+//   kPackLinear    W [N][K] (nn.Linear.weight) -> [NT][NC][64] float4 forward fragments:
+//                  out[(t*NC + c)*64 + lane][s] = W[16t + (lane&15)][16c + 4(lane>>4) + s]
+//   kPackLinearT   the backward's transposed fragments (outputs k, contraction n):
+//                  out[(t*NC + c)*64 + lane][s] = W[16c + 4(lane>>4) + s][16t + (lane&15)]
+//   kPackFwfm      FwFM A operand U[k][l] = (R[l][k] + R[k][l]) / 2 for l > k (model/DeepFMs.py:363-364;
+//                  the diagonal is removed by :366-367); FM: 1 above the diagonal.  Fragment order
+//                  out[(m*S + s)*64 + lane] = U[16m + (lane&15)][4s + (lane>>4)]
+//   kPackFwfmSym   the backward's symmetric off-diagonal (R + R^T)/2 (FM: ones), same order
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void pack_elem(const PackJob& j, int64_t i) {
+  switch (j.type) {
+    case kPackPad:
+      j.dst[i] = (j.src && i < j.a) ? j.src[i] : 0.f;
+      break;
+    case kPackLinear:
+    case kPackLinearT: {
+      const int N = j.a, K = j.b, NC = j.d;
+      const int lane = (int)(i & 63);
+      const int64_t tc = i >> 6;
+      const int c = (int)(tc % NC);
+      const int t = (int)(tc / NC);
+      const bool tr = j.type == kPackLinearT;
+      float v[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int k = k0 + s;
-      v[s] = (n < N && k < K) ? w[(int64_t)n * K + k] : 0.f;
+      for (int s = 0; s < 4; ++s) {
+        const int n = tr ? 16 * c + 4 * (lane >> 4) + s : t * 16 + (lane & 15);
+        const int k = tr ? t * 16 + (lane & 15) : 16 * c + 4 * (lane >> 4) + s;
+        v[s] = (n < N && k < K) ? j.src[(int64_t)n * K + k] : 0.f;
+      }
+      reinterpret_cast<float4*>(j.dst)[i] = make_float4(v[0], v[1], v[2], v[3]);
+      break;
     }
-    out[i] = make_float4(v[0], v[1], v[2], v[3]);
+    case kPackFwfm:
+    case kPackFwfmSym: {
+      const int F = j.a, mode = j.b, S = j.d;
+      const int lane = (int)(i & 63);
+      const int ms = (int)(i >> 6);
+      const int s = ms % S;
+      const int m = ms / S;
+      const int k = 16 * m + (lane & 15);
+      const int l = 4 * s + (lane >> 4);
+      const bool keep = j.type == kPackFwfm ? l > k : l != k;
+      float u = 0.f;
+      if (k < F && l < F && keep) u = (mode == 1) ? 1.f : (j.src[l * F + k] + j.src[k * F + l]) * 0.5f;
+      j.dst[i] = u;
+      break;
+    }
+    default:
+      break;
   }
 }
 
-// dst[i] = i < n ? src[i] : 0 for i < npad (src may be null => zeros)
-__global__ void pad_copy_kernel(const float* __restrict__ src, int n, int npad, float* __restrict__ dst) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += gridDim.x * blockDim.x)
-    dst[i] = (src && i < n) ? src[i] : 0.f;
-}
-
-// FwFM A operand: U[k][l] = (R[l][k] + R[k][l]) * 0.5 for l > k (model/DeepFMs.py:363-364; the
-// diagonal is removed by :366-367), 0 elsewhere; mode 1 = FM (U = 1 above the diagonal).
-// Fragment order out[(m*S + s)*64 + lane] = U[16m + (lane&15)][4s + (lane>>4)].
-__global__ void pack_fwfm_kernel(const float* __restrict__ R, int F, int mode, int MT, int S,
-                                 float* __restrict__ out) {
-  const int total = MT * S * 64;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int lane = i & 63;
-    const int ms = i >> 6;
-    const int s = ms % S;
-    const int m = ms / S;
-    const int k = 16 * m + (lane & 15);
-    const int l = 4 * s + (lane >> 4);
-    float u = 0.f;
-    if (k < F && l < F && l > k) u = (mode == 1) ? 1.f : (R[l * F + k] + R[k * F + l]) * 0.5f;
-    out[i] = u;
+__global__ void __launch_bounds__(256) pack_dense_kernel(const PackList L) {
+  int lo = 0, hi = L.n - 1;
+  const int bid = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L.j[mid].block0 <= bid) lo = mid;
+    else hi = mid - 1;
   }
+  const PackJob& j = L.j[lo];
+  const int64_t i = (int64_t)(bid - j.block0) * 256 + threadIdx.x;
+  if (i < j.total) pack_elem(j, i);
 }
 
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <int D, int TPW, int KS>
+template <int D, int TPW, int KS, bool TRAIN>
 static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, hipStream_t s) {
-  auto k = fwd_kernel<D, TPW, KS>;
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  auto k = fwd_kernel<D, TPW, KS, TRAIN>;
+  {
+    hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
     if (e != hipSuccess) return e;
   }
   const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
@@ -532,24 +566,25 @@ static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int D, int KS>
+template <int D, int KS, bool TRAIN>
 static hipError_t launch_fwd_k(const FwdArgs& a, int tpw, size_t lds, hipStream_t s) {
   switch (tpw) {
-    case 1: return launch_fwd_t<D, 1, KS>(a, lds, s);
-    case 2: return launch_fwd_t<D, 2, KS>(a, lds, s);
-    case 3: return launch_fwd_t<D, 3, KS>(a, lds, s);
-    case 4: return launch_fwd_t<D, 4, KS>(a, lds, s);
-    case 5: return launch_fwd_t<D, 5, KS>(a, lds, s);
-    case 6: return launch_fwd_t<D, 6, KS>(a, lds, s);
-    case 7: return launch_fwd_t<D, 7, KS>(a, lds, s);
-    case 8: return launch_fwd_t<D, 8, KS>(a, lds, s);
+    case 1: return launch_fwd_t<D, 1, KS, TRAIN>(a, lds, s);
+    case 2: return launch_fwd_t<D, 2, KS, TRAIN>(a, lds, s);
+    case 3: return launch_fwd_t<D, 3, KS, TRAIN>(a, lds, s);
+    case 4: return launch_fwd_t<D, 4, KS, TRAIN>(a, lds, s);
+    case 5: return launch_fwd_t<D, 5, KS, TRAIN>(a, lds, s);
+    case 6: return launch_fwd_t<D, 6, KS, TRAIN>(a, lds, s);
+    case 7: return launch_fwd_t<D, 7, KS, TRAIN>(a, lds, s);
+    case 8: return launch_fwd_t<D, 8, KS, TRAIN>(a, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 template <int D>
 static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, size_t lds, hipStream_t s) {
-  return ks == 2 ? launch_fwd_k<D, 2>(a, tpw, lds, s) : launch_fwd_k<D, 1>(a, tpw, lds, s);
+  if (a.flags & kTrain) return launch_fwd_k<D, 1, true>(a, tpw, lds, s);
+  return ks == 2 ? launch_fwd_k<D, 2, false>(a, tpw, lds, s) : launch_fwd_k<D, 1, false>(a, tpw, lds, s);
 }
 
 bool supported_embedding_size(int D) { return D == 4 || D == 8 || D == 10 || D == 16 || D == 32; }
@@ -565,23 +600,9 @@ hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, 
   }
 }
 
-hipError_t launch_pack_linear(const float* w, int N, int K, int NT, int NC, float4* out, hipStream_t s) {
-  const int64_t total = (int64_t)NT * NC * 64;
-  const unsigned grid = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(pack_linear_kernel, dim3(grid), dim3(256), 0, s, w, N, K, NT, NC, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_pad_copy(const float* src, int n, int npad, float* dst, hipStream_t s) {
-  if (npad <= 0) return hipSuccess;
-  const unsigned grid = (unsigned)((npad + 255) / 256 < 1024 ? (npad + 255) / 256 : 1024);
-  hipLaunchKernelGGL(pad_copy_kernel, dim3(grid), dim3(256), 0, s, src, n, npad, dst);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_fwfm(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s) {
-  const int total = MT * S * 64;
-  hipLaunchKernelGGL(pack_fwfm_kernel, dim3((total + 255) / 256), dim3(256), 0, s, R, F, mode, MT, S, out);
+hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s) {
+  if (total_blocks <= 0 || L.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_dense_kernel, dim3(total_blocks), dim3(256), 0, s, L);
   return hipGetLastError();
 }
 

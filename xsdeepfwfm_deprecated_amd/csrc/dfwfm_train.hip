@@ -140,6 +140,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
   if (deep) {
     const int H = p.H, N = p.N, NT = p.NT, NP = NT * 16;
     const float scale = drop ? p.drop_scale : 1.f;
+    const uint32_t dseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
     // G_H = dlogit * fc * (X_H > 0) * scale -> bufA and global
     for (int i = tid; i < kBM * NP; i += NTH) {
       const int b = i / NP;
@@ -198,7 +199,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
               if (k < K && row < p.batch) p.sv_g[l - 1][row * N + k] = gv;
             } else if (k < FD) {
               float gv = acc[j][r];
-              if (drop) gv = dropout_keep(p.seed, 0, row, k, p.drop_p) ? gv * scale : 0.f;
+              if (drop) gv = dropout_keep(dseed, 0, row, k, p.drop_p) ? gv * scale : 0.f;
               bufD[b * SX + k] += gv;
             }
           }
@@ -660,43 +661,68 @@ __global__ void __launch_bounds__(256) adam_kernel(const AdamList list, float st
   }
 }
 
-// transposed fragment pack for the backward: outputs = the layer's inputs k, contraction = n
-// out[(t*NTc + c)*64 + lane][s] = W[n = 16c + 4(lane>>4) + s][k = 16t + (lane&15)]
-__global__ void pack_linear_t_kernel(const float* __restrict__ w, int N, int K, int KT, int NTc,
-                                     float4* __restrict__ out) {
-  const int64_t total = (int64_t)KT * NTc * 64;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(i & 63);
-    const int64_t tc = i >> 6;
-    const int c = (int)(tc % NTc);
-    const int t = (int)(tc / NTc);
-    const int k = t * 16 + (lane & 15);
-    const int n0 = 16 * c + 4 * (lane >> 4);
-    float v[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int n = n0 + s;
-      v[s] = (n < N && k < K) ? w[(int64_t)n * K + k] : 0.f;
-    }
-    out[i] = make_float4(v[0], v[1], v[2], v[3]);
+// Graph-replayable Adam: one thread bumps the device step and derives the step's scalars in double
+// (as torch does from Python floats), the update kernels read them from device memory.
+__global__ void adam_prep_kernel(AdamDevState* st, double lr, double b1, double b2, double eps, double wd) {
+  const int64_t step = st->step + 1;
+  st->step = step;
+  const double bc1 = 1.0 - pow(b1, (double)step);
+  const double bc2 = 1.0 - pow(b2, (double)step);
+  st->step_size = (float)(lr / bc1);
+  st->omb1 = (float)(1.0 - b1);
+  st->b2 = (float)b2;
+  st->omb2 = (float)(1.0 - b2);
+  st->eps = (float)eps;
+  st->wd = (float)wd;
+  st->bc2_sqrt = (float)sqrt(bc2);
+}
+
+__global__ void __launch_bounds__(256) adam_dev_kernel(const AdamList list, const AdamDevState* __restrict__ st) {
+  int lo = 0, hi = list.n - 1;
+  const int bid = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (list.t[mid].block0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const AdamTensor T = list.t[lo];
+  const int64_t i0 = (int64_t)(bid - T.block0) * 1024;
+  const float step_size = st->step_size, omb1 = st->omb1, b2 = st->b2, omb2 = st->omb2, eps = st->eps,
+              wd = st->wd, bc2_sqrt = st->bc2_sqrt;
+  for (int64_t i = i0 + threadIdx.x; i < i0 + 1024 && i < T.n; i += 256) {
+    const float pv = T.p[i];
+    float g = T.g[i];
+    if (wd != 0.f) g = fmaf(wd, pv, g);
+    float m = T.m[i];
+    m = fmaf(omb1, __fsub_rn(g, m), m);
+    float v = __fmul_rn(T.v[i], b2);
+    v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), eps);
+    T.m[i] = m;
+    T.v[i] = v;
+    T.p[i] = __fadd_rn(pv, __fdiv_rn(__fmul_rn(-step_size, m), denom));
   }
 }
 
-// symmetric off-diagonal (R + R^T)/2 (FM: ones) in the FwFM A-fragment order
-__global__ void pack_fwfm_sym_kernel(const float* __restrict__ R, int F, int mode, int MT, int S,
-                                     float* __restrict__ out) {
-  const int total = MT * S * 64;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int lane = i & 63;
-    const int ms = i >> 6;
-    const int s = ms % S;
-    const int m = ms / S;
-    const int k = 16 * m + (lane & 15);
-    const int l = 4 * s + (lane >> 4);
-    float u = 0.f;
-    if (k < F && l < F && l != k) u = (mode == 1) ? 1.f : (R[l * F + k] + R[k * F + l]) * 0.5f;
-    out[i] = u;
+// dL/dz of BCE-with-logits with the loss normalised by `denom` (torch: (sigmoid(z) - y) * 1, then
+// divided by numel for reduction='mean'); optionally the loss sum (stable form) into *loss_sum.
+__global__ void __launch_bounds__(256) bce_grad_kernel(const float* __restrict__ z, const float* __restrict__ y,
+                                                       int64_t n, float denom, float* __restrict__ dz,
+                                                       float* __restrict__ loss_sum) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float l = 0.f;
+  if (i < n) {
+    const float x = z[i], t = y[i];
+    const float sg = 1.f / (1.f + expf(-x));
+    dz[i] = __fdiv_rn(__fsub_rn(sg, t), denom);
+    l = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+  }
+  if (loss_sum) {
+    for (int o = 32; o >= 1; o >>= 1) l += __shfl_xor(l, o);
+    __shared__ float ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = l;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(loss_sum, ((ws[0] + ws[1]) + ws[2]) + ws[3]);
   }
 }
 
@@ -706,9 +732,8 @@ __global__ void pack_fwfm_sym_kernel(const float* __restrict__ R, int F, int mod
 template <int D, int TPW>
 static hipError_t launch_bwd_t(const BwdArgs& a, size_t lds, hipStream_t s) {
   auto k = bwd_kernel<D, TPW>;
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {
+    hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
     if (e != hipSuccess) return e;
   }
   const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
@@ -747,9 +772,8 @@ hipError_t launch_reduce(const RedArgs& a, hipStream_t s) {
   const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
   if (a.F * a.D > kRedMaxFD || a.N > kRedMaxN || a.num * a.D > 512) return hipErrorInvalidValue;
   const size_t lds = sizeof(float) * (size_t)red_layout(a.F, a.D, a.N, a.num).total;
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(reduce_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {
+    hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(reduce_kernel), lds);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(reduce_kernel, dim3(grid), dim3(256), lds, s, a);
@@ -772,8 +796,7 @@ hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream
   if (a.chunk > 4 * 256) return hipErrorInvalidValue;
   const size_t lds = sizeof(float) * kPrivFloats;
   auto k = scatter_kernel<true>;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds);
+  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3(total_blocks), dim3(256), lds, s, a);
   return hipGetLastError();
@@ -793,16 +816,22 @@ hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, 
   return hipGetLastError();
 }
 
-hipError_t launch_pack_linear_t(const float* w, int N, int K, int KT, int NTc, float4* out, hipStream_t s) {
-  const int64_t total = (int64_t)KT * NTc * 64;
-  const unsigned grid = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(pack_linear_t_kernel, dim3(grid), dim3(256), 0, s, w, N, K, KT, NTc, out);
+hipError_t launch_adam_prep(AdamDevState* st, double lr, double b1, double b2, double eps, double wd, hipStream_t s) {
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, s, st, lr, b1, b2, eps, wd);
   return hipGetLastError();
 }
 
-hipError_t launch_pack_fwfm_sym(const float* R, int F, int mode, int MT, int S, float* out, hipStream_t s) {
-  const int total = MT * S * 64;
-  hipLaunchKernelGGL(pack_fwfm_sym_kernel, dim3((total + 255) / 256), dim3(256), 0, s, R, F, mode, MT, S, out);
+hipError_t launch_adam_dev(const AdamList& list, int total_blocks, const AdamDevState* st, hipStream_t s) {
+  if (total_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(total_blocks), dim3(256), 0, s, list, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_bce_grad(const float* z, const float* y, int64_t n, float denom, float* dz, float* loss_sum,
+                           hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bce_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z, y, n, denom, dz,
+                     loss_sum);
   return hipGetLastError();
 }
 

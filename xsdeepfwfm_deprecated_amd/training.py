@@ -15,6 +15,7 @@ Nothing here computes on the CPU: without the HIP library every entry point rais
 """
 from __future__ import annotations
 
+import ctypes
 import logging
 import math
 from time import time
@@ -23,6 +24,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import _lib
 from . import engine as _engine
 
 
@@ -127,6 +129,161 @@ class Adam(torch.optim.Optimizer):
                 for p, *_ in entries:
                     torch.autograd.graph.increment_version(p)  # in-place update behind torch's back
         return loss
+
+
+# --------------------------------------------------------------------------------------- fused step
+class FusedTrainStep:
+    """One reference training step -- fit()'s inner-loop body (:619-637): zero_grad, forward,
+    BCE-with-logits, backward, Adam(lr, weight_decay) -- as HIP launches on pre-built pointers, captured
+    once into a HIP graph and replayed (no per-step host work beyond the input copies).
+
+    Gradients and Adam moments live in flat device buffers (``p.grad`` are views into the gradient
+    buffer, so a data-parallel all-reduce is one call).  Adam's step counter and bias corrections, and
+    the dropout seed, are read from device memory, so every replay is a fresh step.  Under
+    torch.distributed the loss is normalised by the global batch and the step is split into two graphs
+    around an RCCL all-reduce of the gradient buffer."""
+
+    def __init__(self, model, batch_size, lr=1e-3, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8,
+                 use_graph=True, dist=None):
+        dev = model._device()
+        if dev.type != "cuda":
+            raise _lib.DfwfmError("FusedTrainStep runs only on a HIP device")
+        self.model, self.dev = model, dev
+        self.B = int(batch_size)
+        self.lr, self.wd, self.betas, self.eps = float(lr), float(weight_decay), tuple(betas), float(eps)
+        self.dist = dist
+        self.use_graph = use_graph
+        self.eng = model._sync_engine(dev)
+        self.L = _lib.lib()
+        params = [p for p in model.parameters() if p.requires_grad]
+        fields, dense = model._param_layout()
+        known = {id(t) for tup in fields for t in tup if t is not None}
+        known |= {id(v) for k, v in dense.items() if not isinstance(v, list) and v is not None}
+        known |= {id(t) for t in dense["lin_w"] + dense["lin_b"]}
+        if any(id(p) not in known for p in params):
+            raise NotImplementedError("FusedTrainStep: a trainable parameter outside the kernels' layout")
+        total = sum(p.numel() for p in params)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.state = torch.zeros(_lib.ADAM_STATE_BYTES // 8, dtype=torch.int64, device=dev)
+        views, off = {}, 0
+        adam = (_lib.dfwfm_adam_tensor * len(params))()
+        for i, p in enumerate(params):
+            n = p.numel()
+            g, m, v = (t[off:off + n].view_as(p) for t in (self.grad, self.exp_avg, self.exp_avg_sq))
+            p.grad = g
+            views[id(p)] = g
+            adam[i] = _lib.dfwfm_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n)
+            off += n
+        self.params, self.adam, self.n_adam = params, adam, len(params)
+        ptr = lambda t: None if t is None else views[id(t)].data_ptr()  # noqa: E731
+        self.fg = (_lib.dfwfm_field_grads * len(fields))(
+            *[_lib.dfwfm_field_grads(*[ptr(t) for t in tup]) for tup in fields])
+        H = len(dense["lin_w"])
+        self.gW = (ctypes.c_void_p * max(H, 1))(*[ptr(t) for t in dense["lin_w"]])
+        self.gB = (ctypes.c_void_p * max(H, 1))(*[ptr(t) for t in dense["lin_b"]])
+        self.grads = _lib.dfwfm_grads(self.fg, ptr(dense["field_cov"]), ptr(dense["fwfm_lin"]), ptr(dense["fm_1st"]),
+                                      ptr(dense["bias"]), self.gW if H else None, self.gB if H else None,
+                                      ptr(dense["fc_w"]))
+        # set_dense arguments (re-packed inside every step: Adam changes the weights)
+        d = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        self.pW = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in dense["lin_w"]])
+        self.pB = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in dense["lin_b"]])
+        self.dense_args = (d(dense["field_cov"]), d(dense["fwfm_lin"]), d(dense["fm_1st"]), d(dense["bias"]),
+                           self.pW if H else None, self.pB if H else None, d(dense["fc_w"]))
+        ncat, num = model.field_size - model.num, model.num
+        self.ncat, self.num = ncat, num
+        self.xi = torch.zeros(self.B, max(ncat, 1), dtype=torch.int64, device=dev)
+        self.xv = torch.zeros(self.B, max(num, 1), dtype=torch.float32, device=dev)
+        self.y = torch.zeros(self.B, dtype=torch.float32, device=dev)
+        self.out = torch.zeros(self.B, dtype=torch.float32, device=dev)
+        self.dlogit = torch.zeros(self.B, dtype=torch.float32, device=dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.drop_train = 0.0
+        if model.use_deep and model.is_deep_dropout:
+            self.drop_train = float(model.dropout_deep[0])
+        self.drop = self.drop_train
+        self.seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        _lib.check(self.L.dfwfm_set_step_source(self.eng.handle, ctypes.c_void_p(self.state.data_ptr())),
+                   "dfwfm_set_step_source")
+        self.graphs = None
+        self.steps = 0
+
+    def close(self):
+        if self.eng.handle is not None and self.eng.handle.value:
+            self.L.dfwfm_set_step_source(self.eng.handle, None)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _part1(self, n, denom):
+        L, st, h = self.L, self._stream(), self.eng.handle
+        self.grad.zero_()
+        _lib.check(L.dfwfm_model_set_dense(h, *self.dense_args, st), "dfwfm_model_set_dense")
+        _lib.check(L.dfwfm_train_forward(h, ctypes.c_void_p(self.xi.data_ptr()), self.xi.stride(0),
+                                         ctypes.c_void_p(self.xv.data_ptr()), self.xv.stride(0), n,
+                                         ctypes.c_void_p(self.out.data_ptr()), self.drop, self.seed, st),
+                   "dfwfm_train_forward")
+        _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(self.out.data_ptr()), ctypes.c_void_p(self.y.data_ptr()), n,
+                                    float(denom), ctypes.c_void_p(self.dlogit.data_ptr()),
+                                    ctypes.c_void_p(self.loss_sum.data_ptr()), st), "dfwfm_bce_grad")
+        _lib.check(L.dfwfm_backward(h, ctypes.c_void_p(self.dlogit.data_ptr()), ctypes.byref(self.grads), st),
+                   "dfwfm_backward")
+
+    def _part2(self):
+        b1, b2 = self.betas
+        _lib.check(self.L.dfwfm_adam_step_dev(self.adam, self.n_adam, self.lr, b1, b2, self.eps, self.wd,
+                                              ctypes.c_void_p(self.state.data_ptr()), self._stream()),
+                   "dfwfm_adam_step_dev")
+
+    def _allreduce(self):
+        if self.dist is not None:
+            self.dist.all_reduce(self.grad)
+
+    def _capture(self, denom):
+        """Two graphs: forward + backward, then Adam (an RCCL all-reduce runs between them under DP)."""
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g1, stream=s):
+                self._part1(self.B, denom)
+            with torch.cuda.graph(g2, stream=s):
+                self._part2()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        return g1, g2
+
+    def step(self, xi, xv, y, n_global=None):
+        """One step on device tensors xi [n, F-num] int64, xv [n, num] f32, y [n] f32 (n <= batch_size);
+        n_global = rows of the global batch under data parallelism (loss normaliser)."""
+        n = int(xi.shape[0])
+        if n > self.B:
+            raise ValueError(f"batch of {n} rows exceeds the step's {self.B}")
+        denom = float(max(n_global if n_global is not None else n, 1))
+        if n:
+            self.xi[:n].copy_(xi.reshape(n, -1))
+            if self.num:
+                self.xv[:n].copy_(xv[:, :self.num])
+            self.y[:n].copy_(y)
+        self.drop = self.drop_train if self.model.training else 0.0  # nn.Dropout is off in eval mode
+        full = n == self.B
+        if self.use_graph and full and self.steps >= 1:
+            if self.graphs is None or self._graph_key != (denom, self.drop):
+                self.graphs = self._capture(denom)
+                self._graph_key = (denom, self.drop)
+            self.graphs[0].replay()
+            self._allreduce()
+            self.graphs[1].replay()
+        else:
+            self._part1(n, denom)
+            self._allreduce()
+            self._part2()
+        self.steps += 1
+        self.eng._dense_key = None  # weights changed behind torch's version counters: re-pack on next use
+        return self.loss_sum
+
+    _graph_key = None
 
 
 # --------------------------------------------------------------------------------------- pruning
@@ -254,7 +411,14 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
         for p in model.parameters():
             dist.broadcast(p.data, 0)
     model.train()
-    optimizer = make_optimizer(model)
+    # Adam without distillation (the reference default) runs as a graph-replayed fused step;
+    # other optimizers / the KD loss go through autograd + the optimizer
+    fused = model.optimizer_type == "adam" and not teacher_model and getattr(model, "fused_fit", True)
+    bs = model.batch_size
+    gbs = bs * world
+    trainer = FusedTrainStep(model, bs, lr=model.learning_rate, weight_decay=model.weight_decay,
+                             dist=dist) if fused else None
+    optimizer = None if fused else make_optimizer(model)
     num_total, e1, e2, dnn, nz_r = _param_summary(model, log)
     log.info("========")
     log.info(f"Summation of feature sizes: {sum(model.feature_sizes):,}")
@@ -275,10 +439,9 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
     y_d = torch.as_tensor(y_train, dtype=torch.float32).to(device)
     train_result, valid_result = [], []
     n_iter = 0
-    bs = model.batch_size
-    gbs = bs * world
     for epoch in range(model.n_epochs):
         total_loss = 0.0
+        loss_mark = float(trainer.loss_sum.item()) if fused else 0.0
         batch_iter = x_size // gbs
         epoch_begin = batch_begin = time()
         teacher_outputs = None
@@ -297,27 +460,36 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
             lo = min(end, offset + rank * bs)
             hi = min(end, lo + bs)
             n_global = end - offset
-            optimizer.zero_grad()
-            if hi > lo:
-                xi, xv, yb = Xi_d[lo:hi], Xv_d[lo:hi], y_d[lo:hi]
-                outputs = model(xi, xv)
-                if teacher_model:
-                    tb = torch.as_tensor(teacher_outputs[i]).to(device)
-                    loss = model.loss_fn_kd(outputs, tb, yb)
-                else:
-                    # mean over the global batch: the rank's sum / n_global, summed over ranks below
-                    loss = F.binary_cross_entropy_with_logits(outputs, yb, reduction="sum") / n_global \
-                        if dist else F.binary_cross_entropy_with_logits(outputs, yb)
-                loss.backward()
+            xi, xv, yb = Xi_d[lo:hi], Xv_d[lo:hi], y_d[lo:hi]
+            if fused:
+                trainer.step(xi, xv, yb, n_global if dist else None)
             else:
-                loss = torch.zeros((), device=device)
-                for p in model.parameters():
-                    p.grad = torch.zeros_like(p)
-            allreduce_grads(model)
-            optimizer.step()
-            total_loss += loss.item()
+                optimizer.zero_grad()
+                if hi > lo:
+                    outputs = model(xi, xv)
+                    if teacher_model:
+                        tb = torch.as_tensor(teacher_outputs[i]).to(device)
+                        loss = model.loss_fn_kd(outputs, tb, yb)
+                    else:
+                        # mean over the global batch: the rank's sum / n_global, summed over ranks below
+                        loss = F.binary_cross_entropy_with_logits(outputs, yb, reduction="sum") / n_global \
+                            if dist else F.binary_cross_entropy_with_logits(outputs, yb)
+                    loss.backward()
+                else:
+                    loss = torch.zeros((), device=device)
+                    for p in model.parameters():
+                        p.grad = torch.zeros_like(p)
+                allreduce_grads(model)
+                optimizer.step()
+                if model.verbose:
+                    total_loss += loss.item()
             if model.verbose and i % 100 == 99:
-                ev = model.evaluate(xi, xv, yb)
+                if fused:  # mean per-batch loss over the last 100 steps, from the device loss sum
+                    cur = float(trainer.loss_sum.item())
+                    total_loss, loss_mark = (cur - loss_mark) / max(hi - lo, 1), cur
+                # (the reference's evaluate() leaves the model in eval mode -- dropout off -- for the
+                # rest of training, :627-630, :880-893; kept as is)
+                ev = model.evaluate(xi, xv, yb) if hi > lo else float("nan")
                 log.info("[%d, %5d] loss: %.6f metric: %.6f time: %.1f s" %
                          (epoch + 1, i + 1, total_loss / 100.0, ev, time() - batch_begin))
                 total_loss = 0.0
@@ -341,7 +513,8 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
                      (epoch + 1, valid_loss, valid_eval, valid_prauc, valid_rce,
                       100 - no_non_sparse * 100. / num_total, time() - epoch_begin))
         log.info("*" * 50)
-        model.train()
+        # no model.train() here: the reference's eval_by_batch leaves the model in eval mode, so from the
+        # second epoch on it trains without dropout (model/DeepFMs.py:694-714, :766); kept for parity
         perm = np.random.permutation(x_size)
         Xi_train, Xv_train, y_train = Xi_train[perm], Xv_train[perm], y_train[perm]
         pd = torch.as_tensor(perm).to(device)
