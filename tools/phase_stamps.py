@@ -41,8 +41,10 @@ n = _lib.lib().dfwfm_diag_stamps(m._engine.handle, buf, grid * 16,
 st = np.frombuffer(buf, dtype=np.uint64).reshape(grid, 16)[:n].astype(np.int64)
 names = ["stage (params, Xi/Xv)", "gather E + table first order", "shallow (fwlw, FwFM MFMA, sums)",
          "  . fwlw first order", "  . FwFM MFMA (wave 0)", "  . barrier wait", "  . first/second sums",
-         "MLP layer 1", "MLP layer 2", "MLP layer 3", "deep reduce + combine"]
-slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (3, 4), (4, 5), (5, 6), (6, 8)]
+         "MLP layer 1", "  . K loop (wave 0)", "  . epilogue (wave 0)", "  . barrier wait", "MLP layer 2",
+         "MLP layer 3", "deep reduce + combine"]
+slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (3, 4), (3, 12), (12, 13), (13, 4), (4, 5),
+         (5, 6), (6, 8)]
 tot = st[:, 8] - st[:, 0]
 print(f"workgroups {n}; total cycles median {np.median(tot):.0f} (p10 {np.percentile(tot, 10):.0f}, "
       f"p90 {np.percentile(tot, 90):.0f})")

@@ -112,7 +112,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB_PATH
     from concurrent.futures import ThreadPoolExecutor
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"] + os.environ.get("DFWFM_HIPCC_FLAGS", "").split()
     objs = [os.path.join(CSRC, os.path.splitext(s)[0] + ".o") for s in SOURCES]
 
     def compile_one(i):

@@ -19,6 +19,7 @@ struct dfwfm_model {
   int device;
   int F, D, num, H, N;
   int NT, NC0, SX, SY, TPW, MT, S, W0, KS;
+  int TPWF, tail;  // forward: full tiles per wave, split-tail mode (NT == 4*TPWF + 1); TPW = ceil(NT/4)
   int flags;
   size_t lds_bytes;
   // device state (owned)
@@ -171,11 +172,21 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   // one wave per SIMD; DFWFM_KSPLIT=2 runs two per SIMD splitting K (measured slower, kept for A/B)
   m->KS = 1;
   if (const char* ks = getenv("DFWFM_KSPLIT")) m->KS = atoi(ks) == 2 ? 2 : 1;
+  // 4k+1 output tiles (N = 400: 25): the last tile is split by K over the four waves instead of
+  // giving one SIMD an extra whole tile (DFWFM_NO_TAIL=1 disables it, for A/B)
+  m->TPWF = TPW;
+  m->tail = 0;
+  if (c.use_deep && m->KS == 1 && NT % 4 == 1 && NT >= 5 && m->NC0 >= 4 && m->NC0 <= 4 * kTailC &&
+      NT <= 4 * kTailC && !getenv("DFWFM_NO_TAIL")) {
+    m->TPWF = NT / 4;
+    m->tail = 1;
+  }
   const bool second = c.use_fwfm || c.use_fm;
   m->flags = (second ? kHasSecond : 0) | (c.use_deep ? kHasDeep : 0) |
              (c.use_fwlw ? kFoFwlw : kFoTables) | ((second && c.use_lw) ? kFoLw : 0) |
              ((second || c.use_deep) ? kNeedE : 0);
-  const LdsLayout L = lds_layout(F, D, m->MT, m->S, m->SX, m->SY, TPW > 0 ? TPW : 1, m->KS, c.use_deep != 0);
+  const LdsLayout L = lds_layout(F, D, m->MT, m->S, m->SX, m->SY, m->TPWF > 0 ? m->TPWF : 1, m->KS,
+                                 c.use_deep != 0, m->tail != 0);
   m->lds_bytes = sizeof(float) * (size_t)L.total;
   if (m->lds_bytes > 160 * 1024) {
     free_model(m);
@@ -359,6 +370,7 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.MT = m->MT;
   a.S = m->S;
   a.W0 = m->W0;
+  a.tail = m->tail;
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
@@ -421,7 +433,7 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
     }
     a.stamps = m->d_stamps;
   }
-  hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, m->KS, m->lds_bytes, (hipStream_t)stream);
+  hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, m->KS, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
 }
@@ -460,7 +472,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   a.drop_scale = 1.f / (1.f - dropout_p);
   a.seed = seed;
   a.seed_src = m->step_src;
-  hipError_t e = launch_forward(a, m->D, m->TPW > 0 ? m->TPW : 1, 1, m->lds_bytes, (hipStream_t)stream);
+  hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, 1, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
   m->trained = true;
   return DFWFM_OK;

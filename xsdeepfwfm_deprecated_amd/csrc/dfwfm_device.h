@@ -17,6 +17,15 @@ __device__ __forceinline__ void stamp(uint64_t* st, int slot, int tid) {
   if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
 }
 
+// sum over the 16 lanes of an aligned 16-lane group
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 8);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 1);
+  return v;
+}
+
 // constant-rate (100 MHz) clock, comparable across XCDs: workgroup start/end spread
 __device__ __forceinline__ void stamp_rt(uint64_t* st, int slot, int tid) {
   if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memrealtime();
@@ -121,10 +130,12 @@ struct LayerStream {
 
 // K loop of one layer, entered with chunks 0 and 1 already in b0 / b1.  Weight fragments rotate
 // through three register sets, each refilled two chunks ahead of its MFMAs (the loop is unrolled
-// by 3 so no set is ever copied: a copy makes hipcc wait for the load it copies); the activation
-// fragment is read one chunk ahead.  Within a step the refill loads are interleaved with the first
-// MFMAs (sched_group_barrier: 2 MFMA, 1 load, ...), and a sched_barrier closes the step so hipcc
-// cannot sink them to their use.
+// by 3 so no set is ever copied: a copy makes hipcc wait for the load it copies).  The activation
+// fragments rotate with them (three float4, read from LDS two chunks ahead): with only two, every
+// other step's read targeted the register its own MFMAs were still reading, so it issued behind
+// them and the next step's first MFMA waited out the LDS latency.  Within a step the LDS read goes
+// first, then the refill loads interleave with the MFMAs (sched_group_barrier: 2 MFMA, 1 load,
+// ...), and a sched_barrier closes the step so hipcc cannot sink them to their use.
 template <int TPW, int KS>
 __device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __restrict__ act, int SA,
                                            const LayerStream<TPW, KS>& ls, f32x4 (&b0)[TPW],
@@ -135,31 +146,68 @@ __device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __res
   if (n == 0) return;
   const int voff = lane * 16;
   const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
-  float4 a = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(0));
-#define DFWFM_STEP(X, Z, i)                                                             \
-  {                                                                                     \
-    const float4 an = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk((i) + 1));  \
-    ls.load(Z, ls.chunk((i) + 2), voff);                                                \
-    mfma_chunk<TPW>(acc, a, X);                                                         \
-    for (int q = 0; q < TPW; ++q) {                                                     \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                \
-    }                                                                                   \
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TPW, 0);                            \
-    __builtin_amdgcn_sched_barrier(0);                                                  \
-    a = an;                                                                             \
+  float4 a0 = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(0));
+  float4 a1 = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(1));
+  float4 a2;
+#define DFWFM_STEP(X, AX, Z, AZ, i)                                                    \
+  {                                                                                    \
+    AZ = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk((i) + 2));              \
+    ls.load(Z, ls.chunk((i) + 2), voff);                                               \
+    mfma_chunk<TPW>(acc, AX, X);                                                       \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                 \
+    for (int q = 0; q < TPW; ++q) {                                                    \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                               \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                               \
+    }                                                                                  \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TPW, 0);                           \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
   }
   int i = 0;
   for (; i + 3 <= n; i += 3) {
-    DFWFM_STEP(b0, b2, i);
-    DFWFM_STEP(b1, b0, i + 1);
-    DFWFM_STEP(b2, b1, i + 2);
+    DFWFM_STEP(b0, a0, b2, a2, i);
+    DFWFM_STEP(b1, a1, b0, a0, i + 1);
+    DFWFM_STEP(b2, a2, b1, a1, i + 2);
   }
-  if (i < n) DFWFM_STEP(b0, b2, i);
-  if (i + 1 < n) DFWFM_STEP(b1, b0, i + 1);
+  if (i < n) DFWFM_STEP(b0, a0, b2, a2, i);
+  if (i + 1 < n) DFWFM_STEP(b1, a1, b0, a0, i + 1);
 #undef DFWFM_STEP
 }
 
+// The split tail tile: when the layer has 4*TPW + 1 output tiles, tile T = 4*TPW is shared by the
+// four waves, wave g taking K chunks [NC*g/4, NC*(g+1)/4) of it, so every SIMD carries 6.25 tiles
+// instead of one carrying 7.  All of a wave's tail fragments are loaded with the layer's preload
+// (kTailC <= 8 chunks per wave, NC <= 32) and consumed after the main K loop.
+struct TailStream {
+  int sbase, c_lo, cnt;
+  __device__ __forceinline__ void init(int layer_off, int NC, int T, int g) {
+    sbase = __builtin_amdgcn_readfirstlane((layer_off + T * NC * 64) * 16);
+    c_lo = (NC * g) >> 2;
+    cnt = ((NC * (g + 1)) >> 2) - c_lo;
+  }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, f32x4 (&tw)[kTailC], int voff) const {
+#pragma unroll
+    for (int u = 0; u < kTailC; ++u)
+      if (u < cnt)
+        tw[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, sbase + (c_lo + u) * 1024, 0));
+  }
+  // this wave's partial product of the tail tile (two accumulators: no back-to-back dependent MFMAs)
+  __device__ __forceinline__ f32x4 mma(const float* __restrict__ act, int SA, const f32x4 (&tw)[kTailC], int lane) const {
+    const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
+    f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+    for (int u = 0; u < kTailC; ++u) {
+      if (u < cnt) {
+        const float4 a = *reinterpret_cast<const float4*>(arow + 16 * (c_lo + u));
+        f32x4& c = (u & 1) ? a1 : a0;
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, tw[u].x, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, tw[u].y, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, tw[u].z, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, tw[u].w, c, 0, 0, 0);
+      }
+    }
+    return a0 + a1;
+  }
+};
 
 // Counter-based dropout mask (deep tower; reference nn.Dropout(0.5), model/DeepFMs.py:260-282):
 // keep element (layer, row, col) of a step iff a 24-bit hash of (seed, layer, row, col) >= p.

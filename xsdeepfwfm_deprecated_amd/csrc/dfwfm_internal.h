@@ -14,6 +14,7 @@ constexpr int kBM = 16;     // samples per workgroup = one 16-row MFMA tile
 constexpr int kMaxTPW = 8;  // MLP output tiles per wave group => deep_nodes <= 4*8*16 = 512
 constexpr int kMaxMT = 4;   // FwFM row tiles => field_size <= 64
 constexpr int kStampSlots = 16;  // diagnostic phase stamps per workgroup
+constexpr int kTailC = 8;        // split tail tile: K chunks per wave (layer widths <= 4*8*16 = 512)
 
 // flags
 constexpr int kHasSecond = 1;  // FwFM / FM second order
@@ -63,6 +64,7 @@ struct FwdArgs {
   int32_t MT, S;       // FwFM: row tiles ceil(F/16), K steps ceil(F/4)
   int32_t SX, SY;      // LDS row strides (floats) of the two activation tiles
   int32_t W0;          // E-tile columns that must be valid (zero padded past F*D)
+  int32_t tail;        // 1: NT == 4*TPW + 1 and tile 4*TPW is split by K over the four waves
   int32_t flags;
   uint64_t* stamps;    // diagnostics only: [grid][kStampSlots] shader-clock stamps, normally null
   // training (flags & kTrain): activations kept for the backward
@@ -78,13 +80,13 @@ struct FwdArgs {
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.
 struct LdsLayout {
-  int desc, lw, fwlw, upk, bufX, bufY, red, fo, part2, dsum, fs, total;
+  int desc, lw, fwlw, upk, bufX, bufY, red, tailr, fo, part2, dsum, fs, total;
 };
 
 __host__ __device__ inline int r4(int x) { return (x + 3) & ~3; }
 
 __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int SX, int SY, int TPW, int KS,
-                                                bool deep) {
+                                                bool deep, bool tail) {
   LdsLayout L;
   int o = 0;
   L.desc = o;  o += r4(14 * F);
@@ -94,6 +96,7 @@ __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int
   L.bufX = o;  o += kBM * SX;
   L.bufY = o;  o += deep ? kBM * SY : 0;
   L.red = o;   o += (deep && KS == 2) ? 4 * TPW * 64 * 4 : 0;
+  L.tailr = o; o += (deep && tail) ? 4 * 64 * 4 + kBM : 0;  // partials + per-row deep sums of the tail
   L.fo = o;    o += kBM * r4(F);
   L.part2 = o; o += r4(kBM * D);
   L.dsum = o;  o += 4 * kBM;

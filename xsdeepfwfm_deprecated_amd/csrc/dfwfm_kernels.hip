@@ -54,7 +54,8 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   const int flags = p.flags;
   const bool deep = (flags & kHasDeep) != 0;
   const int Fp = r4(F);
-  const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep);
+  const bool tail = KS == 1 && p.tail != 0;
+  const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep, tail);
   FieldDev* desc = reinterpret_cast<FieldDev*>(smem + L.desc);
   float* lw_s = smem + L.lw;
   float* fwlw_s = smem + L.fwlw;
@@ -62,6 +63,7 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   float* bufX = smem + L.bufX;
   float* bufY = smem + L.bufY;
   f32x4* red = reinterpret_cast<f32x4*>(smem + L.red);
+  float* tailr = smem + L.tailr;  // [4 waves][64 lanes][4] partial products of the tail tile
   float* fo = smem + L.fo;
   float* part2 = smem + L.part2;
   float* dsum = smem + L.dsum;
@@ -73,9 +75,16 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   const int kh = wave >> 2; // MLP K half (KS == 2)
 
   LayerStream<TPW, KS> ls;
+  // weight fragments: three register sets, prefetch distance 2 chunks (a fourth set / distance 3
+  // measured slower)
   f32x4 wb0[TPW], wb1[TPW], wb2[TPW];
+#define DFWFM_PRELOAD(LS) (LS).preload(wb0, wb1, lane * 16)
+#define DFWFM_KLOOP(ACC, IN, SA, LS) mlp_k_loop<TPW, KS>(ACC, IN, SA, LS, wb0, wb1, wb2, lane)
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float4*>(p.wpack), (short)0, p.wpack_bytes, 0x00020000);
+  TailStream ts;
+  f32x4 tw[kTailC];
+  constexpr int TT = 4 * TPW;  // the tail tile (when p.tail)
 
   // ---- phase 0: field descriptors -> LDS; this thread's Xi / Xv; shallow parameters in flight --
   // Every load is issued before any is consumed (a load-then-store loop waits one round trip per
@@ -196,7 +205,11 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
     // during the combine, the shallow part and the barriers
     if (deep) {
       ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
-      ls.preload(wb0, wb1, lane * 16);
+      DFWFM_PRELOAD(ls);
+      if (tail) {
+        ts.init(0, p.NC0, TT, g);
+        ts.load(wrsrc, tw, lane * 16);
+      }
     }
     // ... the shallow parameters go to LDS while the row loads are in flight ...
 #pragma unroll
@@ -398,13 +411,26 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
       wf[j] = last ? p.fc[n] : 0.f;
     }
 
+    float bn_t = 0.f, wf_t = 0.f;
+    if (tail) {
+      const int n = TT * 16 + (lane & 15);
+      bn_t = bias[n];
+      wf_t = last ? p.fc[n] : 0.f;
+    }
+
     f32x4 acc[TPW];
-    mlp_k_loop<TPW, KS>(acc, in, SA, ls, wb0, wb1, wb2, lane);
+    DFWFM_KLOOP(acc, in, SA, ls);
+    if (tail) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.mma(in, SA, tw, lane);
+    if (h == 0) stamp(p.stamps, 12, tid);
     // next layer's first chunks go out now, ahead of this layer's epilogue and barrier
     layer_off += p.NT * NC * 64;
     if (!last) {
       ls.init(wrsrc, layer_off, p.NT, p.NT, g, kh);
-      ls.preload(wb0, wb1, lane * 16);
+      DFWFM_PRELOAD(ls);
+      if (tail) {
+        ts.init(layer_off, p.NT, TT, g);
+        ts.load(wrsrc, tw, lane * 16);
+      }
     }
     if constexpr (KS == 2) {
       if (kh == 1) {
@@ -451,7 +477,31 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
         }
       }
     }
+    if (h == 0) stamp(p.stamps, 13, tid);
     __syncthreads();
+    if (tail) {
+      // the tail tile: wave g finishes row (lane>>4)*4 + g of it from the four partial products
+      const int n = TT * 16 + (lane & 15);
+      const bool valid = n < p.N;
+      const int rr = row0 + g;
+      const float* tp = tailr + lane * 4 + g;
+      const float sum = ((tp[0] + tp[256]) + tp[512]) + tp[768];
+      float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
+      if constexpr (train) {
+        const int64_t row = b0 + rr;
+        if (drop) v = dropout_keep(hseed, h + 1, row, n, p.drop_p) ? v * p.drop_scale : 0.f;
+        if (valid && row < p.batch) p.sv_x[h + 1][row * p.N + n] = v;
+      }
+      if (!last) {
+        outa[rr * SO + n] = v;
+        __syncthreads();
+      } else {
+        // the tail's share of deep[b] for row rr, summed over its 16 columns; added last in the final
+        // combine, so a row's logit does not depend on its slot in the tile
+        const float c = sum16(v * wf_t);
+        if ((lane & 15) == 0) tailr[4 * 64 * 4 + rr] = c;
+      }
+    }
     stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
   }
 
@@ -473,7 +523,8 @@ __global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
   }
   __syncthreads();
   if (tid < kBM && b0 + tid < p.batch) {
-    const float deepv = ((dsum[tid] + dsum[kBM + tid]) + dsum[2 * kBM + tid]) + dsum[3 * kBM + tid];
+    float deepv = ((dsum[tid] + dsum[kBM + tid]) + dsum[2 * kBM + tid]) + dsum[3 * kBM + tid];
+    if (tail) deepv += tailr[4 * 64 * 4 + tid];
     p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
   stamp(p.stamps, 8, tid);

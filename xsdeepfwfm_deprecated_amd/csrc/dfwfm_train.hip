@@ -44,15 +44,6 @@ size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY) {
   return sizeof(float) * (size_t)bwd_layout(F, D, MT, S, SX, SY).total;
 }
 
-// sum over the 16 lanes of an aligned 16-lane group
-__device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 8);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 1);
-  return v;
-}
-
 template <int D, int TPW>
 __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
   constexpr int NTH = 256;
