@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--inputs", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
+                         "batch's workgroup shares each CU, hiding the gather / FwFM phases)")
     return ap.parse_args()
 
 
@@ -99,73 +102,96 @@ def main():
         else:
             xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=seed)
         batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
-    out = torch.empty(BATCH, dtype=torch.float32, device=dev)
+    S = max(1, a.streams)
+    outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
 
     with torch.no_grad():
         eng = model._sync_engine(dev)
-        stream = torch.cuda.Stream(dev)
-        stream.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(stream):
-            def step(i):
-                xi, xv = batches[i % n_bufs]
-                eng.forward(xi, xv, out)
+        streams = [torch.cuda.Stream(dev) for _ in range(S)]
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream(dev))
 
-            # G consecutive forwards per captured graph (launch cost amortised: a single-kernel
-            # replay is host-bound at ~10-16 us); a remainder graph keeps the count at exactly K.
-            G = max(1, min(a.graph_steps, a.steps))
-            graphs = None
-            if not a.no_graph:
-                def capture(n):
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=stream):
-                        for i in range(n):
-                            step(i)
-                    return g
-                step(0)  # initialise everything outside the capture
-                graphs = {G: capture(G)}
-                if a.steps % G:
-                    graphs[a.steps % G] = capture(a.steps % G)
-                if a.warmup % G:
-                    graphs.setdefault(a.warmup % G, capture(a.warmup % G))
+        def step(i, k):
+            xi, xv = batches[(i + k) % n_bufs]
+            eng.forward(xi, xv, outs[k])
 
-            def run_n(n):
-                if graphs is None:
+        # G consecutive forwards per captured graph (launch cost amortised: a single-kernel
+        # replay is host-bound at ~10-16 us); a remainder graph keeps the count at exactly K.
+        # With S streams each stream replays its own graphs: S batches in flight at once.
+        G = max(1, min(a.graph_steps, a.steps))
+        graphs = None
+        if not a.no_graph:
+            def capture(n, k):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=streams[k]):
                     for i in range(n):
-                        step(i)
-                    return
-                for _ in range(n // G):
-                    graphs[G].replay()
-                if n % G:
-                    graphs[n % G].replay()
+                        step(i, k)
+                return g
+            for k in range(S):
+                with torch.cuda.stream(streams[k]):
+                    step(0, k)  # initialise everything outside the capture
+            graphs = []
+            for k in range(S):
+                gk = {G: capture(G, k)}
+                if a.steps % G:
+                    gk[a.steps % G] = capture(a.steps % G, k)
+                if a.warmup % G:
+                    gk.setdefault(a.warmup % G, capture(a.warmup % G, k))
+                graphs.append(gk)
 
-            run_n(a.warmup)
-            stream.synchronize()
-            if world > 1:
-                torch.distributed.barrier()
-            torch.cuda.synchronize(dev)
-            t0 = torch.cuda.Event(enable_timing=True)
-            t1 = torch.cuda.Event(enable_timing=True)
-            wall0 = time.perf_counter()
-            t0.record(stream)
-            run_n(a.steps)
-            t1.record(stream)
-            stream.synchronize()
-            torch.cuda.synchronize(dev)
-            wall = time.perf_counter() - wall0
-            if world > 1:
-                torch.distributed.barrier()
+        def run_n(n):
+            for k in range(S):
+                with torch.cuda.stream(streams[k]):
+                    if graphs is None:
+                        for i in range(n):
+                            step(i, k)
+                        continue
+                    for _ in range(n // G):
+                        graphs[k][G].replay()
+                    if n % G:
+                        graphs[k][n % G].replay()
+
+        run_n(a.warmup)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        # per-stream events: a launch's duration while S run side by side (what rocprofv3 reports)
+        s0 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
+        s1 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
+        wall0 = time.perf_counter()
+        t0.record(streams[0])
+        for k, st in enumerate(streams):
+            if k:
+                st.wait_stream(streams[0])
+            s0[k].record(st)
+        run_n(a.steps)
+        for k, st in enumerate(streams):
+            s1[k].record(st)
+            if k:
+                streams[0].wait_stream(st)
+        t1.record(streams[0])
+        streams[0].synchronize()
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - wall0
+        if world > 1:
+            torch.distributed.barrier()
     ms = t0.elapsed_time(t1)
+    launch_ms = sum(s0[k].elapsed_time(s1[k]) for k in range(S)) / (S * a.steps)
     if world > 1:
         t = torch.tensor([ms], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         ms = float(t.item())
 
-    ms_per_step = ms / a.steps
-    value = world * BATCH * a.steps / (ms / 1e3)
+    ms_per_step = ms / (a.steps * S)
+    value = world * S * BATCH * a.steps / (ms / 1e3)
     flops, bytes_ = algorithmic_counts(cfg)
-    t_launch = ms_per_step / 1e3
-    achieved_tf = flops * BATCH / t_launch / 1e12
-    achieved_gbs = bytes_ * BATCH / t_launch / 1e9
+    # achieved = algorithmic FLOP of one launch / its duration, times the launches in flight (each of
+    # the S concurrent launches takes ~S x the per-batch time): the aggregate rate over the timed region
+    achieved_tf = flops * BATCH * S / (launch_ms / 1e3) / 1e12
+    achieved_gbs = bytes_ * BATCH * S / (launch_ms / 1e3) / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -184,10 +210,12 @@ def main():
                                f"batch {BATCH} per GPU",
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
-                   "launch": "eager" if a.no_graph else f"hipGraph replay, {min(a.graph_steps, a.steps)} forwards per graph"},
+                   "launch": ("eager" if a.no_graph else f"hipGraph replay, {min(a.graph_steps, a.steps)} forwards per graph")
+                             + (f", {S} streams (batches in flight)" if S > 1 else "")},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "traffic": traffic,
-                     "kernel": "dfwfm::fwd_kernel<10,7>", "flops_per_sample": flops, "units_per_launch": BATCH},
+                     "kernel": "dfwfm::fwd_kernel<10,6,1,false>", "flops_per_sample": flops,
+                     "units_per_launch": BATCH, "launch_us": round(launch_ms * 1e3, 3), "launches_in_flight": S},
         "roofline_hbm": {"achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "bytes_per_sample": bytes_},
         "wall_s": round(wall, 4),

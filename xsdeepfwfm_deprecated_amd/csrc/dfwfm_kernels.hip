@@ -38,8 +38,13 @@ namespace dfwfm {
 // ---------------------------------------------------------------------------
 // TRAIN: the training-step variant (activations saved, dropout); compiled separately so the inference
 // kernel carries none of it
+#ifndef DFWFM_FWD_WPE
+#define DFWFM_FWD_WPE 2  // register budget of two waves per SIMD (<= 256 per lane): a second batch's
+                         // workgroup fits beside this one (stream-level overlap)
+#endif
 template <int D, int TPW, int KS, bool TRAIN>
-__global__ void __launch_bounds__(256 * KS) fwd_kernel(FwdArgs p) {
+__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(DFWFM_FWD_WPE)))
+fwd_kernel(FwdArgs p) {
   constexpr int NTH = 256 * KS;
   constexpr int NW = 4 * KS;
   constexpr int RPT = (kBM * 64 + NTH - 1) / NTH;  // gather rows per thread (F <= 64)
