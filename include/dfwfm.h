@@ -187,6 +187,27 @@ int dfwfm_adam_step_dev(const dfwfm_adam_tensor* tensors, int32_t n, double lr, 
 int dfwfm_bce_grad(const float* logits, const float* labels, int64_t n, double denom, float* dlogit,
                    float* loss_sum, void* stream);
 
+/* ---- magnitude pruning (reference model/DeepFMs.py:647-673, binary_search_threshold :807-823) ----
+ * The threshold whose fraction of |x| < threshold (compared in f32) hits `target`, found by the
+ * reference's own bisection on (0, 100) -- same rounds, same result -- but from one radix sort of the
+ * magnitudes instead of up to 101 passes with a host sync each.  Runs on `stream`; the threshold is
+ * written to device memory (`thr_dev`, one double) and never read back by the library. */
+typedef struct {
+  const float* values;  /* device                                                                  */
+  int64_t numel;
+  int32_t sym_f;        /* 0: |values|; F > 0: values is F x F and the magnitudes are |(W + W^T)/2| */
+  int32_t reserved;
+} dfwfm_prune_source;
+
+/* Device workspace bytes dfwfm_prune_threshold needs for `numel` magnitudes in total. */
+int64_t dfwfm_prune_workspace_bytes(int64_t numel);
+/* Threshold over the concatenation of n sources (e.g. all second-order tables, :652-656). */
+int dfwfm_prune_threshold(const dfwfm_prune_source* sources, int32_t n, double target, double* thr_dev,
+                          void* workspace, int64_t workspace_bytes, void* stream);
+/* values[i] = 0 where the magnitude (as in the source) < threshold; sym_f > 0 zeroes W[k][l] where
+ * |(W[k][l] + W[l][k]) / 2| < threshold, computed from the unmodified matrix (:666-670). */
+int dfwfm_prune_apply(float* values, int64_t numel, int32_t sym_f, const double* thr_dev, void* stream);
+
 /* Synchronises `stream`, returns the sticky error-flag word and clears it. */
 int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream);
 

@@ -28,8 +28,8 @@ def test_header_declares_expected_api():
     assert header_functions() == sorted([
         "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_bce_grad",
         "dfwfm_diag_stamps", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy",
-        "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_read_error_flag", "dfwfm_set_step_source",
-        "dfwfm_train_forward"])
+        "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_prune_apply", "dfwfm_prune_threshold",
+        "dfwfm_prune_workspace_bytes", "dfwfm_read_error_flag", "dfwfm_set_step_source", "dfwfm_train_forward"])
 
 
 def test_library_exports_every_header_symbol(built):
@@ -55,6 +55,10 @@ def test_abi_version_and_error_string(built):
     assert L.dfwfm_bce_grad(None, None, 4, 4.0, None, None, None) == -1
     assert L.dfwfm_bce_grad(None, None, 0, 0.0, None, None, None) == -1  # denom > 0
     assert L.dfwfm_set_step_source(None, None) == -1
+    assert L.dfwfm_prune_threshold(None, 0, 0.5, None, None, 0, None) == -1
+    assert L.dfwfm_prune_apply(None, 4, 0, None, None) == -1
+    assert L.dfwfm_prune_workspace_bytes(1000) >= 8000  # host-only query (hipcub sizing, no launch)
+    assert ctypes.sizeof(built.dfwfm_prune_source) == 24
 
 
 def test_struct_layouts_match_header(built):

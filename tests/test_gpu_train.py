@@ -227,3 +227,54 @@ def test_fit_fused_matches_autograd_fit(gpu):
         tr, _ = m.fit(xi.reshape(-1, 26, 1), xv, y, [], [], [])
         res.append(tr)
     assert abs(res[0][-1] - res[1][-1]) < 2e-3, res
+
+
+def _ref_prune(params, adaptive, emb_r, emb_corr):
+    """The reference's pruning loop (:647-673) on CPU copies, with binary_search_threshold (:807-823)."""
+    from xsdeepfwfm_deprecated_amd.training import binary_search_threshold
+    out = {k: torch.from_numpy(v.copy()) for k, v in params.items()}
+    stacked = torch.cat([v for k, v in out.items() if "fm_2nd_embeddings" in k], 0)
+    emb_thr = binary_search_threshold(stacked, adaptive * emb_r, stacked.numel())
+    thr = {"emb": emb_thr}
+    for k, v in out.items():
+        if "fm_2nd_embeddings" in k:
+            v[v.abs() < emb_thr] = 0
+        if "linear" in k and "weight" in k:
+            t = binary_search_threshold(v, adaptive, v.numel())
+            thr[k] = t
+            v[v.abs() < t] = 0
+        if k == "field_cov.weight":
+            symm = 0.5 * (v + v.t())
+            t = binary_search_threshold(symm, adaptive * emb_corr, v.numel())
+            thr[k] = t
+            v[symm.abs() < t] = 0
+    return out, thr
+
+
+@pytest.mark.parametrize("name,adaptive", [("train_deepfwfm_fwlw", 0.3), ("train_qr_mult", 0.55),
+                                           ("train_small_mlp", 0.9)])
+def test_device_pruning_matches_reference_bisection(gpu, name, adaptive):
+    """prune_step on the device zeroes exactly what the reference's host bisection zeroes."""
+    from xsdeepfwfm_deprecated_amd.training import prune_step
+    cfg, params, *_ = load_train_golden(name)
+    m = build(cfg, params, gpu)
+    prune_step(m, adaptive, prune_fm=1, prune_r=1, prune_deep=1, emb_r=0.444, emb_corr=1.0)
+    torch.cuda.synchronize()
+    ref, _ = _ref_prune(params, adaptive, 0.444, 1.0)
+    for k, p in m.named_parameters():
+        assert torch.equal(p.detach().cpu(), ref[k]), k
+
+
+def test_device_threshold_equals_reference_value(gpu):
+    from xsdeepfwfm_deprecated_amd.training import DevicePruner, binary_search_threshold
+    g = torch.Generator().manual_seed(7)
+    pr = DevicePruner(gpu)
+    for n, scale, target in [(1000, 0.01, 0.4), (100000, 1.0, 0.9), (37, 3.0, 0.2), (250000, 1e-3, 0.05)]:
+        x = torch.randn(n, generator=g) * scale
+        ref = binary_search_threshold(x, target, n)
+        got = pr.threshold([(x.to(gpu), 0)], target).item()
+        assert got == ref, (n, got, ref)
+    # symmetric R
+    W = torch.randn(39, 39, generator=g) * 0.2
+    ref = binary_search_threshold(0.5 * (W + W.t()), 0.7, W.numel())
+    assert pr.threshold([(W.to(gpu), 39)], 0.7).item() == ref

@@ -68,25 +68,6 @@ def test_binary_search_threshold_hits_target():
     assert abs((w.abs() < thr).float().mean().item() - 0.4) < 1e-3
 
 
-def test_prune_step_masks_like_reference():
-    """prune_step zeroes what the reference's loop zeroes (:647-673): emb by a shared threshold, each
-    linear weight to the target rate, R by its symmetric part (so the mask is symmetric)."""
-    from xsdeepfwfm_deprecated_amd import DeepFMs
-    from conftest import model_kwargs
-    cfg, params, *_ = load_train_golden("train_small_mlp")
-    m = DeepFMs(**model_kwargs(cfg))
-    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
-    from xsdeepfwfm_deprecated_amd.training import prune_step
-    prune_step(m, 0.5, prune_fm=1, prune_r=1, prune_deep=1, emb_r=0.444, emb_corr=1.0)
-    R = m.field_cov.weight.detach()
-    assert torch.equal(R == 0, (R == 0).t())
-    for i in range(1, cfg["h_depth"] + 1):
-        w = getattr(m, f"net_1_linear_{i}").weight
-        assert abs((w == 0).float().mean().item() - 0.5) < 2e-3
-    stacked = torch.cat([p.detach().reshape(-1) for n, p in m.named_parameters() if "fm_2nd_embeddings" in n])
-    assert abs((stacked == 0).float().mean().item() - 0.222) < 2e-3
-
-
 def _dp_worker(rank, world, port, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"

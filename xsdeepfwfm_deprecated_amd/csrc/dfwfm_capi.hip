@@ -787,6 +787,45 @@ int dfwfm_bce_grad(const float* z, const float* y, int64_t n, double denom, floa
   return e == hipSuccess ? DFWFM_OK : hip_fail(e, "bce launch");
 }
 
+int64_t dfwfm_prune_workspace_bytes(int64_t numel) {
+  if (numel <= 0 || numel > 0x7fffffff) return 0;
+  return (int64_t)prune_workspace_bytes(numel);
+}
+
+int dfwfm_prune_threshold(const dfwfm_prune_source* src, int32_t n, double target, double* thr_dev, void* ws,
+                          int64_t ws_bytes, void* stream) {
+  if (!src || n <= 0 || !thr_dev || !ws) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (n > kMaxPruneSrc) return fail(DFWFM_ERR_UNSUPPORTED, "more than %d pruning sources", kMaxPruneSrc);
+  PruneList L;
+  memset(&L, 0, sizeof L);
+  int64_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!src[i].values || src[i].numel <= 0) return fail(DFWFM_ERR_INVALID_ARG, "source %d is empty", i);
+    if (src[i].sym_f < 0 || src[i].sym_f > 64 || (src[i].sym_f > 0 && (int64_t)src[i].sym_f * src[i].sym_f != src[i].numel))
+      return fail(DFWFM_ERR_INVALID_ARG, "source %d: sym_f %d does not match numel", i, src[i].sym_f);
+    L.s[i].p = src[i].values;
+    L.s[i].numel = src[i].numel;
+    L.s[i].offset = off;
+    L.s[i].sym_f = src[i].sym_f;
+    off += src[i].numel;
+  }
+  L.n = n;
+  if (off > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "more than 2^31 magnitudes");
+  if (ws_bytes < (int64_t)prune_workspace_bytes(off))
+    return fail(DFWFM_ERR_INVALID_ARG, "workspace of %lld bytes < %lld", (long long)ws_bytes,
+                (long long)prune_workspace_bytes(off));
+  hipError_t e = launch_prune_threshold(L, target, thr_dev, ws, (size_t)ws_bytes, (hipStream_t)stream);
+  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "prune threshold");
+}
+
+int dfwfm_prune_apply(float* values, int64_t numel, int32_t sym_f, const double* thr_dev, void* stream) {
+  if (!values || !thr_dev || numel < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (sym_f < 0 || sym_f > 64 || (sym_f > 0 && (int64_t)sym_f * sym_f != numel))
+    return fail(DFWFM_ERR_INVALID_ARG, "sym_f %d does not match numel", sym_f);
+  hipError_t e = launch_prune_apply(values, numel, sym_f, thr_dev, (hipStream_t)stream);
+  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "prune apply");
+}
+
 int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream) {
   if (!m || !host || n < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
   if (!m->d_stamps) return fail(DFWFM_ERR_STATE, "no stamps recorded (set DFWFM_DIAG_STAMPS=1)");

@@ -251,6 +251,24 @@ struct PackList {
   int32_t n;
 };
 
+// Pruning sources: magnitudes of p (sym_f > 0: of (W + W^T)/2 for an F x F matrix) at keys[offset..]
+struct PruneSrc {
+  const float* p;
+  int64_t numel;
+  int64_t offset;
+  int32_t sym_f;
+  int32_t pad_;
+};
+constexpr int kMaxPruneSrc = 96;  // the list is a kernel argument (< 4 KiB)
+struct PruneList {
+  PruneSrc s[kMaxPruneSrc];
+  int32_t n;
+};
+size_t prune_workspace_bytes(int64_t n);
+hipError_t launch_prune_threshold(const PruneList& L, double target, double* d_thr, void* ws, size_t ws_bytes,
+                                  hipStream_t s);
+hipError_t launch_prune_apply(float* p, int64_t numel, int sym_f, const double* d_thr, hipStream_t s);
+
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);

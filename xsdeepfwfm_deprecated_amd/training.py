@@ -305,23 +305,67 @@ def binary_search_threshold(param, target_percent, total_no):
     return mid
 
 
+class DevicePruner:
+    """The reference's magnitude pruning on the device (C ABI dfwfm_prune_*): one radix sort per
+    threshold plus the reference's own bisection replayed on the sorted magnitudes -- the same
+    thresholds and masks as binary_search_threshold, without its up-to-101 host-synchronised passes."""
+
+    def __init__(self, device):
+        self.device = device
+        self.ws = torch.empty(0, dtype=torch.uint8, device=device)
+        self.thr = torch.zeros(1, dtype=torch.float64, device=device)
+        self.L = _lib.lib()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def threshold(self, sources, target):
+        """sources: [(tensor, sym_f)]; returns a 1-element float64 device tensor (not synchronised)."""
+        arr = (_lib.dfwfm_prune_source * len(sources))()
+        total = 0
+        for i, (t, sym) in enumerate(sources):
+            if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+                raise RuntimeError("dfwfm pruning: sources must be contiguous float32 HIP tensors")
+            arr[i] = _lib.dfwfm_prune_source(t.data_ptr(), t.numel(), int(sym), 0)
+            total += t.numel()
+        need = int(self.L.dfwfm_prune_workspace_bytes(total))
+        if self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        thr = torch.empty(1, dtype=torch.float64, device=self.device)
+        _lib.check(self.L.dfwfm_prune_threshold(arr, len(sources), float(target), ctypes.c_void_p(thr.data_ptr()),
+                                                ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(), self._stream()),
+                   "dfwfm_prune_threshold")
+        return thr
+
+    def apply(self, t, thr, sym_f=0):
+        _lib.check(self.L.dfwfm_prune_apply(ctypes.c_void_p(t.data_ptr()), t.numel(), int(sym_f),
+                                            ctypes.c_void_p(thr.data_ptr()), self._stream()), "dfwfm_prune_apply")
+        torch.autograd.graph.increment_version(t)
+
+
 def prune_step(model, adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb_corr):
-    """The reference's in-loop magnitude pruning (:647-673)."""
+    """The reference's in-loop magnitude pruning (:647-673) on the device: the second-order tables share
+    one threshold (:652-656), every `*linear*weight` gets its own (:661-664, including
+    fwfm_linear.weight), field_cov is masked by its symmetric part (:666-670)."""
+    dev = model._device()
+    if dev.type != "cuda":
+        raise _lib.DfwfmError("pruning runs on a HIP device (no CPU fallback)")
+    pr = getattr(model, "_pruner", None)
+    if pr is None or pr.device != dev:
+        pr = model._pruner = DevicePruner(dev)
     with torch.no_grad():
-        emb_threshold = None
+        named = list(model.named_parameters())
         if prune_fm != 0:
-            stacked = torch.cat([p.data for n, p in model.named_parameters() if "fm_2nd_embeddings" in n], 0)
-            emb_threshold = model.binary_search_threshold(stacked, adaptive_sparse * emb_r, stacked.numel())
-        for name, param in model.named_parameters():
-            if "fm_2nd_embeddings" in name and prune_fm != 0:
-                param.data[param.data.abs() < emb_threshold] = 0
+            embs = [p.data for n, p in named if "fm_2nd_embeddings" in n]
+            thr = pr.threshold([(e, 0) for e in embs], adaptive_sparse * emb_r)
+            for e in embs:
+                pr.apply(e, thr)
+        for name, param in named:
             if "linear" in name and "weight" in name and prune_deep != 0:
-                thr = model.binary_search_threshold(param.data, adaptive_sparse, param.numel())
-                param.data[param.data.abs() < thr] = 0
+                pr.apply(param.data, pr.threshold([(param.data, 0)], adaptive_sparse))
             if name == "field_cov.weight" and prune_r != 0:
-                symm = 0.5 * (param.data + param.data.t())
-                thr = model.binary_search_threshold(symm, adaptive_sparse * emb_corr, param.numel())
-                param.data[symm.abs() < thr] = 0
+                F_ = param.shape[0]
+                pr.apply(param.data, pr.threshold([(param.data, F_)], adaptive_sparse * emb_corr), F_)
 
 
 # --------------------------------------------------------------------------------------- fit
