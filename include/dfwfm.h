@@ -208,6 +208,15 @@ int dfwfm_prune_threshold(const dfwfm_prune_source* sources, int32_t n, double t
  * |(W[k][l] + W[l][k]) / 2| < threshold, computed from the unmodified matrix (:666-670). */
 int dfwfm_prune_apply(float* values, int64_t numel, int32_t sym_f, const double* thr_dev, void* stream);
 
+/* ---- evaluation metrics (reference eval_by_batch, model/DeepFMs.py:777-800) --------------------
+ * From logits z and labels y (device, n each): pred = sigmoid(z) in f32; writes 8 doubles to out_dev:
+ * {roc_auc_score(y, pred), auc(precision_recall_curve), log_loss, RCE, CTR, positives, n, distinct
+ * predictions}, the sklearn 1.7 definitions (ties grouped, [1-p, p] renormalised and clipped to the
+ * float64 eps).  AUC is NaN when only one class is present (sklearn raises). */
+int64_t dfwfm_metrics_workspace_bytes(int64_t n);
+int dfwfm_eval_metrics(const float* logits, const float* labels, int64_t n, double* out_dev, void* workspace,
+                       int64_t workspace_bytes, void* stream);
+
 /* Synchronises `stream`, returns the sticky error-flag word and clears it. */
 int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream);
 

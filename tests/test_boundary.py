@@ -27,8 +27,8 @@ def header_functions():
 def test_header_declares_expected_api():
     assert header_functions() == sorted([
         "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_bce_grad",
-        "dfwfm_diag_stamps", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy",
-        "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_prune_apply", "dfwfm_prune_threshold",
+        "dfwfm_diag_stamps", "dfwfm_eval_metrics", "dfwfm_forward", "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy",
+        "dfwfm_metrics_workspace_bytes", "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_prune_apply", "dfwfm_prune_threshold",
         "dfwfm_prune_workspace_bytes", "dfwfm_read_error_flag", "dfwfm_set_step_source", "dfwfm_train_forward"])
 
 
@@ -59,6 +59,8 @@ def test_abi_version_and_error_string(built):
     assert L.dfwfm_prune_apply(None, 4, 0, None, None) == -1
     assert L.dfwfm_prune_workspace_bytes(1000) >= 8000  # host-only query (hipcub sizing, no launch)
     assert ctypes.sizeof(built.dfwfm_prune_source) == 24
+    assert L.dfwfm_eval_metrics(None, None, 4, None, None, 0, None) == -1
+    assert L.dfwfm_metrics_workspace_bytes(1000) > 40 * 1000
 
 
 def test_struct_layouts_match_header(built):

@@ -155,3 +155,58 @@ def test_criteo_size_properties_large_batch(criteo, gpu):
     assert np.array_equal(d, a)
     sel = np.arange(0, 65536, 997)
     assert logit_close(a[sel], dfwfm_oracle.forward(cfg, params, xi[sel], xv[sel])) < 1e-5
+
+
+@pytest.mark.parametrize("n,levels,rate", [(1000, 0, 0.3), (50000, 64, 0.25), (123457, 0, 0.02), (4097, 3, 0.5)])
+def test_device_metrics_match_sklearn(gpu, n, levels, rate):
+    """DeviceMetrics == sklearn roc_auc_score / precision_recall_curve+auc / log_loss / RCE (the reference's
+    eval_by_batch metrics, :777-800), including heavily tied predictions."""
+    from sklearn.metrics import auc, log_loss, precision_recall_curve, roc_auc_score
+    from xsdeepfwfm_deprecated_amd.metrics import DeviceMetrics
+    rng = np.random.default_rng(n)
+    z = rng.normal(size=n).astype(np.float32) * 2
+    if levels:
+        z = np.round(z * levels / 4) / (levels / 4)  # many exact ties
+    y = (rng.random(n) < 1 / (1 + np.exp(-(z + rng.normal(size=n))))) * 1.0
+    y = np.where(rng.random(n) < rate, y, 0.0).astype(np.float32)
+    m = DeviceMetrics(gpu)(torch.from_numpy(z).to(gpu), torch.from_numpy(y).to(gpu))
+    # the device's f32 sigmoid may differ from torch-CPU's by an ulp per element, which can merge or split
+    # near-equal predictions: the AUCs agree to ~1e-7 here (exactly on separated logits, next test), the
+    # log-loss to ~1e-9 relative
+    pred = torch.sigmoid(torch.from_numpy(z)).numpy().astype("float64")
+    assert abs(m["auc"] - roc_auc_score(y, pred)) < 1e-6
+    prec, rec, _ = precision_recall_curve(y, pred)
+    assert abs(m["prauc"] - auc(rec, prec)) < 1e-6
+    ll = log_loss(y, pred)
+    assert abs(m["log_loss"] - ll) < 1e-7 * max(1.0, ll)
+    c = float(np.mean(y == 1))
+    rce = (1.0 - ll / log_loss(y, [c] * n)) * 100.0
+    assert abs(m["rce"] - rce) < 1e-5
+    assert m["n"] == n and m["positives"] == float((y == 1).sum())
+
+
+def test_eval_by_batch_matches_reference_auc(gpu):
+    """eval_by_batch (device logits + device metrics) reproduces the reference's AUC on tiny-criteo."""
+    cfg, params, xi, xv, y, l32, l64, auc_ref = load_golden("tiny_deepfwfm_lw")
+    m = make_model(cfg, params, gpu)
+    loss, auc_got, prauc, rce = m.eval_by_batch(xi, xv, y, len(y))
+    assert abs(auc_got - auc_ref) <= 1e-4
+    from sklearn.metrics import log_loss
+    assert abs(loss - log_loss(y, dfwfm_oracle.sigmoid(l64))) < 1e-4
+
+
+def test_device_metrics_exact_on_separated_logits(gpu):
+    """With logits far enough apart that every platform's f32 sigmoid orders them the same, and exact
+    repeats for ties, the device AUC / PR-AUC equal sklearn's to rounding."""
+    from sklearn.metrics import auc, precision_recall_curve, roc_auc_score
+    from xsdeepfwfm_deprecated_amd.metrics import DeviceMetrics
+    rng = np.random.default_rng(3)
+    levels = np.linspace(-4, 4, 401).astype(np.float32)
+    z = levels[rng.integers(0, len(levels), size=20000)]
+    y = (rng.random(20000) < 1 / (1 + np.exp(-z))).astype(np.float32)
+    m = DeviceMetrics(gpu)(torch.from_numpy(z).to(gpu), torch.from_numpy(y).to(gpu))
+    pred = torch.sigmoid(torch.from_numpy(z)).numpy().astype("float64")
+    assert m["distinct_predictions"] == len(np.unique(pred))
+    assert abs(m["auc"] - roc_auc_score(y, pred)) < 1e-12
+    prec, rec, _ = precision_recall_curve(y, pred)
+    assert abs(m["prauc"] - auc(rec, prec)) < 1e-12

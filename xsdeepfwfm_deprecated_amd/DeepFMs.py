@@ -341,23 +341,33 @@ class DeepFMs(nn.Module):
         return torch.cat(out) if out else torch.empty(0, device=self._device())
 
     def eval_by_batch(self, Xi, Xv, y, x_size):
-        """Reference model/DeepFMs.py:750-784: loss, AUC, PR-AUC, RCE at batch 8192."""
+        """Reference model/DeepFMs.py:750-784: loss, AUC, PR-AUC, RCE over batches of 8192.  The logits
+        stay on the device and the metrics are computed there (metrics.DeviceMetrics, sklearn
+        definitions); the loss is the reference's per-batch BCE mean weighted by the batch length."""
         self.eval()
-        Xi = np.asarray(Xi)
-        Xv = np.asarray(Xv)
-        y = np.asarray(y)
+        dev = self._device()
+        ncat = self.field_size - self.num
+        Xi_d = torch.as_tensor(np.asarray(Xi)[:x_size]).reshape(x_size, ncat).to(dev, dtype=torch.int64)
+        Xv_d = torch.as_tensor(np.asarray(Xv)[:x_size], dtype=torch.float32).to(dev)
+        y_d = torch.as_tensor(np.asarray(y)[:x_size], dtype=torch.float32).to(dev)
         bs = 8192
-        total_loss = 0.0
-        y_pred = []
+        logits = torch.empty(x_size, dtype=torch.float32, device=dev)
+        total_loss = torch.zeros((), dtype=torch.float64, device=dev)
         with torch.no_grad():
             for off in range(0, x_size, bs):
                 end = min(x_size, off + bs)
-                logits = self(torch.as_tensor(Xi[off:end]), torch.as_tensor(Xv[off:end], dtype=torch.float32))
-                yb = torch.as_tensor(y[off:end], dtype=torch.float32, device=logits.device)
-                total_loss += F.binary_cross_entropy_with_logits(logits, yb).item() * (end - off)
-                y_pred.extend(torch.sigmoid(logits).cpu().numpy().astype("float64"))
-        total_metric = self.eval_metric(y, y_pred)
-        return total_loss / x_size, total_metric, self.compute_prauc(y_pred, y), self.compute_rce(y_pred, y)
+                out = self(Xi_d[off:end], Xv_d[off:end])
+                logits[off:end] = out
+                total_loss += F.binary_cross_entropy_with_logits(out, y_d[off:end]).double() * (end - off)
+        if self.eval_metric is not metrics.roc_auc_score:  # a user metric gets host arrays, as before
+            y_pred = torch.sigmoid(logits).cpu().numpy().astype("float64")
+            return (total_loss.item() / x_size, self.eval_metric(np.asarray(y)[:x_size], y_pred),
+                    self.compute_prauc(y_pred, np.asarray(y)[:x_size]), self.compute_rce(y_pred, np.asarray(y)[:x_size]))
+        dm = getattr(self, "_dev_metrics", None)
+        if dm is None or dm.device != dev:
+            dm = self._dev_metrics = metrics.DeviceMetrics(dev)
+        m = dm(logits, y_d)
+        return total_loss.item() / x_size, m["auc"], m["prauc"], m["rce"]
 
     def compute_prauc(self, pred, gt):
         return metrics.prauc(gt, pred)

@@ -21,7 +21,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
-SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_capi.hip"]
+SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_capi.hip"]
 HEADERS = ["dfwfm_internal.h", "dfwfm_device.h", os.path.join("..", "..", "include", "dfwfm.h")]
 ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
 
@@ -96,6 +96,8 @@ SIGNATURES = {
     "dfwfm_prune_threshold": (ctypes.c_int, [ctypes.POINTER(dfwfm_prune_source), ctypes.c_int32, ctypes.c_double,
                                              _P, _P, ctypes.c_int64, _P]),
     "dfwfm_prune_apply": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int32, _P, _P]),
+    "dfwfm_metrics_workspace_bytes": (ctypes.c_int64, [ctypes.c_int64]),
+    "dfwfm_eval_metrics": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, _P, ctypes.c_int64, _P]),
     "dfwfm_read_error_flag": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
     "dfwfm_last_error": (ctypes.c_char_p, []),
     "dfwfm_diag_stamps": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64, _P]),

@@ -826,6 +826,22 @@ int dfwfm_prune_apply(float* values, int64_t numel, int32_t sym_f, const double*
   return e == hipSuccess ? DFWFM_OK : hip_fail(e, "prune apply");
 }
 
+int64_t dfwfm_metrics_workspace_bytes(int64_t n) {
+  if (n <= 0 || n > 0x7fffffff) return 0;
+  return (int64_t)metrics_workspace_bytes(n);
+}
+
+int dfwfm_eval_metrics(const float* z, const float* y, int64_t n, double* out, void* ws, int64_t ws_bytes,
+                       void* stream) {
+  if (!z || !y || !out || !ws) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (n <= 0 || n > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "n = %lld outside [1, 2^31)", (long long)n);
+  if (ws_bytes < (int64_t)metrics_workspace_bytes(n))
+    return fail(DFWFM_ERR_INVALID_ARG, "workspace of %lld bytes < %lld", (long long)ws_bytes,
+                (long long)metrics_workspace_bytes(n));
+  hipError_t e = launch_metrics(z, y, n, out, ws, (size_t)ws_bytes, (hipStream_t)stream);
+  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "eval metrics");
+}
+
 int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream) {
   if (!m || !host || n < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
   if (!m->d_stamps) return fail(DFWFM_ERR_STATE, "no stamps recorded (set DFWFM_DIAG_STAMPS=1)");

@@ -269,6 +269,10 @@ hipError_t launch_prune_threshold(const PruneList& L, double target, double* d_t
                                   hipStream_t s);
 hipError_t launch_prune_apply(float* p, int64_t numel, int sym_f, const double* d_thr, hipStream_t s);
 
+size_t metrics_workspace_bytes(int64_t n);
+hipError_t launch_metrics(const float* z, const float* y, int64_t n, double* out, void* ws, size_t ws_bytes,
+                          hipStream_t s);
+
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
