@@ -1,5 +1,7 @@
 """GPU: one HIP training step (fused forward in train mode -> HIP backward -> HIP Adam), through the C ABI,
 against the reference's one-step goldens and the training oracle (with the kernels' dropout masks)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -278,3 +280,23 @@ def test_device_threshold_equals_reference_value(gpu):
     W = torch.randn(39, 39, generator=g) * 0.2
     ref = binary_search_threshold(0.5 * (W + W.t()), 0.7, W.numel())
     assert pr.threshold([(W.to(gpu), 39)], 0.7).item() == ref
+
+
+def test_main_all_tiny_criteo_end_to_end(gpu, tmp_path):
+    """main_all.py (the reference entry point) on the tiny-criteo fixture rows: native ingest, fit with the
+    fused HIP step (one epoch), save, reload, print_size_of_model, run_benchmark (device metrics)."""
+    import shutil
+    import subprocess
+    import sys
+    from conftest import GOLDEN, REPO
+    data = tmp_path / "data"
+    data.mkdir()
+    src = os.path.join(GOLDEN, "ingest", "tiny_train_head.csv")
+    shutil.copy(src, data / "tiny_train_input.csv")
+    shutil.copy(src, data / "tiny_test_input.csv")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "main_all.py"), "-dataset", "tiny-criteo", "-n_epochs",
+                        "1", "-batch_size", "256", "-data_root", str(tmp_path)], cwd=str(tmp_path),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "Training [1] loss" in r.stdout and "Acc:" in r.stdout and "Avg forward pass time" in r.stdout
+    assert any(f.startswith("DeepFwFM_l2_") for f in os.listdir(tmp_path / "saved_models"))

@@ -24,6 +24,9 @@ LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
 SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_capi.hip"]
 HEADERS = ["dfwfm_internal.h", "dfwfm_device.h", os.path.join("..", "..", "include", "dfwfm.h")]
 ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
+INGEST_PATH = os.path.join(PKG_DIR, "libdfwfm_ingest.so")
+INGEST_SOURCES = ["dfwfm_ingest.cpp"]
+INGEST_HEADERS = [os.path.join("..", "..", "include", "dfwfm_ingest.h")]
 
 DFWFM_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported", -3: "HIP error", -4: "bad state"}
@@ -116,9 +119,33 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def _stale_ingest() -> bool:
+    if not os.path.exists(INGEST_PATH):
+        return True
+    t = os.path.getmtime(INGEST_PATH)
+    deps = [os.path.join(CSRC, s) for s in INGEST_SOURCES + INGEST_HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_ingest(force: bool = False, verbose: bool = False) -> str:
+    """Compile the host-only ingest library (g++, no GPU code)."""
+    if not force and not _stale_ingest():
+        return INGEST_PATH
+    cxx = os.environ.get("CXX", "g++")
+    tmp = INGEST_PATH + ".tmp"
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", tmp] + \
+        [os.path.join(CSRC, s) for s in INGEST_SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, INGEST_PATH)
+    return INGEST_PATH
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile libdfwfm.so for gfx950 in-tree (hipcc cross-compiles without a GPU): one object per
-    translation unit, compiled in parallel, then linked."""
+    translation unit, compiled in parallel, then linked; and the host-only ingest library."""
+    build_ingest(force, verbose)
     if not force and not _stale():
         return LIB_PATH
     from concurrent.futures import ThreadPoolExecutor
@@ -140,6 +167,36 @@ def build(force: bool = False, verbose: bool = False) -> str:
         os.remove(o)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
+
+
+_ingest = None
+INGEST_SIGNATURES = {
+    "dfwfm_csv_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p),
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),
+    "dfwfm_csv_parse": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int32]),
+    "dfwfm_csv_close": (None, [ctypes.c_void_p]),
+    "dfwfm_feature_map_counts": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
+    "dfwfm_ingest_last_error": (ctypes.c_char_p, []),
+}
+
+
+def ingest_lib():
+    """The host ingest library (include/dfwfm_ingest.h); raises DfwfmError if it is missing."""
+    global _ingest
+    if _ingest is not None:
+        return _ingest
+    with _lock:
+        if _ingest is None:
+            if not os.path.exists(INGEST_PATH):
+                raise DfwfmError(f"{INGEST_PATH} is missing: run xsdeepfwfm_deprecated_amd.build()")
+            L = ctypes.CDLL(INGEST_PATH)
+            for name, (res, args) in INGEST_SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _ingest = L
+    return _ingest
 
 
 def lib():
