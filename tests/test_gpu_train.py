@@ -300,3 +300,57 @@ def test_main_all_tiny_criteo_end_to_end(gpu, tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "Training [1] loss" in r.stdout and "Acc:" in r.stdout and "Avg forward pass time" in r.stdout
     assert any(f.startswith("DeepFwFM_l2_") for f in os.listdir(tmp_path / "saved_models"))
+
+
+def _dp_fit_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = _fit_small(batch_size=256)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _fit_small(batch_size):
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = [1] * 13 + [50, 300, 7, 1000, 20, 5, 64, 9, 100, 3, 11, 17, 250, 4, 6, 30, 8, 2, 40, 12, 90, 5, 15,
+                        300, 7, 60]
+    xi, xv = synth.synth_inputs(sizes, 13, 4096, seed=5)
+    logit = ((xi[:, 0] % 7) - 3) * 0.6 + (xv[:, 0] > 30) * 1.0 - 0.5
+    y = (np.random.default_rng(1).random(4096) < 1 / (1 + np.exp(-logit))).astype(np.float32)
+    m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1, n_epochs=2,
+                batch_size=batch_size, learning_rate=1e-2, weight_decay=3e-7, h_depth=2, deep_nodes=64,
+                is_deep_dropout=False, random_seed=3).to("cuda:0")
+    tr, _ = m.fit(xi.reshape(-1, 26, 1), xv, y, [], [], [])
+    torch.cuda.synchronize()
+    return tr, {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+
+
+def test_data_parallel_fit_two_ranks(gpu):
+    """config 5 semantics on one GPU: two gloo ranks (both on cuda:0) run fit with batch 256 each; every
+    rank ends with bit-identical weights, and training matches one process on the global batch of 512
+    (same init and shuffles; float summation order differs)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_fit_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (tr0, w0), (tr1, w1) = res[0], res[1]
+    assert all(np.array_equal(w0[k], w1[k]) for k in w0)  # replicas stay identical
+    tr_single, w_single = _fit_small(batch_size=512)
+    assert abs(tr0[-1] - tr_single[-1]) < 5e-3, (tr0, tr_single)
+    num = sum(float(np.abs(w0[k] - w_single[k]).sum()) for k in w0)
+    den = sum(float(np.abs(w_single[k]).sum()) for k in w0)
+    assert num / den < 1e-2, num / den
