@@ -9,7 +9,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-graph > gpurun_out/pmc_${TAG}_$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-graph --streams 1 > gpurun_out/pmc_${TAG}_$i.log 2>&1
   rc=$?
   echo "pass $i [$grp] rc=$rc"
   if [ $rc -ge 124 ]; then exit $rc; fi

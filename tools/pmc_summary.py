@@ -23,7 +23,7 @@ for path in glob.glob(os.path.join(root, f"pmc_{tag}_*", "run_counter_collection
         vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
         durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 med = {k: st.median(v) for k, v in vals.items()}
-out = {"kernel": "dfwfm::fwd_kernel<10,7,1>", "counters_median_per_dispatch": med,
+out = {"kernel": "dfwfm::fwd_kernel<10,6,1,false>", "counters_median_per_dispatch": med,
        "profiled_duration_us_median": st.median(durs) / 1e3 if durs else None}
 if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
     out["hbm_bytes_per_launch"] = int(2 * med["FETCH_SIZE"] * 1024 + med["WRITE_SIZE"] * 1024)
