@@ -93,27 +93,28 @@ def forward_graph(cfg, params, Xi, Xv, masks=None, drop_p=0.0):
 
 # ---- training step (reference model/DeepFMs.py:553-637) -------------------------------------------
 def _mix32(x):
+    """murmur3's 32-bit finaliser (csrc/dfwfm_device.h mix32)."""
     x = x.astype(np.uint32)
     x ^= x >> np.uint32(16)
-    x = (x * np.uint32(0x7FEB352D)).astype(np.uint32)
-    x ^= x >> np.uint32(15)
-    x = (x * np.uint32(0x846CA68B)).astype(np.uint32)
+    x = (x * np.uint32(0x85EBCA6B)).astype(np.uint32)
+    x ^= x >> np.uint32(13)
+    x = (x * np.uint32(0xC2B2AE35)).astype(np.uint32)
     x ^= x >> np.uint32(16)
     return x
 
 
 def dropout_masks(seed, p, B, widths, row0=0):
     """The HIP kernels' counter-hash dropout keep masks (csrc/dfwfm_device.h dropout_keep), restated:
-    keep (layer, row, col) iff (hash >> 8) / 2^24 >= p.  widths[h] = columns of layer h's output."""
+    keep (layer, row, col) iff (mix32(seed ^ row*K1 ^ col*K2 ^ layer*K3) >> 8) / 2^24 >= p.
+    widths[h] = columns of layer h's output."""
     out = []
     with np.errstate(over="ignore"):
         rows = (np.arange(B, dtype=np.int64) + row0).astype(np.uint32)[:, None]
         for layer, w in enumerate(widths):
             cols = np.arange(w, dtype=np.uint32)[None, :]
-            hc = _mix32(cols + np.uint32(0x632BE5AB))
-            hr = _mix32(rows ^ hc)
-            hl = _mix32((np.uint32(layer) * np.uint32(0x9E3779B9)).astype(np.uint32) ^ hr)
-            h = _mix32(np.uint32(seed) ^ hl)
+            key = (np.uint32(seed) ^ (rows * np.uint32(0x9E3779B9)) ^ (cols * np.uint32(0x7FEB352D))
+                   ^ np.uint32((layer * 0x846CA68B) & 0xFFFFFFFF)).astype(np.uint32)
+            h = _mix32(key)
             u = (h >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
             out.append(torch.from_numpy(u >= np.float32(p)))
     return out

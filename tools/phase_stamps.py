@@ -19,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--fwlw", action="store_true")
+ap.add_argument("--train", action="store_true", help="stamp the training-mode forward (activations saved)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 sizes = synth.CRITEO_FEATURE_SIZES
@@ -26,13 +27,20 @@ m = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, u
             use_fwlw=a.fwlw, numerical=13, use_cuda=True)
 shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
 m.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_state(shapes, 39, 10, 400, True, True).items()})
-m = m.to(dev).eval()
+m = m.to(dev).train() if a.train else m.to(dev).eval()
 m.strict_index_check = False
 xi, xv = synth.synth_inputs(sizes, 13, a.batch, seed=5)
 xi, xv = torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)
-with torch.no_grad():
+if a.train:
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    y = torch.zeros(a.batch, device=dev)
+    t = FusedTrainStep(m, a.batch, use_graph=False)
     for _ in range(a.iters):
-        m(xi, xv)
+        t.step(xi, xv, y)
+else:
+    with torch.no_grad():
+        for _ in range(a.iters):
+            m(xi, xv)
 torch.cuda.synchronize()
 grid = (a.batch + 15) // 16
 buf = (ctypes.c_uint64 * (grid * 16))()

@@ -47,6 +47,7 @@ struct dfwfm_model {
   float* sv_x[kMaxH + 1];
   float* sv_g[kMaxH + 1];
   float* sv_de;
+  float* sv_x0;           // X_0 after deep-tower dropout (without dropout X_0 is sv_e)
   float* red_part;        // per-16-row-tile partial sums of the shallow reductions
   FieldDev h_fields[64];  // host copy of the field descriptors (scatter task planning)
   // the last dfwfm_train_forward, replayed by dfwfm_backward
@@ -380,7 +381,8 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
 int ensure_workspace(dfwfm_model* m, int64_t batch) {
   if (batch <= m->ws_batch) return DFWFM_OK;
   const int64_t FD = (int64_t)m->F * m->D;
-  const int64_t per_row = 2 * FD + m->F + (m->H > 0 ? r4((int)FD) + 2 * (int64_t)m->H * m->N : 0);
+  const int64_t SE = r4((int)FD);
+  const int64_t per_row = SE + FD + m->F + (m->H > 0 ? SE + 2 * (int64_t)m->H * m->N : 0);
   const int64_t red_blocks = (batch + kBM - 1) / kBM;
   const int64_t red_floats = red_blocks * red_outputs(m->F, m->D, m->N, m->num);
   if (m->d_ws) (void)hipFree(m->d_ws);
@@ -390,19 +392,36 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   // every array starts 16-byte aligned: the row counts are multiples of 4 or the offsets are padded
   auto al = [](int64_t x) { return (x + 3) & ~(int64_t)3; };
   float* p = m->d_ws;
-  m->sv_e = p;   p += al(FD * batch);
+  m->sv_e = p;   p += al(SE * batch);
   m->sv_de = p;  p += al(FD * batch);
   m->red_part = p;  p += al(red_floats);
   m->sv_fo = p;  p += al((int64_t)m->F * batch);
   for (int h = 0; h <= kMaxH; ++h) m->sv_x[h] = m->sv_g[h] = nullptr;
   if (m->H > 0) {
-    m->sv_x[0] = p;  p += r4((int)FD) * batch;
+    m->sv_x0 = p;  p += SE * batch;
     for (int h = 1; h <= m->H; ++h) {
       m->sv_x[h] = p;  p += (int64_t)m->N * batch;
       m->sv_g[h] = p;  p += (int64_t)m->N * batch;
     }
   }
   m->ws_batch = batch;
+  return DFWFM_OK;
+}
+
+// diagnostics only: with DFWFM_DIAG_STAMPS=<which> the launch records per-workgroup phase clocks
+int diag_stamps_buffer(dfwfm_model* m, int64_t batch, int which, uint64_t** out) {
+  *out = nullptr;
+  const char* stv = getenv("DFWFM_DIAG_STAMPS");
+  if (!stv || atoi(stv) != which) return DFWFM_OK;
+  const size_t grid = (size_t)((batch + kBM - 1) / kBM);
+  if (grid > m->stamps_cap) {
+    if (m->d_stamps) (void)hipFree(m->d_stamps);
+    m->d_stamps = nullptr;
+    m->stamps_cap = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_stamps), grid * kStampSlots * sizeof(uint64_t)));
+    m->stamps_cap = grid;
+  }
+  *out = m->d_stamps;
   return DFWFM_OK;
 }
 
@@ -420,19 +439,7 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   // diagnostics only (phase timing): DFWFM_DIAG_DROP_FLAGS clears flag bits, results become invalid
   if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
-  a.stamps = nullptr;
-  const char* stv = getenv("DFWFM_DIAG_STAMPS");
-  if (stv && atoi(stv) == 1) {
-    const size_t grid = (size_t)((batch + kBM - 1) / kBM);
-    if (grid > m->stamps_cap) {
-      if (m->d_stamps) (void)hipFree(m->d_stamps);
-      m->d_stamps = nullptr;
-      m->stamps_cap = 0;
-      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_stamps), grid * kStampSlots * sizeof(uint64_t)));
-      m->stamps_cap = grid;
-    }
-    a.stamps = m->d_stamps;
-  }
+  if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, m->KS, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
@@ -467,11 +474,14 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   a.flags |= kTrain | ((m->H > 0 && dropout_p > 0.f) ? kDrop : 0);
   a.sv_e = m->sv_e;
   a.sv_fo = m->sv_fo;
+  // without deep-tower dropout X_0 == E: one saved copy
+  m->sv_x[0] = m->H > 0 ? ((dropout_p > 0.f) ? m->sv_x0 : m->sv_e) : nullptr;
   for (int h = 0; h <= m->H; ++h) a.sv_x[h] = m->sv_x[h];
   a.drop_p = dropout_p;
   a.drop_scale = 1.f / (1.f - dropout_p);
   a.seed = seed;
   a.seed_src = m->step_src;
+  if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, 1, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
   m->trained = true;
@@ -524,18 +534,8 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
     a.seed = m->t_seed;
     a.seed_src = m->step_src;
     // diagnostics only: DFWFM_DIAG_STAMPS=2 records the backward's phase clocks instead of the forward's
-    const char* stv = getenv("DFWFM_DIAG_STAMPS");
-    if (stv && atoi(stv) == 2) {
-      const size_t grid = (size_t)((batch + kBM - 1) / kBM);
-      if (grid > m->stamps_cap) {
-        if (m->d_stamps) (void)hipFree(m->d_stamps);
-        m->d_stamps = nullptr;
-        m->stamps_cap = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_stamps), grid * kStampSlots * sizeof(uint64_t)));
-        m->stamps_cap = grid;
-      }
-      a.stamps = m->d_stamps;
-    }
+    int src = diag_stamps_buffer(m, batch, 2, &a.stamps);
+    if (src != DFWFM_OK) return src;
     const size_t lds = backward_lds_bytes(F, D, m->MT, m->S, m->SX, m->SY);
     e = launch_backward(a, D, m->TPW > 0 ? m->TPW : 1, lds, s);
     if (e != hipSuccess) return hip_fail(e, "backward launch");

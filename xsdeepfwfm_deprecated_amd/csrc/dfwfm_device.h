@@ -210,19 +210,33 @@ struct TailStream {
 };
 
 // Counter-based dropout mask (deep tower; reference nn.Dropout(0.5), model/DeepFMs.py:260-282):
-// keep element (layer, row, col) of a step iff a 24-bit hash of (seed, layer, row, col) >= p.
-// The same function regenerates the mask in the backward.
+// keep element (layer, row, col) of a step iff the top 24 bits of a murmur3-finalised key
+// (seed ^ row*K1 ^ col*K2 ^ layer*K3) / 2^24 >= p.  The same function regenerates the mask in the
+// backward; oracle/torch_port.dropout_masks restates it.
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
-  x *= 0x7feb352dU;
-  x ^= x >> 15;
-  x *= 0x846ca68bU;
+  x *= 0x85EBCA6BU;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35U;
   x ^= x >> 16;
   return x;
 }
 __device__ __forceinline__ bool dropout_keep(uint32_t seed, int layer, int64_t row, int col, float p) {
-  const uint32_t h = mix32(seed ^ mix32((uint32_t)layer * 0x9E3779B9U ^ mix32((uint32_t)row ^ mix32((uint32_t)col + 0x632BE5ABU))));
+  const uint32_t h =
+      mix32(seed ^ ((uint32_t)row * 0x9E3779B9U) ^ ((uint32_t)col * 0x7FEB352DU) ^ ((uint32_t)layer * 0x846CA68BU));
   return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
+// Copy rows [0, nrows) x 4*cols4 floats of an LDS tile (row stride lds_stride) to global rows of stride
+// gstride (both multiples of 4 floats, 16-byte aligned bases): one float4 per lane per step.
+__device__ __forceinline__ void store_tile(float* __restrict__ g, int64_t gstride, const float* __restrict__ lds,
+                                           int lds_stride, int nrows, int cols4, int tid, int nth) {
+  const int n = nrows * cols4;
+  for (int i = tid; i < n; i += nth) {
+    const int b = i / cols4;
+    const int c = (i - b * cols4) * 4;
+    *reinterpret_cast<float4*>(g + b * gstride + c) = *reinterpret_cast<const float4*>(lds + b * lds_stride + c);
+  }
 }
 
 // Dropout seed of a step: the host's seed, or -- for graph-replayed steps -- that seed mixed with a

@@ -255,12 +255,13 @@ fwd_kernel(FwdArgs p) {
   stamp(p.stamps, 2, tid);
   constexpr bool train = TRAIN;
   const int FD = F * D;
-  if constexpr (train) {  // E, before dropout, for the shallow backward
-    for (int i = tid; i < kBM * FD; i += NTH) {
-      const int b = i / FD;
-      const int c = i - b * FD;
-      if (b0 + b < p.batch) p.sv_e[(b0 + b) * FD + c] = bufX[b * SX + c];
-    }
+  const int SE = r4(FD);  // row stride of the saved E / X_0 tiles
+  const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
+  const bool drop0 = train && deep && (flags & kDrop) != 0;
+  if constexpr (train) {
+    // E for the shallow backward.  Without deep-tower dropout E is also X_0 and is saved after
+    // layer 1's K loop from the same LDS tile (stores issued behind that layer's weight stream)
+    if (drop0 || !deep) store_tile(p.sv_e + b0 * SE, SE, bufX, SX, nrows, SE / 4, tid, NTH);
   }
 
   // ---- phase S: shallow part ----------------------------------------------
@@ -347,17 +348,13 @@ fwd_kernel(FwdArgs p) {
       const int b = i / F;
       if (b0 + b < p.batch) p.sv_fo[(b0 + b) * F + (i - b * F)] = fo[b * Fp + (i - b * F)];
     }
-    if (deep) {  // deep_emb dropout (net_1_linear_0_dropout, model/DeepFMs.py:411) and X_0
-      const bool drop = (flags & kDrop) != 0;
-      const uint32_t dseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
+    if (drop0) {  // deep_emb dropout (net_1_linear_0_dropout, model/DeepFMs.py:411), in place
+      const uint32_t dseed = step_seed(p.seed, p.seed_src);
       for (int i = tid; i < kBM * FD; i += NTH) {
         const int b = i / FD;
         const int c = i - b * FD;
-        const int64_t row = b0 + b;
-        float v = bufX[b * SX + c];
-        if (drop) v = dropout_keep(dseed, 0, row, c, p.drop_p) ? v * p.drop_scale : 0.f;
-        bufX[b * SX + c] = v;
-        if (row < p.batch) p.sv_x[0][row * r4(FD) + c] = v;  // rows 16-byte aligned for dw_kernel
+        const float v = bufX[b * SX + c];
+        bufX[b * SX + c] = dropout_keep(dseed, 0, b0 + b, c, p.drop_p) ? v * p.drop_scale : 0.f;
       }
     }
   }
@@ -437,6 +434,14 @@ fwd_kernel(FwdArgs p) {
         ts.load(wrsrc, tw, lane * 16);
       }
     }
+    if constexpr (train) {
+      // this layer's input X_h for the backward, from LDS (intact until the next layer's epilogue):
+      // behind the next layer's preload, so those loads do not wait for the stores (vmcnt is in order)
+      if (h == 0)
+        store_tile(p.sv_x[0] + b0 * SE, SE, in, SA, nrows, SE / 4, tid, NTH);
+      else
+        store_tile(p.sv_x[h] + b0 * p.N, p.N, in, SA, nrows, p.N / 4, tid, NTH);
+    }
     if constexpr (KS == 2) {
       if (kh == 1) {
 #pragma unroll
@@ -459,15 +464,12 @@ fwd_kernel(FwdArgs p) {
           if constexpr (train) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              // dropout after the ReLU (net_1_linear_{h}_dropout, :416-426), X_h kept for the backward
+              // dropout after the ReLU (net_1_linear_{h}_dropout, :416-426); the tile goes to LDS also
+              // in the last layer, from where X_H is saved for the backward
               float v = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
-              const int64_t row = b0 + row0 + r;
-              if (drop) v = dropout_keep(hseed, h + 1, row, n, p.drop_p) ? v * p.drop_scale : 0.f;
-              if (valid && row < p.batch) p.sv_x[h + 1][row * p.N + n] = v;
-              if (!last)
-                outa[(row0 + r) * SO + n] = v;
-              else
-                dpart[r] = fmaf(v, wf[j], dpart[r]);
+              if (drop) v = dropout_keep(hseed, h + 1, b0 + row0 + r, n, p.drop_p) ? v * p.drop_scale : 0.f;
+              outa[(row0 + r) * SO + n] = v;
+              if (last) dpart[r] = fmaf(v, wf[j], dpart[r]);
             }
           } else if (!last) {
 #pragma unroll
@@ -493,9 +495,8 @@ fwd_kernel(FwdArgs p) {
       const float sum = ((tp[0] + tp[256]) + tp[512]) + tp[768];
       float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
       if constexpr (train) {
-        const int64_t row = b0 + rr;
-        if (drop) v = dropout_keep(hseed, h + 1, row, n, p.drop_p) ? v * p.drop_scale : 0.f;
-        if (valid && row < p.batch) p.sv_x[h + 1][row * p.N + n] = v;
+        if (drop) v = dropout_keep(hseed, h + 1, b0 + rr, n, p.drop_p) ? v * p.drop_scale : 0.f;
+        if (last) outa[rr * SO + n] = v;  // X_H is saved from LDS
       }
       if (!last) {
         outa[rr * SO + n] = v;
@@ -508,6 +509,14 @@ fwd_kernel(FwdArgs p) {
       }
     }
     stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
+  }
+
+  if constexpr (train) {
+    // X_H (the last layer's output after ReLU / dropout) from LDS: the buffer the last layer wrote
+    if (tail) __syncthreads();  // the tail tile's rows were written after the layer's barrier
+    float* last_out = ((p.H - 1) & 1) == 0 ? bufY : bufX;
+    const int SL = ((p.H - 1) & 1) == 0 ? SY : SX;
+    store_tile(p.sv_x[p.H] + b0 * p.N, p.N, last_out, SL, nrows, p.N / 4, tid, NTH);
   }
 
   // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the 16 lanes sharing (lane>>4), then the 4 groups

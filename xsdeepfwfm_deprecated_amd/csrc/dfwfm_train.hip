@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
     const int b = i / p.W0;
     const int c = i - b * p.W0;
     const int64_t row = b0 + b;
-    bufE[b * SX + c] = (second && c < FD && row < p.batch) ? p.sv_e[row * FD + c] : 0.f;
+    bufE[b * SX + c] = (second && c < FD && row < p.batch) ? p.sv_e[row * r4(FD) + c] : 0.f;
     bufD[b * SX + c] = 0.f;
   }
   __syncthreads();
@@ -226,7 +226,7 @@ struct RedLds {
 __host__ __device__ inline RedLds red_layout(int F, int D, int N, int num) {
   RedLds L;
   int o = 0;
-  L.e = o;   o += r4(kBM * F * D);  // rows packed (stride F*D), as in the workspace
+  L.e = o;   o += kBM * r4(F * D);  // rows of stride r4(F*D), as in the workspace
   L.fo = o;  o += r4(kBM * F);
   L.xh = o;  o += r4(kBM * N);
   L.xv = o;  o += r4(kBM * (num > 0 ? num : 1));
@@ -274,6 +274,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int F = a.F, D = a.D, FD = F * D, num = a.num, N = a.N, numD = num * D;
+  const int SE = r4(FD);  // row stride of the saved E
   const RedLds L = red_layout(F, D, N, num);
   float* es = sm + L.e;
   float* fos = sm + L.fo;
@@ -286,7 +287,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
   const bool need_e = a.g_fwlw || a.g_R;
   const bool need_num2 = numD > 0 && a.sv_de != nullptr;
   if (tid < kBM) dl[tid] = tid < nt ? a.dlogit[rb + tid] : 0.f;
-  if (need_e) stage_linear<8>(es, a.sv_e + rb * FD, nt * FD, r4(kBM * FD), tid);
+  if (need_e) stage_linear<8>(es, a.sv_e + rb * SE, nt * SE, kBM * SE, tid);
   if (a.g_lw) stage_linear<2>(fos, a.sv_fo + rb * F, nt * F, r4(kBM * F), tid);
   if (a.g_fc) stage_linear<8>(xhs, a.x_h + rb * N, nt * N, r4(kBM * N), tid);
   if (num > 0)
@@ -330,7 +331,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
       float s = 0.f;
       if (a.g_fwlw)
 #pragma unroll
-        for (int b = 0; b < kBM; ++b) s = fmaf(dl[b], es[b * FD + i], s);
+        for (int b = 0; b < kBM; ++b) s = fmaf(dl[b], es[b * SE + i], s);
       o_fw[i] = s;
     }
   }
@@ -375,8 +376,8 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
         const int n = 4 * s + (lane >> 4);
         const int b = n / D;
         const int d = n - b * D;
-        const float av = kA < F ? dl[b] * es[b * FD + kA * D + d] : 0.f;
-        const float bv = lB < F ? es[b * FD + lB * D + d] : 0.f;
+        const float av = kA < F ? dl[b] * es[b * SE + kA * D + d] : 0.f;
+        const float bv = lB < F ? es[b * SE + lB * D + d] : 0.f;
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
       }
 #pragma unroll
