@@ -50,7 +50,19 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
                          "batch's workgroup shares each CU, hiding the gather / FwFM phases)")
+    ap.add_argument("--stagger-cycles", type=int, default=0,
+                    help="start stream k after a k x this many cycle spin (offsets the streams' phases)")
     return ap.parse_args()
+
+
+def kernel_name():
+    """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
+    train, part, tile groups); DFWFM_NG / DFWFM_SPLIT select the A/B variants."""
+    ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
+    tpw = 6 if ng == 4 else 3
+    if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):
+        return f"dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::fwd_kernel<10,{tpw},1,false,2,{ng}>"
+    return f"dfwfm::fwd_kernel<10,{tpw},1,false,0,{ng}>"
 
 
 def algorithmic_counts(cfg):
@@ -167,6 +179,9 @@ def main():
             if k:
                 st.wait_stream(streams[0])
             s0[k].record(st)
+            if k and a.stagger_cycles:
+                with torch.cuda.stream(st):
+                    torch.cuda._sleep(k * a.stagger_cycles)
         run_n(a.steps)
         for k, st in enumerate(streams):
             s1[k].record(st)
@@ -214,7 +229,7 @@ def main():
                              + (f", {S} streams (batches in flight)" if S > 1 else "")},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "traffic": traffic,
-                     "kernel": "dfwfm::fwd_kernel<10,6,1,false>", "flops_per_sample": flops,
+                     "kernel": kernel_name(), "flops_per_sample": flops,
                      "units_per_launch": BATCH, "launch_us": round(launch_ms * 1e3, 3), "launches_in_flight": S},
         "roofline_hbm": {"achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "bytes_per_sample": bytes_},

@@ -112,6 +112,19 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
 int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv,
                   int64_t xv_stride, int64_t batch, float* out, void* stream);
 
+/* The forward as two launches on `stream` -- the gather / shallow part (E tile and first + second
+ * order to `workspace`), then the MLP and the combine -- so that two batches in flight on two
+ * streams overlap their MLPs on every CU.  Same logits as dfwfm_forward, bit for bit.
+ * dfwfm_forward_workspace_bytes reports the workspace a batch needs (0: this model runs the single
+ * fused launch, e.g. no deep part, and dfwfm_forward_ws == dfwfm_forward).  The workspace is
+ * caller-owned device memory, 16-byte aligned, in use until the launches complete on `stream`;
+ * NULL also selects the fused launch.  Replaces the same reference call as dfwfm_forward
+ * (model/DeepFMs.py:285-469). */
+int dfwfm_forward_workspace_bytes(dfwfm_model* m, int64_t batch, size_t* bytes);
+int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv,
+                     int64_t xv_stride, int64_t batch, float* out, void* workspace, size_t ws_bytes,
+                     void* stream);
+
 /* ---- training step (reference model/DeepFMs.py:553-637) ---------------------------------- */
 
 /* Forward of a training step: as dfwfm_forward, and additionally keeps (in model-owned device

@@ -210,3 +210,37 @@ def test_device_metrics_exact_on_separated_logits(gpu):
     assert abs(m["auc"] - roc_auc_score(y, pred)) < 1e-12
     prec, rec, _ = precision_recall_curve(y, pred)
     assert abs(m["prauc"] - auc(rec, prec)) < 1e-12
+
+
+@pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_qr_mult", "deepfwfm_fwlw_lw", "deepfwfm_small_mlp"])
+@pytest.mark.parametrize("B", [1, 17, 256])
+def test_split_forward_is_bit_identical_to_fused(gpu, name, B, monkeypatch):
+    # dfwfm_forward_ws (gather launch + MLP launch, opt-in DFWFM_SPLIT=1, read at model creation)
+    # against dfwfm_forward (one fused launch)
+    import ctypes
+    from xsdeepfwfm_deprecated_amd import _lib
+    monkeypatch.setenv("DFWFM_SPLIT", "1")
+    cfg, params, xi, xv, *_ = load_golden(name)
+    m = make_model(cfg, params, gpu)
+    xi_t = torch.from_numpy(xi[:B]).to(gpu)
+    xv_t = torch.from_numpy(xv[:B]).to(gpu)
+    with torch.no_grad():
+        split = m(xi_t, xv_t)
+        eng = m._engine
+        n = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().dfwfm_forward_workspace_bytes(eng.handle, B, ctypes.byref(n)), "ws bytes")
+        assert n.value > 0  # deep models run split
+        fused = torch.empty(B, device=gpu)
+        s = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+        _lib.check(_lib.lib().dfwfm_forward(eng.handle, ctypes.c_void_p(xi_t.data_ptr()), xi_t.stride(0),
+                                            ctypes.c_void_p(xv_t.data_ptr()), xv_t.stride(0), B,
+                                            ctypes.c_void_p(fused.data_ptr()), s), "fused forward")
+        # a too-small workspace is refused
+        ws = torch.empty(n.value, dtype=torch.uint8, device=gpu)
+        rc = _lib.lib().dfwfm_forward_ws(eng.handle, ctypes.c_void_p(xi_t.data_ptr()), xi_t.stride(0),
+                                         ctypes.c_void_p(xv_t.data_ptr()), xv_t.stride(0), B,
+                                         ctypes.c_void_p(fused.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                         n.value - 4, s)
+        assert rc == -1
+    torch.cuda.synchronize()
+    assert torch.equal(split.cpu(), fused.cpu())

@@ -8,7 +8,7 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int T>
-__global__ void __launch_bounds__(256) mfma_loop(float* out, int iters, uint64_t* cyc) {
+__global__ void __launch_bounds__(512) mfma_loop(float* out, int iters, uint64_t* cyc) {
   f32x4 acc[T];
 #pragma unroll
   for (int j = 0; j < T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -22,19 +22,19 @@ __global__ void __launch_bounds__(256) mfma_loop(float* out, int iters, uint64_t
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < T; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
-  out[blockIdx.x * 256 + threadIdx.x] = s;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
 template <int T>
-void run(float* out, uint64_t* cyc, int iters) {
-  hipLaunchKernelGGL(mfma_loop<T>, dim3(256), dim3(256), 0, 0, out, iters, cyc);
+void run(float* out, uint64_t* cyc, int iters, int nth = 256) {
+  hipLaunchKernelGGL(mfma_loop<T>, dim3(256), dim3(nth), 0, 0, out, iters, cyc);
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  hipLaunchKernelGGL(mfma_loop<T>, dim3(256), dim3(256), 0, 0, out, iters, cyc);
+  hipLaunchKernelGGL(mfma_loop<T>, dim3(256), dim3(nth), 0, 0, out, iters, cyc);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -44,19 +44,21 @@ void run(float* out, uint64_t* cyc, int iters) {
   double mean = 0;
   for (int i = 0; i < 256; ++i) mean += c[i] / 256.0;
   const double n = (double)iters * T;
-  const double tflops = 256.0 * 4 * n * 2048 / (ms * 1e-3) / 1e12;
-  printf("T=%d: %.2f cycles/MFMA (s_memtime), %.1f TFLOP/s, clock %.2f GHz\n", T, mean / n, tflops,
+  const double tflops = 256.0 * (nth / 64) * n * 2048 / (ms * 1e-3) / 1e12;
+  printf("waves/CU=%d T=%d: %.2f cycles/MFMA (s_memtime), %.1f TFLOP/s, clock %.2f GHz\n", nth / 64, T, mean / n, tflops,
          mean / (ms * 1e-3) / 1e9);
 }
 
 int main() {
   float* out;
   uint64_t* cyc;
-  hipMalloc(&out, 256 * 256 * sizeof(float));
+  hipMalloc(&out, 256 * 512 * sizeof(float));
   hipMalloc(&cyc, 256 * sizeof(uint64_t));
   run<4>(out, cyc, 20000);
   run<6>(out, cyc, 20000);
   run<7>(out, cyc, 20000);
   run<8>(out, cyc, 20000);
+  run<6>(out, cyc, 20000, 512);
+  run<8>(out, cyc, 20000, 512);
   return 0;
 }

@@ -21,6 +21,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
+# A/B of build variants only (e.g. libdfwfm_ns4.so built with DFWFM_HIPCC_FLAGS=-DDFWFM_NSETS=4)
+LOAD_PATH = os.path.join(PKG_DIR, os.environ["DFWFM_LIB"]) if os.environ.get("DFWFM_LIB") else LIB_PATH
 SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_capi.hip"]
 HEADERS = ["dfwfm_internal.h", "dfwfm_device.h", os.path.join("..", "..", "include", "dfwfm.h")]
 ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
@@ -84,6 +86,9 @@ SIGNATURES = {
     "dfwfm_model_set_tables": (ctypes.c_int, [_P, ctypes.POINTER(dfwfm_field_tables), ctypes.c_int32, _P]),
     "dfwfm_model_set_dense": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P]),
     "dfwfm_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
+    "dfwfm_forward_workspace_bytes": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]),
+    "dfwfm_forward_ws": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P,
+                                        ctypes.c_size_t, _P]),
     "dfwfm_train_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P,
                                            ctypes.c_float, ctypes.c_uint32, _P]),
     "dfwfm_backward": (ctypes.c_int, [_P, _P, ctypes.POINTER(dfwfm_grads), _P]),
@@ -153,7 +158,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"] + os.environ.get("DFWFM_HIPCC_FLAGS", "").split()
     objs = [os.path.join(CSRC, os.path.splitext(s)[0] + ".o") for s in SOURCES]
 
+    hdr_m = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
+    stamp = os.path.join(CSRC, ".build_flags")  # objects built with other flags are stale
+    if not os.path.exists(stamp) or open(stamp).read() != " ".join(flags):
+        force = True
+
     def compile_one(i):
+        src = os.path.join(CSRC, SOURCES[i])
+        if not force and os.path.exists(objs[i]) and \
+                os.path.getmtime(objs[i]) >= max(os.path.getmtime(src), hdr_m):
+            return  # object up to date (kept between builds; *.o is git- and gpurun-ignored)
         cmd = [hipcc] + flags + ["-c", "-o", objs[i], os.path.join(CSRC, SOURCES[i])]
         if verbose:
             print(" ".join(cmd))
@@ -161,10 +175,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         list(ex.map(compile_one, range(len(SOURCES))))
+    with open(stamp, "w") as f:
+        f.write(" ".join(flags))
     tmp = LIB_PATH + ".tmp"
     subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", tmp] + objs, check=True, cwd=CSRC)
-    for o in objs:
-        os.remove(o)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
@@ -207,10 +221,10 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB_PATH):
-            raise DfwfmError(f"{LIB_PATH} is missing: run xsdeepfwfm_deprecated_amd.build() "
+        if not os.path.exists(LOAD_PATH):
+            raise DfwfmError(f"{LOAD_PATH} is missing: run xsdeepfwfm_deprecated_amd.build() "
                              "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(LOAD_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -22,6 +22,10 @@ struct dfwfm_model {
   int TPWF, tail;  // forward: full tiles per wave, split-tail mode (NT == 4*TPWF + 1); TPW = ceil(NT/4)
   int flags;
   size_t lds_bytes;
+  size_t lds_gather;   // split forward: LDS of the gather launch (no MLP buffers)
+  int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
+  size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
+  int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
   // device state (owned)
   FieldDev* d_fields;
   float* d_upack;  // FwFM A-operand fragments [MT][S][64]
@@ -35,6 +39,8 @@ struct dfwfm_model {
   float* d_bias;   // [1]
   uint64_t* d_stamps;  // diagnostics (DFWFM_DIAG_STAMPS)
   size_t stamps_cap;   // workgroups the stamp buffer holds
+  size_t stamps_ring;  // launches kept (DFWFM_DIAG_RING), each its own slice of the buffer
+  size_t stamps_next;  // next slice
   // training
   float4* d_wtpack;    // transposed MLP packs for dX_{l-1} = G_l W_l
   size_t wtpack_elems;
@@ -189,7 +195,32 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   const LdsLayout L = lds_layout(F, D, m->MT, m->S, m->SX, m->SY, m->TPWF > 0 ? m->TPWF : 1, m->KS,
                                  c.use_deep != 0, m->tail != 0);
   m->lds_bytes = sizeof(float) * (size_t)L.total;
-  if (m->lds_bytes > 160 * 1024) {
+  m->lds_gather = sizeof(float) * (size_t)lds_layout(F, D, m->MT, m->S, m->SX, m->SY, m->TPWF > 0 ? m->TPWF : 1,
+                                                     1, false, false).total;
+  // inference: eight tile groups (two waves per SIMD at <= 128 registers) when the layer fits them
+  // (<= 32 output tiles); DFWFM_NG=4 selects the four-wave kernel the training forward uses
+  m->NG = 4;
+  m->TPWI = m->TPWF;
+  m->tailI = m->tail;
+  m->lds_inf = m->lds_bytes;
+  if (c.use_deep && m->KS == 1 && NT <= 32 && m->NC0 <= 32) {
+    const char* ng = getenv("DFWFM_NG");
+    if (!ng || atoi(ng) == 8) {
+      m->NG = 8;
+      m->tailI = (NT % 8 == 1 && NT >= 9 && m->NC0 >= 8 && !getenv("DFWFM_NO_TAIL")) ? 1 : 0;
+      m->TPWI = m->tailI ? NT / 8 : (NT + 7) / 8;
+      m->lds_inf = sizeof(float) * (size_t)lds_layout(F, D, m->MT, m->S, m->SX, m->SY, m->TPWI, 1, true,
+                                                      m->tailI != 0, 8).total;
+    }
+  }
+  // split forward (opt-in, DFWFM_SPLIT=1): the gather / shallow part and the MLP as two launches, each
+  // with its own roofline (HBM-bound gather, MFMA-bound MLP) for profiling.  Measured slower than the
+  // fused launch (50.4 vs 43.0 us per batch alone, 43.4 vs 35.5 with two batches in flight): under a
+  // co-resident MLP's weight stream the gather launch's dependent loads wait ~3x longer, and in the
+  // fused kernel that wait is hidden behind the other workgroup's MLP instead of serialised
+  const char* sp = getenv("DFWFM_SPLIT");
+  m->split = (c.use_deep && m->KS == 1 && sp && atoi(sp) != 0) ? 1 : 0;
+  if (m->lds_bytes > 160 * 1024 || m->lds_inf > 160 * 1024) {
     free_model(m);
     return fail(DFWFM_ERR_UNSUPPORTED, "LDS tile of %zu bytes exceeds 160 KiB", m->lds_bytes);
   }
@@ -408,20 +439,33 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   return DFWFM_OK;
 }
 
+// split forward workspace: E rows [B][NC0*16] then first + second [B]
+size_t split_e_floats(const dfwfm_model* m, int64_t batch) { return (size_t)batch * m->NC0 * 16; }
+size_t split_ws_bytes(const dfwfm_model* m, int64_t batch) {
+  return sizeof(float) * (split_e_floats(m, batch) + (size_t)batch);
+}
+
 // diagnostics only: with DFWFM_DIAG_STAMPS=<which> the launch records per-workgroup phase clocks
 int diag_stamps_buffer(dfwfm_model* m, int64_t batch, int which, uint64_t** out) {
   *out = nullptr;
   const char* stv = getenv("DFWFM_DIAG_STAMPS");
   if (!stv || atoi(stv) != which) return DFWFM_OK;
   const size_t grid = (size_t)((batch + kBM - 1) / kBM);
-  if (grid > m->stamps_cap) {
+  // DFWFM_DIAG_RING=R: R launches in a row (e.g. captured into graphs on several streams) each get
+  // their own slice, for a cross-launch timeline (tools/timeline.py)
+  const char* rv = getenv("DFWFM_DIAG_RING");
+  const size_t ring = rv && atoi(rv) > 1 ? (size_t)atoi(rv) : 1;
+  if (grid > m->stamps_cap || ring != m->stamps_ring) {
     if (m->d_stamps) (void)hipFree(m->d_stamps);
     m->d_stamps = nullptr;
     m->stamps_cap = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_stamps), grid * kStampSlots * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_stamps), ring * grid * kStampSlots * sizeof(uint64_t)));
     m->stamps_cap = grid;
+    m->stamps_ring = ring;
+    m->stamps_next = 0;
   }
-  *out = m->d_stamps;
+  *out = m->d_stamps + (m->stamps_next % ring) * m->stamps_cap * kStampSlots;
+  m->stamps_next++;
   return DFWFM_OK;
 }
 
@@ -440,7 +484,38 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
-  hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, m->KS, m->lds_bytes, (hipStream_t)stream);
+  a.tail = m->tailI;
+  hipError_t e = launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "forward launch");
+  return DFWFM_OK;
+}
+
+int dfwfm_forward_workspace_bytes(dfwfm_model* m, int64_t batch, size_t* bytes) {
+  if (!m || !bytes || batch < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  *bytes = m->split ? split_ws_bytes(m, batch) : 0;
+  return DFWFM_OK;
+}
+
+int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
+                     int64_t batch, float* out, void* workspace, size_t ws_bytes, void* stream) {
+  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  if (!m->split || !workspace) return dfwfm_forward(m, xi, xi_stride, xv, xv_stride, batch, out, stream);
+  int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
+  if (rc != DFWFM_OK || batch == 0) return rc;
+  if (ws_bytes < split_ws_bytes(m, batch))
+    return fail(DFWFM_ERR_INVALID_ARG, "workspace of %zu bytes < %zu (dfwfm_forward_workspace_bytes)", ws_bytes,
+                split_ws_bytes(m, batch));
+  if (reinterpret_cast<uintptr_t>(workspace) % 16) return fail(DFWFM_ERR_INVALID_ARG, "workspace not 16-byte aligned");
+  FwdArgs a;
+  fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, out);
+  if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
+  a.part_stride = m->NC0 * 16;
+  a.part_e = static_cast<float*>(workspace);
+  a.part_fs = a.part_e + split_e_floats(m, batch);
+  if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
+  a.tail = m->tailI;
+  hipError_t e = launch_forward_split(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->NG, m->lds_gather, m->lds_inf,
+                                      (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
 }
@@ -482,7 +557,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   a.seed = seed;
   a.seed_src = m->step_src;
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
-  hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, 1, m->lds_bytes, (hipStream_t)stream);
+  hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, 1, 4, m->lds_bytes, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
   m->trained = true;
   return DFWFM_OK;
@@ -845,7 +920,7 @@ int dfwfm_eval_metrics(const float* z, const float* y, int64_t n, double* out, v
 int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream) {
   if (!m || !host || n < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
   if (!m->d_stamps) return fail(DFWFM_ERR_STATE, "no stamps recorded (set DFWFM_DIAG_STAMPS=1)");
-  const size_t cap = m->stamps_cap * kStampSlots;
+  const size_t cap = m->stamps_cap * kStampSlots * (m->stamps_ring ? m->stamps_ring : 1);
   const size_t cnt = (size_t)n < cap ? (size_t)n : cap;
   HIP_TRY(hipMemcpyAsync(host, m->d_stamps, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));

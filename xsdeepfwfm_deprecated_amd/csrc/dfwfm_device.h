@@ -31,6 +31,18 @@ __device__ __forceinline__ void stamp_rt(uint64_t* st, int slot, int tid) {
   if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
+// workgroup start (slot 14) / end (slot 15) on the 100 MHz clock; the end word carries the XCC and
+// the CU / SH / SE bits of HW_ID in bits 48-59, for a cross-launch timeline (tools/timeline.py)
+__device__ __forceinline__ void stamp_start_rt(uint64_t* st, int tid) { stamp_rt(st, 14, tid); }
+__device__ __forceinline__ void stamp_end_rt(uint64_t* st, int tid) {
+  if (st != nullptr && tid == 0) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+    const uint64_t id = (uint64_t)(((xcc & 0xF) << 8) | ((hw >> 8) & 0xFF));
+    st[(size_t)blockIdx.x * kStampSlots + 15] = __builtin_amdgcn_s_memrealtime() | (id << 48);
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict__ src) {
   if constexpr (D % 4 == 0) {
@@ -98,7 +110,7 @@ __device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[TPW], const float4& a, c
 // c0, c0+KS, ... of the packed [NT][NC][64] float4 layout.  Loads are buffer loads: the per-tile
 // base and the chunk offset are scalar (SALU), the only vector operand is lane*16 -- flat loads
 // spent a 64-bit VALU add per load in front of the MFMAs.
-template <int TPW, int KS>
+template <int TPW, int KS, int NG = 4>
 struct LayerStream {
   __amdgpu_buffer_rsrc_t rsrc;
   int sbase[TPW];  // byte offset of each owned tile's [NC][64] block (wave-uniform)
@@ -107,7 +119,7 @@ struct LayerStream {
     rsrc = r;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-      int t = g + 4 * j;
+      int t = g + NG * j;
       t = t < NT ? t : NT - 1;
       sbase[j] = __builtin_amdgcn_readfirstlane((layer_off + t * NC * 64) * 16);
     }
@@ -136,9 +148,9 @@ struct LayerStream {
 // them and the next step's first MFMA waited out the LDS latency.  Within a step the LDS read goes
 // first, then the refill loads interleave with the MFMAs (sched_group_barrier: 2 MFMA, 1 load,
 // ...), and a sched_barrier closes the step so hipcc cannot sink them to their use.
-template <int TPW, int KS>
+template <int TPW, int KS, int NG = 4>
 __device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __restrict__ act, int SA,
-                                           const LayerStream<TPW, KS>& ls, f32x4 (&b0)[TPW],
+                                           const LayerStream<TPW, KS, NG>& ls, f32x4 (&b0)[TPW],
                                            f32x4 (&b1)[TPW], f32x4 (&b2)[TPW], int lane) {
 #pragma unroll
   for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -149,53 +161,78 @@ __device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __res
   float4 a0 = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(0));
   float4 a1 = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(1));
   float4 a2;
+#define DFWFM_MFMA_STEP(X, AX)                                                         \
+  mfma_chunk<TPW>(acc, AX, X);                                                         \
+  __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                   \
+  for (int q = 0; q < TPW; ++q) {                                                      \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                 \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                 \
+  }                                                                                    \
+  __builtin_amdgcn_sched_group_barrier(0x008, 2 * TPW, 0);                             \
+  __builtin_amdgcn_sched_barrier(0);
+  // a step that refills the set it frees with chunk i + 2
 #define DFWFM_STEP(X, AX, Z, AZ, i)                                                    \
   {                                                                                    \
     AZ = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk((i) + 2));              \
     ls.load(Z, ls.chunk((i) + 2), voff);                                               \
-    mfma_chunk<TPW>(acc, AX, X);                                                       \
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                 \
-    for (int q = 0; q < TPW; ++q) {                                                    \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                               \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                               \
-    }                                                                                  \
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TPW, 0);                           \
-    __builtin_amdgcn_sched_barrier(0);                                                 \
+    DFWFM_MFMA_STEP(X, AX)                                                             \
   }
+  // a drain step (no chunk left to fetch): no load at all -- a load of a chunk nobody consumes keeps a
+  // register busy past the loop and the epilogue then waits for it, i.e. for the next layer's preload
+#define DFWFM_STEP_N(X, AX) \
+  { DFWFM_MFMA_STEP(X, AX) }
   int i = 0;
-  for (; i + 3 <= n; i += 3) {
+  for (; i + 5 <= n; i += 3) {  // steady state: steps i..i+2 fetch chunks i+2..i+4 < n
     DFWFM_STEP(b0, a0, b2, a2, i);
     DFWFM_STEP(b1, a1, b0, a0, i + 1);
     DFWFM_STEP(b2, a2, b1, a1, i + 2);
   }
-  if (i < n) DFWFM_STEP(b0, a0, b2, a2, i);
-  if (i + 1 < n) DFWFM_STEP(b1, a1, b0, a0, i + 1);
+  const int r = n - i;  // 1..4 steps left; step j fetches chunk i + j + 2 only while that is < n
+  if (r == 1) {
+    DFWFM_STEP_N(b0, a0);
+  } else if (r == 2) {
+    DFWFM_STEP_N(b0, a0);
+    DFWFM_STEP_N(b1, a1);
+  } else if (r == 3) {
+    DFWFM_STEP(b0, a0, b2, a2, i);
+    DFWFM_STEP_N(b1, a1);
+    DFWFM_STEP_N(b2, a2);
+  } else {
+    DFWFM_STEP(b0, a0, b2, a2, i);
+    DFWFM_STEP(b1, a1, b0, a0, i + 1);
+    DFWFM_STEP_N(b2, a2);
+    DFWFM_STEP_N(b0, a0);
+  }
+#undef DFWFM_STEP_N
 #undef DFWFM_STEP
+#undef DFWFM_MFMA_STEP
 }
 
 // The split tail tile: when the layer has 4*TPW + 1 output tiles, tile T = 4*TPW is shared by the
 // four waves, wave g taking K chunks [NC*g/4, NC*(g+1)/4) of it, so every SIMD carries 6.25 tiles
 // instead of one carrying 7.  All of a wave's tail fragments are loaded with the layer's preload
 // (kTailC <= 8 chunks per wave, NC <= 32) and consumed after the main K loop.
+template <int NG = 4>
 struct TailStream {
+  static constexpr int C = kTailC * 4 / NG;  // K chunks per wave at most (layer widths <= 512)
   int sbase, c_lo, cnt;
   __device__ __forceinline__ void init(int layer_off, int NC, int T, int g) {
     sbase = __builtin_amdgcn_readfirstlane((layer_off + T * NC * 64) * 16);
-    c_lo = (NC * g) >> 2;
-    cnt = ((NC * (g + 1)) >> 2) - c_lo;
+    c_lo = (NC * g) / NG;
+    cnt = (NC * (g + 1)) / NG - c_lo;
   }
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, f32x4 (&tw)[kTailC], int voff) const {
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, f32x4 (&tw)[C], int voff) const {
 #pragma unroll
-    for (int u = 0; u < kTailC; ++u)
+    for (int u = 0; u < C; ++u)
       if (u < cnt)
         tw[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, sbase + (c_lo + u) * 1024, 0));
   }
   // this wave's partial product of the tail tile (two accumulators: no back-to-back dependent MFMAs)
-  __device__ __forceinline__ f32x4 mma(const float* __restrict__ act, int SA, const f32x4 (&tw)[kTailC], int lane) const {
+  __device__ __forceinline__ f32x4 mma(const float* __restrict__ act, int SA, const f32x4 (&tw)[C], int lane) const {
     const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
     f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
-    for (int u = 0; u < kTailC; ++u) {
+    for (int u = 0; u < C; ++u) {
       if (u < cnt) {
         const float4 a = *reinterpret_cast<const float4*>(arow + 16 * (c_lo + u));
         f32x4& c = (u & 1) ? a1 : a0;

@@ -76,6 +76,10 @@ struct FwdArgs {
   float drop_scale;         // 1 / (1 - p)
   uint32_t seed;            // dropout hash seed of this step
   const int64_t* seed_src;  // device step counter mixed into the seed (graph replay), or null
+  // split forward (launch_forward_split): the gather launch writes, the MLP launch reads
+  float* part_e;            // [B][part_stride] E tile rows (W0 columns, zero padded past F*D)
+  float* part_fs;           // [B] first + second order
+  int32_t part_stride;      // floats per row (W0, a multiple of 4)
 };
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.
@@ -86,7 +90,7 @@ struct LdsLayout {
 __host__ __device__ inline int r4(int x) { return (x + 3) & ~3; }
 
 __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int SX, int SY, int TPW, int KS,
-                                                bool deep, bool tail) {
+                                                bool deep, bool tail, int NG = 4) {
   LdsLayout L;
   int o = 0;
   L.desc = o;  o += r4(14 * F);
@@ -96,10 +100,10 @@ __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int
   L.bufX = o;  o += kBM * SX;
   L.bufY = o;  o += deep ? kBM * SY : 0;
   L.red = o;   o += (deep && KS == 2) ? 4 * TPW * 64 * 4 : 0;
-  L.tailr = o; o += (deep && tail) ? 4 * 64 * 4 + kBM : 0;  // partials + per-row deep sums of the tail
+  L.tailr = o; o += (deep && tail) ? NG * 64 * 4 + kBM : 0;  // partials + per-row deep sums of the tail
   L.fo = o;    o += kBM * r4(F);
   L.part2 = o; o += r4(kBM * D);
-  L.dsum = o;  o += 4 * kBM;
+  L.dsum = o;  o += NG * kBM;
   L.fs = o;    o += kBM;
   L.total = r4(o);
   return L;
@@ -274,7 +278,8 @@ hipError_t launch_metrics(const float* z, const float* y, int64_t n, double* out
                           hipStream_t s);
 
 bool supported_embedding_size(int D);
-hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, hipStream_t s);
+hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s);
+hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 hipError_t launch_backward(const BwdArgs& a, int D, int tpw, size_t lds, hipStream_t s);
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);

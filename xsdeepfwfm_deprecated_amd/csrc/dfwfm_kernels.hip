@@ -42,11 +42,19 @@ namespace dfwfm {
 #define DFWFM_FWD_WPE 2  // register budget of two waves per SIMD (<= 256 per lane): a second batch's
                          // workgroup fits beside this one (stream-level overlap)
 #endif
-template <int D, int TPW, int KS, bool TRAIN>
-__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(DFWFM_FWD_WPE)))
+// PART: 0 = the whole forward in one launch; 1 = stage, gather and shallow part only, E tile and
+// first + second to p.part_e / p.part_fs; 2 = MLP and combine from p.part_e / p.part_fs (the split
+// forward: two launches per batch, see launch_forward_split)
+// NG: MLP output-tile groups = waves (4: one wave per SIMD, <= 256 registers; 8: two per SIMD, <= 128
+// registers, so one workgroup issues MFMAs from two waves per SIMD while a second batch's workgroup
+// on the same CU runs its gather)
+template <int D, int TPW, int KS, bool TRAIN, int PART, int NG>
+__global__ void __launch_bounds__(64 * NG * KS)
+__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (NG == 8 ? 4 : DFWFM_FWD_WPE))))
 fwd_kernel(FwdArgs p) {
-  constexpr int NTH = 256 * KS;
-  constexpr int NW = 4 * KS;
+  static_assert(NG == 4 || (NG == 8 && KS == 1 && !TRAIN), "8 tile groups: inference, no K split");
+  constexpr int NTH = 64 * NG * KS;
+  constexpr int NW = NG * KS;
   constexpr int RPT = (kBM * 64 + NTH - 1) / NTH;  // gather rows per thread (F <= 64)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -57,10 +65,10 @@ fwd_kernel(FwdArgs p) {
   const int SX = p.SX;
   const int SY = p.SY;
   const int flags = p.flags;
-  const bool deep = (flags & kHasDeep) != 0;
+  const bool deep = PART != 1 && (flags & kHasDeep) != 0;  // the MLP runs in this launch
   const int Fp = r4(F);
   const bool tail = KS == 1 && p.tail != 0;
-  const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep, tail);
+  const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep, tail, NG);  // PART 1: no MLP buffers
   FieldDev* desc = reinterpret_cast<FieldDev*>(smem + L.desc);
   float* lw_s = smem + L.lw;
   float* fwlw_s = smem + L.fwlw;
@@ -76,21 +84,67 @@ fwd_kernel(FwdArgs p) {
 
   const int64_t b0 = (int64_t)blockIdx.x * kBM;
   stamp(p.stamps, 0, tid);
-  const int g = wave & 3;   // MLP output-tile group
-  const int kh = wave >> 2; // MLP K half (KS == 2)
+  stamp_start_rt(p.stamps, tid);
+  const int g = wave & (NG - 1);  // MLP output-tile group
+  const int kh = wave / NG;       // MLP K half (KS == 2)
 
-  LayerStream<TPW, KS> ls;
+  LayerStream<TPW, KS, NG> ls;
   // weight fragments: three register sets, prefetch distance 2 chunks (a fourth set / distance 3
   // measured slower)
   f32x4 wb0[TPW], wb1[TPW], wb2[TPW];
 #define DFWFM_PRELOAD(LS) (LS).preload(wb0, wb1, lane * 16)
-#define DFWFM_KLOOP(ACC, IN, SA, LS) mlp_k_loop<TPW, KS>(ACC, IN, SA, LS, wb0, wb1, wb2, lane)
+#define DFWFM_KLOOP(ACC, IN, SA, LS) mlp_k_loop<TPW, KS, NG>(ACC, IN, SA, LS, wb0, wb1, wb2, lane)
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float4*>(p.wpack), (short)0, p.wpack_bytes, 0x00020000);
-  TailStream ts;
-  f32x4 tw[kTailC];
-  constexpr int TT = 4 * TPW;  // the tail tile (when p.tail)
+  // biases [H][NT*16] and net_1_fc [NT*16] (padded, so every tile's lanes are in range)
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.mlp_b), (short)0, p.H * p.NT * 16 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.fc), (short)0, p.NT * 16 * 4, 0x00020000);
+  TailStream<NG> ts;
+  f32x4 tw[TailStream<NG>::C];
+  constexpr int TT = NG * TPW;  // the tail tile (when p.tail)
 
+  constexpr bool train = TRAIN;
+  const int FD = F * D;
+  const int SE = r4(FD);  // row stride of the saved E / X_0 tiles
+  const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
+  const bool drop0 = train && deep && (flags & kDrop) != 0;
+  if constexpr (PART == 2) {
+    // ---- the E tile and first + second of the gather launch; layer-0 weights behind them ----------
+    constexpr int kEPT = (kBM * 128 + NTH - 1) / NTH;  // float4 of the tile per thread (<= 512 columns)
+    const int PS4 = p.part_stride >> 2;
+    const int n4 = kBM * PS4;
+    f32x4 ev[kEPT];
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k) {
+      const int i = tid + k * NTH;
+      const int b = i / PS4;
+      ev[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (i < n4 && b < nrows) ev[k] = reinterpret_cast<const f32x4*>(p.part_e + (b0 + b) * p.part_stride)[i - b * PS4];
+    }
+    const float fsv = tid < nrows ? p.part_fs[b0 + tid] : 0.f;
+    ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
+    DFWFM_PRELOAD(ls);
+    if (tail) {
+      ts.init(0, p.NC0, TT, g);
+      ts.load(wrsrc, tw, lane * 16);
+    }
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k) {
+      const int i = tid + k * NTH;
+      const int b = i / PS4;
+      if (i < n4) reinterpret_cast<f32x4*>(bufX + b * SX)[i - b * PS4] = ev[k];
+    }
+    for (int i = tid + kEPT * NTH; i < n4; i += NTH) {  // rows wider than 512 columns
+      const int b = i / PS4;
+      reinterpret_cast<float4*>(bufX + b * SX)[i - b * PS4] =
+          b < nrows ? reinterpret_cast<const float4*>(p.part_e + (b0 + b) * p.part_stride)[i - b * PS4]
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < kBM) fs[tid] = fsv;
+    __syncthreads();
+  } else {
   // ---- phase 0: field descriptors -> LDS; this thread's Xi / Xv; shallow parameters in flight --
   // Every load is issued before any is consumed (a load-then-store loop waits one round trip per
   // iteration).  Only the descriptors and the tile's Xi / Xv gate the gather; the FwFM fragments,
@@ -98,11 +152,14 @@ fwd_kernel(FwdArgs p) {
   constexpr int kDescPT = (7 * 64 + NTH - 1) / NTH;    // uint2 words of descriptors per thread
   constexpr int kUpkPT = (kMaxMT * 16 * 16 + NTH - 1) / NTH;  // float4 of FwFM fragments per thread
   constexpr int kFwlwPT = (64 * 32 + NTH - 1) / NTH;   // fwlw floats per thread
-  uint2 dw[kDescPT];
+  // ext-vector element types throughout: HIP's uint2 / float4 are unions, which keeps these arrays out
+  // of registers (scratch, and a vmcnt(0) at every spill point)
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 dw[kDescPT];
 #pragma unroll
   for (int k = 0; k < kDescPT; ++k) {
     const int i = tid + k * NTH;
-    if (i < 7 * F) dw[k] = reinterpret_cast<const uint2*>(p.fields)[i];
+    if (i < 7 * F) dw[k] = reinterpret_cast<const u32x2*>(p.fields)[i];
   }
   int64_t key[RPT];  // gather row r -> field f = r / 16, sample b = r % 16: index or Xv bits
 #pragma unroll
@@ -118,12 +175,12 @@ fwd_kernel(FwdArgs p) {
         key[k] = p.xi[gb * p.xi_stride + (f - num)];
     }
   }
-  float4 uw[kUpkPT];
+  f32x4 uw[kUpkPT];
   const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
 #pragma unroll
   for (int k = 0; k < kUpkPT; ++k) {
     const int i = tid + k * NTH;
-    if (i < n_upk) uw[k] = reinterpret_cast<const float4*>(p.upack)[i];
+    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(p.upack)[i];
   }
   float fw[kFwlwPT];
   const int n_fwlw = (flags & kFoFwlw) ? F * D : 0;
@@ -136,7 +193,7 @@ fwd_kernel(FwdArgs p) {
 #pragma unroll
   for (int k = 0; k < kDescPT; ++k) {
     const int i = tid + k * NTH;
-    if (i < 7 * F) reinterpret_cast<uint2*>(desc)[i] = dw[k];
+    if (i < 7 * F) reinterpret_cast<u32x2*>(desc)[i] = dw[k];
   }
   __syncthreads();
   stamp(p.stamps, 1, tid);
@@ -220,7 +277,7 @@ fwd_kernel(FwdArgs p) {
 #pragma unroll
     for (int k = 0; k < kUpkPT; ++k) {
       const int i = tid + k * NTH;
-      if (i < n_upk) reinterpret_cast<float4*>(upk)[i] = uw[k];
+      if (i < n_upk) reinterpret_cast<f32x4*>(upk)[i] = uw[k];
     }
 #pragma unroll
     for (int k = 0; k < kFwlwPT; ++k) {
@@ -253,11 +310,10 @@ fwd_kernel(FwdArgs p) {
   }
   __syncthreads();
   stamp(p.stamps, 2, tid);
-  constexpr bool train = TRAIN;
-  const int FD = F * D;
-  const int SE = r4(FD);  // row stride of the saved E / X_0 tiles
-  const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
-  const bool drop0 = train && deep && (flags & kDrop) != 0;
+  if constexpr (PART == 1) {
+    // the E tile (W0 columns, zero padded past F*D) for the MLP launch, behind the shallow part
+    store_tile(p.part_e + b0 * p.part_stride, p.part_stride, bufX, SX, nrows, p.part_stride >> 2, tid, NTH);
+  }
   if constexpr (train) {
     // E for the shallow backward.  Without deep-tower dropout E is also X_0 and is saved after
     // layer 1's K loop from the same LDS tile (stores issued behind that layer's weight stream)
@@ -380,9 +436,14 @@ fwd_kernel(FwdArgs p) {
 
   if (!deep) {
     __syncthreads();
-    if (tid < kBM && b0 + tid < p.batch) p.out[b0 + tid] = fs[tid] + p.bias[0];
+    if constexpr (PART == 1) {
+      if (tid < kBM && b0 + tid < p.batch) p.part_fs[b0 + tid] = fs[tid];
+    } else {
+      if (tid < kBM && b0 + tid < p.batch) p.out[b0 + tid] = fs[tid] + p.bias[0];
+    }
     return;
   }
+  }  // PART != 2
 
   stamp(p.stamps, 3, tid);
   if constexpr (train) __syncthreads();  // the dropped X_0 tile is complete before layer 1 reads it
@@ -390,7 +451,6 @@ fwd_kernel(FwdArgs p) {
   const int row0 = (lane >> 4) * 4;
   const bool drop = train && (flags & kDrop) != 0;
   const uint32_t hseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
-  float dpart[4] = {0.f, 0.f, 0.f, 0.f};
   int layer_off = 0;  // float4 offset of layer h in wpack
   for (int h = 0; h < p.H; ++h) {
     const bool even = (h & 1) == 0;
@@ -400,48 +460,32 @@ fwd_kernel(FwdArgs p) {
     const int SO = even ? SY : SX;
     const int NC = h == 0 ? p.NC0 : p.NT;
     const bool last = h == p.H - 1;
-    const float* bias = p.mlp_b + (size_t)h * p.NT * 16;
-
-    // epilogue operands, fetched before the K loop so they arrive under it
+    // epilogue operands, fetched before the K loop so they arrive under it; buffer loads (scalar layer
+    // offset, 32-bit lane offset): per-tile 64-bit addresses would be kept across the layer loop
+    const int boff = h * p.NT * 16 * 4;
     float bn[TPW], wf[TPW];
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-      int t = g + 4 * j;
+      int t = g + NG * j;
       t = t < p.NT ? t : p.NT - 1;
-      const int n = t * 16 + (lane & 15);
-      bn[j] = bias[n];
-      wf[j] = last ? p.fc[n] : 0.f;
+      const int n4 = (t * 16 + (lane & 15)) * 4;
+      bn[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, n4, boff, 0));
+      wf[j] = last ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(frsrc, n4, 0, 0)) : 0.f;
     }
 
     float bn_t = 0.f, wf_t = 0.f;
     if (tail) {
-      const int n = TT * 16 + (lane & 15);
-      bn_t = bias[n];
-      wf_t = last ? p.fc[n] : 0.f;
+      const int n4 = (TT * 16 + (lane & 15)) * 4;
+      bn_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, n4, boff, 0));
+      wf_t = last ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(frsrc, n4, 0, 0)) : 0.f;
     }
 
+    // the tail tile's share first: its fragments (loaded with the preload) are then dead during the
+    // K loop, which runs at the register budget
+    if (tail) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.mma(in, SA, tw, lane);
     f32x4 acc[TPW];
     DFWFM_KLOOP(acc, in, SA, ls);
-    if (tail) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.mma(in, SA, tw, lane);
     if (h == 0) stamp(p.stamps, 12, tid);
-    // next layer's first chunks go out now, ahead of this layer's epilogue and barrier
-    layer_off += p.NT * NC * 64;
-    if (!last) {
-      ls.init(wrsrc, layer_off, p.NT, p.NT, g, kh);
-      DFWFM_PRELOAD(ls);
-      if (tail) {
-        ts.init(layer_off, p.NT, TT, g);
-        ts.load(wrsrc, tw, lane * 16);
-      }
-    }
-    if constexpr (train) {
-      // this layer's input X_h for the backward, from LDS (intact until the next layer's epilogue):
-      // behind the next layer's preload, so those loads do not wait for the stores (vmcnt is in order)
-      if (h == 0)
-        store_tile(p.sv_x[0] + b0 * SE, SE, in, SA, nrows, SE / 4, tid, NTH);
-      else
-        store_tile(p.sv_x[h] + b0 * p.N, p.N, in, SA, nrows, p.N / 4, tid, NTH);
-    }
     if constexpr (KS == 2) {
       if (kh == 1) {
 #pragma unroll
@@ -453,11 +497,12 @@ fwd_kernel(FwdArgs p) {
         for (int j = 0; j < TPW; ++j) acc[j] += red[(g * TPW + j) * 64 + lane];
       }
     }
+    float dpart[4] = {0.f, 0.f, 0.f, 0.f};  // last layer: this lane's share of deep[b] (not live across layers)
     if (kh == 0) {
       // C/D layout: col = lane&15 (neuron), row = (lane>>4)*4 + r (sample)
 #pragma unroll
       for (int j = 0; j < TPW; ++j) {
-        const int t = g + 4 * j;
+        const int t = g + NG * j;
         if (t < p.NT) {
           const int n = t * 16 + (lane & 15);
           const bool valid = n < p.N;  // padded neurons stay exactly 0 (bias/fc pads are 0)
@@ -484,29 +529,62 @@ fwd_kernel(FwdArgs p) {
         }
       }
     }
+    if (last && kh == 0) {
+      // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the 16 lanes sharing (lane>>4), then (after the
+      // final barrier) the NG groups
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dpart[r] = sum16(dpart[r]);
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dsum[g * kBM + row0 + r] = dpart[r];
+      }
+    }
+    // next layer's first chunks go out now, ahead of the barrier -- but after the epilogue: once they
+    // are issued, any wait on a vector-memory result (a bias, a spill reload) waits for them too
+    layer_off += p.NT * NC * 64;
+    if (!last) {
+      ls.init(wrsrc, layer_off, p.NT, p.NT, g, kh);
+      DFWFM_PRELOAD(ls);
+      if (tail) {
+        ts.init(layer_off, p.NT, TT, g);
+        ts.load(wrsrc, tw, lane * 16);
+      }
+    }
+    if constexpr (train) {
+      // this layer's input X_h for the backward, from LDS (intact until the next layer's epilogue):
+      // behind the next layer's preload, so those loads do not wait for the stores (vmcnt is in order)
+      if (h == 0)
+        store_tile(p.sv_x[0] + b0 * SE, SE, in, SA, nrows, SE / 4, tid, NTH);
+      else
+        store_tile(p.sv_x[h] + b0 * p.N, p.N, in, SA, nrows, p.N / 4, tid, NTH);
+    }
     if (h == 0) stamp(p.stamps, 13, tid);
     __syncthreads();
     if (tail) {
-      // the tail tile: wave g finishes row (lane>>4)*4 + g of it from the four partial products
-      const int n = TT * 16 + (lane & 15);
-      const bool valid = n < p.N;
-      const int rr = row0 + g;
-      const float* tp = tailr + lane * 4 + g;
-      const float sum = ((tp[0] + tp[256]) + tp[512]) + tp[768];
-      float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
-      if constexpr (train) {
-        if (drop) v = dropout_keep(hseed, h + 1, b0 + rr, n, p.drop_p) ? v * p.drop_scale : 0.f;
-        if (last) outa[rr * SO + n] = v;  // X_H is saved from LDS
+      // the tail tile: wave g < 4 finishes row (lane>>4)*4 + g of it from the NG partial products
+      if (g < 4) {
+        const int n = TT * 16 + (lane & 15);
+        const bool valid = n < p.N;
+        const int rr = row0 + g;
+        const float* tp = tailr + lane * 4 + g;
+        float sum = tp[0];
+#pragma unroll
+        for (int w = 1; w < NG; ++w) sum += tp[w * 256];
+        float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
+        if constexpr (train) {
+          if (drop) v = dropout_keep(hseed, h + 1, b0 + rr, n, p.drop_p) ? v * p.drop_scale : 0.f;
+          if (last) outa[rr * SO + n] = v;  // X_H is saved from LDS
+        }
+        if (!last) {
+          outa[rr * SO + n] = v;
+        } else {
+          // the tail's share of deep[b] for row rr, summed over its 16 columns; added last in the final
+          // combine, so a row's logit does not depend on its slot in the tile
+          const float c = sum16(v * wf_t);
+          if ((lane & 15) == 0) tailr[NG * 64 * 4 + rr] = c;
+        }
       }
-      if (!last) {
-        outa[rr * SO + n] = v;
-        __syncthreads();
-      } else {
-        // the tail's share of deep[b] for row rr, summed over its 16 columns; added last in the final
-        // combine, so a row's logit does not depend on its slot in the tile
-        const float c = sum16(v * wf_t);
-        if ((lane & 15) == 0) tailr[4 * 64 * 4 + rr] = c;
-      }
+      if (!last) __syncthreads();
     }
     stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
   }
@@ -519,29 +597,16 @@ fwd_kernel(FwdArgs p) {
     store_tile(p.sv_x[p.H] + b0 * p.N, p.N, last_out, SL, nrows, p.N / 4, tid, NTH);
   }
 
-  // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the 16 lanes sharing (lane>>4), then the 4 groups
-  if (kh == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = dpart[r];
-      v += __shfl_xor(v, 8);
-      v += __shfl_xor(v, 4);
-      v += __shfl_xor(v, 2);
-      v += __shfl_xor(v, 1);
-      dpart[r] = v;
-    }
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dsum[g * kBM + row0 + r] = dpart[r];
-    }
-  }
   __syncthreads();
   if (tid < kBM && b0 + tid < p.batch) {
-    float deepv = ((dsum[tid] + dsum[kBM + tid]) + dsum[2 * kBM + tid]) + dsum[3 * kBM + tid];
-    if (tail) deepv += tailr[4 * 64 * 4 + tid];
+    float deepv = dsum[tid];
+#pragma unroll
+    for (int w = 1; w < NG; ++w) deepv += dsum[w * kBM + tid];
+    if (tail) deepv += tailr[NG * 64 * 4 + tid];
     p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
   stamp(p.stamps, 8, tid);
+  stamp_end_rt(p.stamps, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -619,15 +684,15 @@ __global__ void __launch_bounds__(256) pack_dense_kernel(const PackList L) {
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <int D, int TPW, int KS, bool TRAIN>
+template <int D, int TPW, int KS, bool TRAIN, int PART = 0, int NG = 4>
 static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, hipStream_t s) {
-  auto k = fwd_kernel<D, TPW, KS, TRAIN>;
+  auto k = fwd_kernel<D, TPW, KS, TRAIN, PART, NG>;
   {
     hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
     if (e != hipSuccess) return e;
   }
   const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256 * KS), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NG * KS), lds, s, a);
   return hipGetLastError();
 }
 
@@ -646,21 +711,70 @@ static hipError_t launch_fwd_k(const FwdArgs& a, int tpw, size_t lds, hipStream_
   }
 }
 
+// eight tile groups (inference): at most 32 output tiles, so at most 4 per wave
+template <int D, int PART>
+static hipError_t launch_fwd_8(const FwdArgs& a, int tpw, size_t lds, hipStream_t s) {
+  switch (tpw) {
+    case 1: return launch_fwd_t<D, 1, 1, false, PART, 8>(a, lds, s);
+    case 2: return launch_fwd_t<D, 2, 1, false, PART, 8>(a, lds, s);
+    case 3: return launch_fwd_t<D, 3, 1, false, PART, 8>(a, lds, s);
+    case 4: return launch_fwd_t<D, 4, 1, false, PART, 8>(a, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <int D>
-static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, size_t lds, hipStream_t s) {
+static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
   if (a.flags & kTrain) return launch_fwd_k<D, 1, true>(a, tpw, lds, s);
+  if (ng == 8) return launch_fwd_8<D, 0>(a, tpw, lds, s);
   return ks == 2 ? launch_fwd_k<D, 2, false>(a, tpw, lds, s) : launch_fwd_k<D, 1, false>(a, tpw, lds, s);
+}
+
+// the split forward: gather launch (PART 1; no MLP, so one instantiation per D) then MLP launch
+// (PART 2) on the same stream
+template <int D, int TPW>
+static hipError_t launch_mlp4(const FwdArgs& a, size_t lds2, hipStream_t s) {
+  return launch_fwd_t<D, TPW, 1, false, 2, 4>(a, lds2, s);
+}
+
+template <int D>
+static hipError_t launch_split_d(const FwdArgs& a, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s) {
+  hipError_t e = launch_fwd_t<D, 1, 1, false, 1, 4>(a, lds1, s);
+  if (e != hipSuccess) return e;
+  if (ng == 8) return launch_fwd_8<D, 2>(a, tpw, lds2, s);
+  switch (tpw) {
+    case 1: return launch_mlp4<D, 1>(a, lds2, s);
+    case 2: return launch_mlp4<D, 2>(a, lds2, s);
+    case 3: return launch_mlp4<D, 3>(a, lds2, s);
+    case 4: return launch_mlp4<D, 4>(a, lds2, s);
+    case 5: return launch_mlp4<D, 5>(a, lds2, s);
+    case 6: return launch_mlp4<D, 6>(a, lds2, s);
+    case 7: return launch_mlp4<D, 7>(a, lds2, s);
+    case 8: return launch_mlp4<D, 8>(a, lds2, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s) {
+  switch (D) {
+    case 4: return launch_split_d<4>(a, tpw, ng, lds1, lds2, s);
+    case 8: return launch_split_d<8>(a, tpw, ng, lds1, lds2, s);
+    case 10: return launch_split_d<10>(a, tpw, ng, lds1, lds2, s);
+    case 16: return launch_split_d<16>(a, tpw, ng, lds1, lds2, s);
+    case 32: return launch_split_d<32>(a, tpw, ng, lds1, lds2, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 bool supported_embedding_size(int D) { return D == 4 || D == 8 || D == 10 || D == 16 || D == 32; }
 
-hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, size_t lds, hipStream_t s) {
+hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
   switch (D) {
-    case 4: return launch_fwd_d<4>(a, tpw, ks, lds, s);
-    case 8: return launch_fwd_d<8>(a, tpw, ks, lds, s);
-    case 10: return launch_fwd_d<10>(a, tpw, ks, lds, s);
-    case 16: return launch_fwd_d<16>(a, tpw, ks, lds, s);
-    case 32: return launch_fwd_d<32>(a, tpw, ks, lds, s);
+    case 4: return launch_fwd_d<4>(a, tpw, ks, ng, lds, s);
+    case 8: return launch_fwd_d<8>(a, tpw, ks, ng, lds, s);
+    case 10: return launch_fwd_d<10>(a, tpw, ks, ng, lds, s);
+    case 16: return launch_fwd_d<16>(a, tpw, ks, ng, lds, s);
+    case 32: return launch_fwd_d<32>(a, tpw, ks, ng, lds, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -109,11 +109,25 @@ class ForwardEngine:
             out = torch.empty(B, dtype=torch.float32, device=self.device)
         xs = xi.stride(0) if ncat > 0 else 0
         vs = xv.stride(0) if num > 0 else 0
-        rc = _lib.lib().dfwfm_forward(self.handle, ctypes.c_void_p(xi.data_ptr()), xs,
-                                      ctypes.c_void_p(xv.data_ptr()), vs, B,
-                                      ctypes.c_void_p(out.data_ptr()), _stream_handle(self.device))
+        ws_bytes = self._ws_bytes(B)
+        # split forward (gather launch + MLP launch): its workspace comes from torch's stream-ordered
+        # caching allocator, so batches in flight on several streams never share one
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device) if ws_bytes else None
+        rc = _lib.lib().dfwfm_forward_ws(self.handle, ctypes.c_void_p(xi.data_ptr()), xs,
+                                         ctypes.c_void_p(xv.data_ptr()), vs, B,
+                                         ctypes.c_void_p(out.data_ptr()), _ptr(ws), ws_bytes,
+                                         _stream_handle(self.device))
         _lib.check(rc, "dfwfm_forward")
         return out
+
+    def _ws_bytes(self, B: int) -> int:
+        cache = self.__dict__.setdefault("_ws_cache", {})
+        if B not in cache:
+            n = ctypes.c_size_t(0)
+            _lib.check(_lib.lib().dfwfm_forward_workspace_bytes(self.handle, B, ctypes.byref(n)),
+                       "dfwfm_forward_workspace_bytes")
+            cache[B] = int(n.value)
+        return cache[B]
 
     # -- training step -------------------------------------------------------
     def train_forward(self, xi, xv, out, dropout_p: float, seed: int) -> int:
