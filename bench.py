@@ -39,8 +39,8 @@ PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md, HBM3E spec peak
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=20, help="forwards captured per hipGraph")
@@ -50,8 +50,6 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
                          "batch's workgroup shares each CU, hiding the gather / FwFM phases)")
-    ap.add_argument("--stagger-cycles", type=int, default=0,
-                    help="start stream k after a k x this many cycle spin (offsets the streams' phases)")
     return ap.parse_args()
 
 
@@ -152,15 +150,21 @@ def main():
                 graphs.append(gk)
 
         def run_n(n):
-            for k in range(S):
-                with torch.cuda.stream(streams[k]):
-                    if graphs is None:
-                        for i in range(n):
+            # enqueue round-robin over the streams (stream k's replays must not wait behind the host
+            # enqueueing all of stream 0's first: the streams would start one after the other)
+            if graphs is None:
+                for i in range(n):
+                    for k in range(S):
+                        with torch.cuda.stream(streams[k]):
                             step(i, k)
-                        continue
-                    for _ in range(n // G):
+                return
+            for _ in range(n // G):
+                for k in range(S):
+                    with torch.cuda.stream(streams[k]):
                         graphs[k][G].replay()
-                    if n % G:
+            if n % G:
+                for k in range(S):
+                    with torch.cuda.stream(streams[k]):
                         graphs[k][n % G].replay()
 
         run_n(a.warmup)
@@ -179,9 +183,6 @@ def main():
             if k:
                 st.wait_stream(streams[0])
             s0[k].record(st)
-            if k and a.stagger_cycles:
-                with torch.cuda.stream(st):
-                    torch.cuda._sleep(k * a.stagger_cycles)
         run_n(a.steps)
         for k, st in enumerate(streams):
             s1[k].record(st)
