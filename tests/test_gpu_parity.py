@@ -244,3 +244,32 @@ def test_split_forward_is_bit_identical_to_fused(gpu, name, B, monkeypatch):
         assert rc == -1
     torch.cuda.synchronize()
     assert torch.equal(split.cpu(), fused.cpu())
+
+
+def _sweep_case(F, num, D, N, H, fwlw, seed):
+    """A synthetic DeepFwFM config (small tables) and its params / inputs, for shape sweeps."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = [1] * num + [int(x) for x in 50 + (np.arange(F - num) * 37) % 400]
+    cfg = dict(field_size=F, feature_sizes=sizes, embedding_size=D, use_fwfm=1, use_fm=0, use_logit=0,
+               use_deep=1, use_lw=1, use_fwlw=int(fwlw), h_depth=H, deep_nodes=N, numerical=num,
+               embedding_bag=0, qr_flag=0, qr_operation="mult", qr_collisions=4, qr_threshold=200)
+    m = DeepFMs(**model_kwargs(cfg))
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    params = synth.synth_state(shapes, F, D, N, True, True, seed=seed)
+    xi, xv = synth.synth_inputs(sizes, num, 48, seed=seed)
+    return cfg, params, xi, xv
+
+
+# deep_nodes covers the eight-wave kernel with the split 25th tile (400: 3 + tail; 144: 1 + tail),
+# without it (256: 2 per wave; 512: 4; 96: 6 tiles; 340: 22 ragged), and the four-wave fallback (D = 32:
+# 78 layer-1 chunks)
+@pytest.mark.parametrize("ng", ["8", "4"])
+@pytest.mark.parametrize("D,N,H,fwlw", [(10, 400, 3, 0), (10, 144, 2, 1), (4, 256, 1, 0), (16, 512, 2, 0),
+                                        (8, 96, 3, 1), (32, 400, 1, 0), (10, 340, 2, 0)])
+def test_forward_shape_sweep_matches_oracle(gpu, monkeypatch, ng, D, N, H, fwlw):
+    monkeypatch.setenv("DFWFM_NG", ng)
+    cfg, params, xi, xv = _sweep_case(39, 13, D, N, H, fwlw, seed=D * 1000 + N + H)
+    m = make_model(cfg, params, gpu)
+    got = run(m, xi, xv, gpu)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close(got, ref) < 1e-5

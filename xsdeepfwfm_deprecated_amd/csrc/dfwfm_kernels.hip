@@ -425,7 +425,9 @@ fwd_kernel(FwdArgs p) {
       const float x = fo[b * Fp + f];
       first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
     }
-    if ((flags & kHasSecond) && q < D) second = part2[b * D + q];
+    if (flags & kHasSecond) {
+      for (int d = q; d < D; d += 16) second += part2[b * D + d];  // D = 32: two terms per lane
+    }
 #pragma unroll
     for (int o = 8; o >= 1; o >>= 1) {
       first += __shfl_xor(first, o);
