@@ -354,3 +354,31 @@ def test_data_parallel_fit_two_ranks(gpu):
     num = sum(float(np.abs(w0[k] - w_single[k]).sum()) for k in w0)
     den = sum(float(np.abs(w_single[k]).sum()) for k in w0)
     assert num / den < 1e-2, num / den
+
+
+@pytest.mark.parametrize("D,N,H,fwlw", [(4, 256, 1, 0), (16, 512, 2, 0), (8, 96, 3, 1), (10, 144, 2, 1),
+                                        (16, 340, 1, 1)])
+def test_train_step_shape_sweep_matches_oracle(gpu, D, N, H, fwlw):
+    """Gradients of one HIP step vs the training oracle over embedding sizes and MLP shapes."""
+    from test_gpu_parity import _sweep_case
+    cfg, params, xi, xv = _sweep_case(39, 13, D, N, H, fwlw, seed=7 * D + N + H)
+    y = (np.arange(len(xi)) % 3 == 0).astype(np.float32)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    out, loss, grads, newp = hip_step(m, xi, xv, y, gpu, 1e-3, 3e-7)
+    o_out, o_loss, og, onew = torch_port.train_step(cfg, params, xi, xv, y, 1e-3, 3e-7)
+    assert logit_close(out, o_out) < 1e-5
+    assert abs(loss - o_loss) <= 1e-5 * max(1.0, abs(o_loss))
+    for k in og:
+        sc = np.abs(og[k]).max()
+        assert np.abs(grads[k] - og[k]).max() <= G_TOL * sc + 1e-12, k
+
+
+def test_train_step_unsupported_shape_raises(gpu):
+    """D = 32 with a 400-wide MLP needs more than 160 KiB of backward LDS: refused loudly, never run."""
+    from test_gpu_parity import _sweep_case
+    from xsdeepfwfm_deprecated_amd._lib import DfwfmError
+    cfg, params, xi, xv = _sweep_case(39, 13, 32, 400, 1, 0, seed=5)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    y = np.zeros(len(xi), np.float32)
+    with pytest.raises(DfwfmError, match="unsupported"):
+        hip_step(m, xi, xv, y, gpu, 1e-3, 0.0)
