@@ -273,3 +273,27 @@ def test_forward_shape_sweep_matches_oracle(gpu, monkeypatch, ng, D, N, H, fwlw)
     got = run(m, xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
     assert logit_close(got, ref) < 1e-5
+
+
+@pytest.mark.parametrize("inputs", ["uniform", "zipf"])
+def test_full_size_criteo_batch_matches_oracle(gpu, inputs):
+    """The bench workload at full size (Criteo-39 tables, 1.33 M rows; B = 4096): a sample of rows vs the
+    float64 oracle, and every sampled row bit-identical when run alone (no dependence on batch-mates)."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = synth.CRITEO_FEATURE_SIZES
+    cfg = dict(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0,
+               use_deep=1, use_lw=1, use_fwlw=0, h_depth=3, deep_nodes=400, numerical=13, embedding_bag=0,
+               qr_flag=0, qr_operation="mult", qr_collisions=4, qr_threshold=200)
+    m = DeepFMs(**model_kwargs(cfg))
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=1234)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    m = m.to(gpu).eval()
+    gen = synth.zipf_inputs if inputs == "zipf" else synth.synth_inputs
+    xi, xv = gen(sizes, 13, 4096, seed=11)
+    full = run(m, xi, xv, gpu)
+    rows = np.random.default_rng(0).choice(4096, 96, replace=False)
+    ref = dfwfm_oracle.forward(cfg, params, xi[rows], xv[rows])
+    assert logit_close(full[rows], ref) < 1e-5
+    alone = run(m, xi[rows], xv[rows], gpu)
+    assert np.array_equal(alone, full[rows])

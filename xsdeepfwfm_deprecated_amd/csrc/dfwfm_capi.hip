@@ -679,6 +679,7 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
     };
     auto add = [&](float* gt, const float* other, int64_t c, int f, int kind, int src, int64_t rows) -> int {
       if (!gt || rows <= 0) return DFWFM_OK;
+      if (rows > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: table of more than 2^31 rows", f);
       const int w = src == 0 ? D : 1;
       const bool is_priv = rows * (w + 1) <= kPrivFloats;
       ScatterArgs& L = is_priv ? priv : atom;
