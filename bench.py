@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
+    ap.add_argument("--config", choices=["deepfwfm", "qr", "pruned"], default="deepfwfm",
+                    help="BASELINE.json configs[1] (default), [2] QR embeddings (embedding_bag=1 qr_flag=1, c=4, "
+                         "threshold 200, mult), [3] pruned (sparse 0.90, emb_r 0.444, prune_r 1: the reference's "
+                         "magnitude masks applied on the device)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=20, help="forwards captured per hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -63,7 +67,7 @@ def kernel_name():
     return f"dfwfm::fwd_kernel<10,{tpw},1,false,0,{ng}>"
 
 
-def algorithmic_counts(cfg):
+def algorithmic_counts(cfg, sizes=None):
     """Per-sample algorithmic FLOPs and HBM bytes of the fused forward."""
     F, D, N, H, num = 39, 10, 400, 3, 13
     ncat = F - num
@@ -74,6 +78,9 @@ def algorithmic_counts(cfg):
     bytes_ = ncat * 8 + num * 4 + ncat * D * 4 + 4     # Xi + Xv + gathered rows + logit
     if not cfg["use_fwlw"]:
         bytes_ += ncat * 4                             # first-order table rows
+    if cfg.get("qr_flag") and sizes is not None:       # QR fields read a remainder row too
+        nqr = sum(1 for n in sizes[num:] if n > cfg["qr_threshold"])
+        bytes_ += nqr * (D * 4 + (0 if cfg["use_fwlw"] else 4))
     return flops, bytes_
 
 
@@ -93,15 +100,24 @@ def main():
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
     sizes = synth.CRITEO_FEATURE_SIZES
     fwlw = a.first_order == "fwlw"
+    qr = a.config == "qr"
     cfg = dict(field_size=39, numerical=13, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0, use_deep=1,
-               use_lw=1, use_fwlw=int(fwlw), h_depth=3, deep_nodes=400)
+               use_lw=1, use_fwlw=int(fwlw), h_depth=3, deep_nodes=400, embedding_bag=int(qr), qr_flag=int(qr),
+               qr_operation="mult", qr_collisions=4, qr_threshold=200)
     model = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1,
-                    use_lw=1, use_fwlw=fwlw, numerical=13, use_cuda=True)
+                    use_lw=1, use_fwlw=fwlw, numerical=13, embedding_bag=int(qr), qr_flag=int(qr),
+                    qr_operation="mult", qr_collisions=4, qr_threshold=200, use_cuda=True)
     shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
     params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=1234)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     model = model.to(dev).eval()
     model.strict_index_check = False
+    if a.config == "pruned":
+        # reference :647-673 with sparse=0.90, emb_r=0.444, prune_r=1 (main_all.py flags of config 4)
+        from xsdeepfwfm_deprecated_amd.training import prune_step
+        prune_step(model, 0.90, 1, 1, 1, 0.444, 1.0)
+        torch.cuda.synchronize(dev)
+        params = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
 
     n_bufs = 4  # distinct resident batches, rotated, so gathers are not L2-hot repeats
     batches = []
@@ -203,7 +219,7 @@ def main():
 
     ms_per_step = ms / (a.steps * S)
     value = world * S * BATCH * a.steps / (ms / 1e3)
-    flops, bytes_ = algorithmic_counts(cfg)
+    flops, bytes_ = algorithmic_counts(cfg, sizes)
     # achieved = algorithmic FLOP of one launch / its duration, times the launches in flight (each of
     # the S concurrent launches takes ~S x the per-batch time): the aggregate rate over the timed region
     achieved_tf = flops * BATCH * S / (launch_ms / 1e3) / 1e12
@@ -222,8 +238,10 @@ def main():
         "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic Criteo-39 ({a.inputs} indices over the real field sizes, Xv integers 0..63; "
                 "deterministic hash-init weights with the reference's init_weights scales)",
-        "config": {"workload": f"DeepFwFM forward, Criteo-39, emb 10, MLP 3x400, FwFM + {a.first_order}; "
-                               f"batch {BATCH} per GPU",
+        "config": {"workload": f"DeepFwFM forward, Criteo-39, emb 10, MLP 3x400, FwFM + {a.first_order}"
+                               + {"deepfwfm": "", "qr": ", QR embeddings (c=4, mult, threshold 200)",
+                                  "pruned": ", pruned (sparse 0.90, emb_r 0.444, prune_r 1)"}[a.config]
+                               + f"; batch {BATCH} per GPU",
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
                    "launch": ("eager" if a.no_graph else f"hipGraph replay, {min(a.graph_steps, a.steps)} forwards per graph")
