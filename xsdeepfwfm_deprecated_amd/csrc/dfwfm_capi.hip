@@ -557,7 +557,9 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   a.seed = seed;
   a.seed_src = m->step_src;
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
-  hipError_t e = launch_forward(a, m->D, m->TPWF > 0 ? m->TPWF : 1, 1, 4, m->lds_bytes, (hipStream_t)stream);
+  // the eight-wave layout when the model has it (DFWFM_NG=4 keeps the four-wave kernel)
+  a.tail = m->tailI;
+  hipError_t e = launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, 1, m->NG, m->lds_inf, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
   m->trained = true;
   return DFWFM_OK;

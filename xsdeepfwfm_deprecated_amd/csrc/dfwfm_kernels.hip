@@ -47,12 +47,12 @@ namespace dfwfm {
 // forward: two launches per batch, see launch_forward_split)
 // NG: MLP output-tile groups = waves (4: one wave per SIMD, <= 256 registers; 8: two per SIMD, <= 128
 // registers, so one workgroup issues MFMAs from two waves per SIMD while a second batch's workgroup
-// on the same CU runs its gather)
+// on the same CU runs its gather; the training variant, one batch in flight, keeps 256 registers)
 template <int D, int TPW, int KS, bool TRAIN, int PART, int NG>
 __global__ void __launch_bounds__(64 * NG * KS)
-__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (NG == 8 ? 4 : DFWFM_FWD_WPE))))
+__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE))))
 fwd_kernel(FwdArgs p) {
-  static_assert(NG == 4 || (NG == 8 && KS == 1 && !TRAIN), "8 tile groups: inference, no K split");
+  static_assert(NG == 4 || (NG == 8 && KS == 1), "8 tile groups: no K split");
   constexpr int NTH = 64 * NG * KS;
   constexpr int NW = NG * KS;
   constexpr int RPT = (kBM * 64 + NTH - 1) / NTH;  // gather rows per thread (F <= 64)
@@ -714,20 +714,20 @@ static hipError_t launch_fwd_k(const FwdArgs& a, int tpw, size_t lds, hipStream_
 }
 
 // eight tile groups (inference): at most 32 output tiles, so at most 4 per wave
-template <int D, int PART>
+template <int D, int PART, bool TRAIN = false>
 static hipError_t launch_fwd_8(const FwdArgs& a, int tpw, size_t lds, hipStream_t s) {
   switch (tpw) {
-    case 1: return launch_fwd_t<D, 1, 1, false, PART, 8>(a, lds, s);
-    case 2: return launch_fwd_t<D, 2, 1, false, PART, 8>(a, lds, s);
-    case 3: return launch_fwd_t<D, 3, 1, false, PART, 8>(a, lds, s);
-    case 4: return launch_fwd_t<D, 4, 1, false, PART, 8>(a, lds, s);
+    case 1: return launch_fwd_t<D, 1, 1, TRAIN, PART, 8>(a, lds, s);
+    case 2: return launch_fwd_t<D, 2, 1, TRAIN, PART, 8>(a, lds, s);
+    case 3: return launch_fwd_t<D, 3, 1, TRAIN, PART, 8>(a, lds, s);
+    case 4: return launch_fwd_t<D, 4, 1, TRAIN, PART, 8>(a, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 template <int D>
 static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
-  if (a.flags & kTrain) return launch_fwd_k<D, 1, true>(a, tpw, lds, s);
+  if (a.flags & kTrain) return ng == 8 ? launch_fwd_8<D, 0, true>(a, tpw, lds, s) : launch_fwd_k<D, 1, true>(a, tpw, lds, s);
   if (ng == 8) return launch_fwd_8<D, 0>(a, tpw, lds, s);
   return ks == 2 ? launch_fwd_k<D, 2, false>(a, tpw, lds, s) : launch_fwd_k<D, 1, false>(a, tpw, lds, s);
 }
