@@ -276,6 +276,37 @@ __device__ __forceinline__ void store_tile(float* __restrict__ g, int64_t gstrid
   }
 }
 
+// Copy rows [0, nrows) x 4*cols4 floats of a global tile (row stride gstride floats) into an LDS tile
+// (row stride lds_stride), zero-filling rows [nrows, kBM) and columns [4*cols4, 4*pad4): KPT float4 per
+// thread in flight, every load issued before any LDS store (a load-then-store loop waits out one
+// round trip per iteration).  16-byte aligned bases and strides.
+template <int KPT>
+__device__ __forceinline__ void load_tile(float* __restrict__ lds, int lds_stride, const float* __restrict__ g,
+                                          int64_t gstride, int nrows, int cols4, int pad4, int tid, int nth) {
+  const int n = kBM * pad4;
+  f32x4 v[KPT];
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = tid + k * nth;
+    const int b = i / pad4;
+    const int c = i - b * pad4;
+    v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (i < n && b < nrows && c < cols4) v[k] = reinterpret_cast<const f32x4*>(g + b * gstride)[c];
+  }
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = tid + k * nth;
+    const int b = i / pad4;
+    if (i < n) reinterpret_cast<f32x4*>(lds + b * lds_stride)[i - b * pad4] = v[k];
+  }
+  for (int i = tid + KPT * nth; i < n; i += nth) {  // wider tiles
+    const int b = i / pad4;
+    const int c = i - b * pad4;
+    reinterpret_cast<f32x4*>(lds + b * lds_stride)[c] =
+        (b < nrows && c < cols4) ? reinterpret_cast<const f32x4*>(g + b * gstride)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 // Dropout seed of a step: the host's seed, or -- for graph-replayed steps -- that seed mixed with a
 // device step counter (read at kernel time, so every replay draws fresh masks).
 __device__ __forceinline__ uint32_t step_seed(uint32_t base, const int64_t* src) {

@@ -23,7 +23,7 @@
 namespace dfwfm {
 
 struct BwdLds {
-  int lw, fwlw, rsk, bufE, bufD, bufA, dl, total;
+  int lw, fwlw, rsk, bufE, bufD, bufA, dl, fc, total;
 };
 
 __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX, int SY) {
@@ -36,6 +36,7 @@ __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX
   L.bufD = o;  o += kBM * SX;                   // dE tile
   L.bufA = o;  o += kBM * SY;                   // G buffer
   L.dl = o;    o += kBM;
+  L.fc = o;    o += SY;                       // net_1_fc (G_H = dlogit * fc * mask)
   L.total = r4(o);
   return L;
 }
@@ -68,8 +69,10 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
   float* bufA = smem + L.bufA;
   float* bufB = bufE;  // the E tile is dead once the shallow dE is formed
   float* dl = smem + L.dl;
+  float* fc_s = smem + L.fc;
   const int64_t b0 = (int64_t)blockIdx.x * kBM;
   const int row0 = (lane >> 4) * 4;
+  const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
 
   // ---- P0: stage --------------------------------------------------------------
   stamp(p.stamps, 0, tid);
@@ -82,12 +85,13 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
     for (int i = tid; i < p.MT * p.S * 16; i += NTH)
       reinterpret_cast<float4*>(rsk)[i] = reinterpret_cast<const float4*>(p.rsk)[i];
   if (tid < kBM) dl[tid] = (b0 + tid < p.batch) ? p.dlogit[b0 + tid] : 0.f;
-  for (int i = tid; i < kBM * p.W0; i += NTH) {
-    const int b = i / p.W0;
-    const int c = i - b * p.W0;
-    const int64_t row = b0 + b;
-    bufE[b * SX + c] = (second && c < FD && row < p.batch) ? p.sv_e[row * r4(FD) + c] : 0.f;
-    bufD[b * SX + c] = 0.f;
+  if (deep)
+    for (int i = tid; i < p.NT * 16; i += NTH) fc_s[i] = p.fc[i];
+  // the E tile: rows of r4(F*D) floats (zero past F*D), zero-padded to W0 columns
+  load_tile<7>(bufE, SX, p.sv_e + b0 * r4(FD), r4(FD), second ? nrows : 0, r4(FD) / 4, p.W0 / 4, tid, NTH);
+  for (int i = tid; i < kBM * (p.W0 / 4); i += NTH) {
+    const int b = i / (p.W0 / 4);
+    reinterpret_cast<f32x4*>(bufD + b * SX)[i - b * (p.W0 / 4)] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
   stamp(p.stamps, 1, tid);
@@ -132,16 +136,15 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
     const int H = p.H, N = p.N, NT = p.NT, NP = NT * 16;
     const float scale = drop ? p.drop_scale : 1.f;
     const uint32_t dseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
-    // G_H = dlogit * fc * (X_H > 0) * scale -> bufA and global
+    // G_H = dlogit * fc * (X_H > 0) * scale -> bufA (X_H staged there first; stored to the workspace
+    // at the top of layer H, behind its weight preload)
+    load_tile<7>(bufA, SY, p.sv_x[H] + b0 * N, N, nrows, N / 4, NP / 4, tid, NTH);
+    __syncthreads();
     for (int i = tid; i < kBM * NP; i += NTH) {
       const int b = i / NP;
       const int n = i - b * NP;
-      const int64_t row = b0 + b;
-      const bool ok = n < N && row < p.batch;
-      const float x = ok ? p.sv_x[H][row * N + n] : 0.f;
-      const float gv = (ok && x > 0.f) ? dl[b] * p.fc[n] * scale : 0.f;
-      bufA[b * SY + n] = gv;
-      if (ok) p.sv_g[H][row * N + n] = gv;
+      const float x = bufA[b * SY + n];
+      bufA[b * SY + n] = (n < N && x > 0.f) ? dl[b] * fc_s[n] * scale : 0.f;
     }
     __syncthreads();
     stamp(p.stamps, 3, tid);
@@ -161,6 +164,9 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
       for (int t0 = 0; t0 < KT; t0 += 4 * TPW) {
         ls.init(wrsrc, p.wt_off[l] + t0 * NT * 64, NT, KT - t0, wave, 0);
         ls.preload(wb0, wb1, lane * 16);
+        // G_l (this layer's input tile) -> workspace for the weight-gradient GEMM: coalesced rows
+        // from LDS, behind the preload (stores count in vmcnt too)
+        if (t0 == 0 && !(flags & (1 << 10))) store_tile(p.sv_g[l] + b0 * N, N, in, SY, nrows, N / 4, tid, NTH);
         // epilogue operands: the ReLU/dropout mask source X_{l-1} for this lane's outputs
         float xm[TPW][4];
 #pragma unroll
@@ -170,7 +176,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int64_t row = b0 + row0 + r;
-            xm[j][r] = (l > 1 && t < KT && k < K && row < p.batch) ? p.sv_x[l - 1][row * N + k] : 0.f;
+            xm[j][r] = (l > 1 && t < KT && k < K && row < p.batch) ? ((flags & (1 << 11)) ? 1.f : p.sv_x[l - 1][row * N + k]) : 0.f;
           }
         }
         f32x4 acc[TPW];
@@ -185,9 +191,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
             const int b = row0 + r;
             const int64_t row = b0 + b;
             if (l > 1) {
-              const float gv = (k < K && xm[j][r] > 0.f) ? acc[j][r] * scale : 0.f;
-              outg[b * SY + k] = gv;
-              if (k < K && row < p.batch) p.sv_g[l - 1][row * N + k] = gv;
+              outg[b * SY + k] = (k < K && xm[j][r] > 0.f) ? acc[j][r] * scale : 0.f;
             } else if (k < FD) {
               float gv = acc[j][r];
               if (drop) gv = dropout_keep(dseed, 0, row, k, p.drop_p) ? gv * scale : 0.f;
