@@ -10,7 +10,7 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
-template <int TPW, int MT, int NW = 4, bool LD = true, bool AL = true, int NS = 3, bool REAL = false>
+template <int TPW, int MT, int NW = 4, bool LD = true, bool AL = true, int NS = 3, bool REAL = false, int IL = 0>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 16 ? 8 : NW / 2)))
 kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out) {
   __shared__ f32x4 actl[MT][32 * 64];
@@ -62,12 +62,33 @@ kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out) {
     _Pragma("unroll") for (int m = 0; m < MT; ++m)                                   \
     _Pragma("unroll") for (int j = 0; j < TPW; ++j)                                  \
       acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(AX[m][s], X[j][s], acc[m][j], 0, 0, 0); \
-    __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);                              \
-    for (int q = 0; q < TPW; ++q) {                                                  \
+    if constexpr (IL == 0) {                                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);                            \
+      for (int q = 0; q < TPW; ++q) {                                                \
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT, 0);                      \
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                           \
+      }                                                                              \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT * TPW, 0);                  \
+    } else if constexpr (IL == 1) {                                                  \
+      __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);                            \
+      for (int q = 0; q < TPW; ++q) {                                                \
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * MT, 0);                      \
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                           \
+      }                                                                              \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT * TPW, 0);                  \
+    } else if constexpr (IL == 2) {                                                  \
+      __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);                            \
+      __builtin_amdgcn_sched_group_barrier(0x020, TPW, 0);                           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * MT * TPW, 0);                  \
+    } else {                                                                         \
       __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT, 0);                        \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                             \
+      __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);                            \
+      for (int q = 0; q < TPW; ++q) {                                                \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1 * MT, 0);                      \
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                           \
+      }                                                                              \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT * TPW, 0);                  \
     }                                                                                \
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT * TPW, 0);                    \
     __builtin_amdgcn_sched_barrier(0);                                               \
   }
     int i = 0;
@@ -114,18 +135,18 @@ kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out) {
   if (s == 12345.678f) out[threadIdx.x] = s;
 }
 
-template <int TPW, int MT, int NW = 4, bool LD = true, bool AL = true, int NS = 3, bool REAL = false>
+template <int TPW, int MT, int NW = 4, bool LD = true, bool AL = true, int NS = 3, bool REAL = false, int IL = 0>
 void run(const char* name, const f32x4* w, int grid, float* out, hipStream_t* st, int nst) {
   const int NT_ = NW * TPW, NC = 25, layers = 3;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL>), dim3(grid), dim3(64 * NW), 0, st[0], w, NT_, NC, layers, out);
+  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL, IL>), dim3(grid), dim3(64 * NW), 0, st[0], w, NT_, NC, layers, out);
   CHECK(hipDeviceSynchronize());
   const int reps = 100;
   CHECK(hipEventRecord(e0, 0));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL>), dim3(grid), dim3(64 * NW), 0, st[r % nst], w, NT_, NC, layers, out);
+    hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL, IL>), dim3(grid), dim3(64 * NW), 0, st[r % nst], w, NT_, NC, layers, out);
   for (int k = 0; k < nst; ++k) {
     hipEvent_t ev;
     CHECK(hipEventCreate(&ev));
@@ -155,10 +176,10 @@ int main() {
   CHECK(hipMemcpy(w, h, n * sizeof(f32x4), hipMemcpyHostToDevice));
   hipStream_t st[4];
   for (int k = 0; k < 4; ++k) CHECK(hipStreamCreate(&st[k]));
-  run<6, 1>("TPW=6 4 waves", w, 256, out, st, 1);
-  run<6, 1, 4, true, true, 3, true>("TPW=6 4 waves, real act layout+epilogue", w, 256, out, st, 1);
-  run<3, 1, 8>("TPW=3 8 waves", w, 256, out, st, 1);
-  run<3, 1, 8, true, true, 3, true>("TPW=3 8 waves, real act layout+epilogue", w, 256, out, st, 1);
-  run<3, 1, 8, true, true, 3, true>("TPW=3 8 waves, real act layout+epilogue", w, 512, out, st, 1);
+  run<3, 1, 8, true, true, 3, true, 0>("TPW=3 8w real, IL0 (forward today)", w, 256, out, st, 1);
+  run<3, 1, 8, true, true, 3, true, 1>("TPW=3 8w real, IL1 4 mfma : 1 load", w, 256, out, st, 1);
+  run<3, 1, 8, true, true, 3, true, 2>("TPW=3 8w real, IL2 loads first", w, 256, out, st, 1);
+  run<3, 1, 8, true, true, 3, true, 3>("TPW=3 8w real, IL3 1 mfma : 1 load", w, 256, out, st, 1);
+  run<3, 1, 8, true, true, 3, true, 0>("TPW=3 8w real, IL0 (forward today)", w, 256, out, st, 1);
   return 0;
 }
