@@ -116,3 +116,12 @@ def test_unsupported_variants_raise():
         DeepFMs(**kw, static_quantization=True)
     with pytest.raises(SystemExit):
         DeepFMs(**dict(kw, use_fm=1))  # fwfm and fm together
+
+
+def test_custom_op_is_registered_with_schema():
+    """torch.ops.dfwfm.forward: the forward surfaced as a PyTorch custom operator (torch_ops.py)."""
+    import torch
+    import xsdeepfwfm_deprecated_amd  # noqa: F401  -- registers the op
+    schema = str(torch.ops.dfwfm.forward.default._schema)
+    assert schema == ("dfwfm::forward(SymInt model_id, Tensor xi, Tensor xv, Tensor[] params, bool train, "
+                      "float dropout_p, SymInt seed) -> (Tensor, Tensor)")

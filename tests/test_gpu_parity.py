@@ -297,3 +297,22 @@ def test_full_size_criteo_batch_matches_oracle(gpu, inputs):
     assert logit_close(full[rows], ref) < 1e-5
     alone = run(m, xi[rows], xv[rows], gpu)
     assert np.array_equal(alone, full[rows])
+
+
+def test_custom_op_opcheck_and_matches_engine(gpu):
+    """torch.ops.dfwfm.forward passes torch.library.opcheck (schema, fake tensor, autograd
+    registration) and returns the engine's logits bit for bit."""
+    from xsdeepfwfm_deprecated_amd import torch_ops
+    cfg, params, xi, xv, *_ = load_golden("deepfwfm_lw")
+    m = make_model(cfg, params, gpu)
+    xi_t = torch.from_numpy(xi[:64]).to(gpu)
+    xv_t = torch.from_numpy(xv[:64]).to(gpu)
+    with torch.no_grad():
+        ref = m(xi_t, xv_t)  # syncs the engine
+    plist = [p for p in m.parameters() if p.requires_grad]
+    mid = torch_ops.register(m)
+    torch.library.opcheck(torch.ops.dfwfm.forward.default, (mid, xi_t, xv_t, plist, False, 0.0, 0),
+                          test_utils=("test_schema", "test_faketensor", "test_autograd_registration"))
+    with torch.no_grad():
+        out, tok = torch.ops.dfwfm.forward(mid, xi_t, xv_t, plist, False, 0.0, 0)
+    assert torch.equal(out.cpu(), ref.cpu())

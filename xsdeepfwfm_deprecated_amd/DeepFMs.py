@@ -286,7 +286,9 @@ class DeepFMs(nn.Module):
         if needs_grad:
             from .training import train_forward
             return train_forward(self, eng, xi, xv)
-        out = eng.forward(xi, xv)
+        from . import torch_ops  # torch.ops.dfwfm.forward (the registered custom op)
+        params = [q for q in self.parameters() if q.requires_grad]
+        out, _ = torch.ops.dfwfm.forward(torch_ops.register(self), xi, xv, params, False, 0.0, 0)
         if self.strict_index_check:
             self.check_index_errors()
         return out

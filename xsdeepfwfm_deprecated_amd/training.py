@@ -1,9 +1,9 @@
 """Training path of DeepFMs (reference model/DeepFMs.py:497-748, 807-823) on the HIP kernels.
 
-* ``train_forward``: an autograd Function whose forward is the fused HIP forward in training mode
-  (activations kept, deep-tower dropout from a counter hash) and whose backward is the fused HIP
-  backward (csrc/dfwfm_train.hip) writing every parameter's gradient -- dense, like the
-  reference's ``nn.Embedding(sparse=False)`` -- into one flat per-step buffer.
+* ``train_forward``: ``torch.ops.dfwfm.forward`` in training mode (torch_ops.py: the fused HIP
+  forward keeping its activations, deep-tower dropout from a counter hash) whose registered backward
+  is the fused HIP backward (csrc/dfwfm_train.hip) writing every parameter's gradient -- dense, like
+  the reference's ``nn.Embedding(sparse=False)`` -- into one flat per-step buffer.
 * ``Adam``: ``torch.optim.Adam`` (coupled L2, bias correction) as one HIP kernel per <= 40 tensors,
   same defaults and ``state_dict`` layout.
 * ``fit``: the reference's epoch loop -- init_weights, optimizer, BCE-with-logits (or the KD loss),
@@ -29,32 +29,6 @@ from . import engine as _engine
 
 
 # --------------------------------------------------------------------------------------- autograd
-class _TrainForward(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, model, eng, xi, xv, dropout_p, seed, *params):
-        out = torch.empty(xi.shape[0], dtype=torch.float32, device=eng.device)
-        ctx.token = eng.train_forward(xi, xv, out, dropout_p, seed)
-        ctx.model, ctx.eng = model, eng
-        ctx.inputs = (xi, xv)  # the backward kernel re-reads the indices
-        ctx.params = params
-        return out
-
-    @staticmethod
-    def backward(ctx, grad_out):
-        model, eng, params = ctx.model, ctx.eng, ctx.params
-        need = ctx.needs_input_grad[6:]
-        flat, views = _grad_buffer(params, need, eng.device)
-        by_id = {id(p): g for p, g in zip(params, views)}
-        fields, dense = model._param_layout()
-        fg = [tuple(None if t is None else by_id.get(id(t)) for t in tup) for tup in fields]
-        dg = {k: (None if v is None else by_id.get(id(v))) for k, v in dense.items() if not isinstance(v, list)}
-        dg["lin_w"] = [by_id.get(id(t)) for t in dense["lin_w"]]
-        dg["lin_b"] = [by_id.get(id(t)) for t in dense["lin_b"]]
-        eng.backward(ctx.token, grad_out.contiguous(), fg, dg)
-        model._grad_flat = flat
-        return (None,) * 6 + tuple(views)
-
-
 def _grad_buffer(params, need, device):
     """One zeroed flat buffer holding every needed gradient (a single memset and, under data
     parallelism, a single all-reduce); returns it and per-parameter views (None where not needed)."""
@@ -78,8 +52,10 @@ def train_forward(model, eng, xi, xv):
         if any(float(d) != p for d in model.dropout_deep):
             raise NotImplementedError("dfwfm: per-layer dropout rates must be equal")
     seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+    from . import torch_ops
     params = [q for q in model.parameters() if q.requires_grad]
-    return _TrainForward.apply(model, eng, xi, xv, p, seed, *params)
+    out, _ = torch.ops.dfwfm.forward(torch_ops.register(model), xi, xv, params, True, p, seed)
+    return out
 
 
 # --------------------------------------------------------------------------------------- Adam
