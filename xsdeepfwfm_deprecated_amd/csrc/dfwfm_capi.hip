@@ -616,7 +616,12 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
     int src = diag_stamps_buffer(m, batch, 2, &a.stamps);
     if (src != DFWFM_OK) return src;
     const size_t lds = backward_lds_bytes(F, D, m->MT, m->S, m->SX, m->SY);
-    e = launch_backward(a, D, m->TPW > 0 ? m->TPW : 1, lds, s);
+    // eight waves (the 8*TPW+1-th tile split by K, like the forward) unless DFWFM_NG=4
+    const char* ngs = getenv("DFWFM_NG");
+    const int NT = m->NT;
+    const bool ng8 = H > 0 && NT <= 32 && !(ngs && atoi(ngs) == 4);
+    const int tpw = ng8 ? (NT % 8 == 1 && NT >= 9 ? NT / 8 : (NT + 7) / 8) : (m->TPW > 0 ? m->TPW : 1);
+    e = launch_backward(a, D, tpw > 0 ? tpw : 1, ng8 ? 8 : 4, lds, s);
     if (e != hipSuccess) return hip_fail(e, "backward launch");
   }
 

@@ -281,7 +281,7 @@ bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s);
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
-hipError_t launch_backward(const BwdArgs& a, int D, int tpw, size_t lds, hipStream_t s);
+hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds, hipStream_t s);
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
 hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages

@@ -23,7 +23,7 @@
 namespace dfwfm {
 
 struct BwdLds {
-  int lw, fwlw, rsk, bufE, bufD, bufA, dl, fc, total;
+  int lw, fwlw, rsk, bufE, bufD, bufA, dl, fc, tailr, total;
 };
 
 __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX, int SY) {
@@ -37,6 +37,7 @@ __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX
   L.bufA = o;  o += kBM * SY;                   // G buffer
   L.dl = o;    o += kBM;
   L.fc = o;    o += SY;                       // net_1_fc (G_H = dlogit * fc * mask)
+  L.tailr = o; o += 8 * 64 * 4;               // split-tail partial products (eight waves)
   L.total = r4(o);
   return L;
 }
@@ -45,10 +46,14 @@ size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY) {
   return sizeof(float) * (size_t)bwd_layout(F, D, MT, S, SX, SY).total;
 }
 
-template <int D, int TPW>
-__global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
-  constexpr int NTH = 256;
-  constexpr int NW = 4;
+// NG: waves = output-tile groups of the MLP chain.  4: one wave per SIMD, TPW tiles each; 8: two
+// per SIMD (256 registers, one workgroup per CU) with the 8*TPW+1-th tile of a layer split by K over
+// the eight waves (tail), as in the forward.
+template <int D, int TPW, int NG>
+__global__ void __launch_bounds__(64 * NG) __attribute__((amdgpu_waves_per_eu(NG == 8 ? 2 : 1)))
+bwd_kernel(BwdArgs p) {
+  constexpr int NTH = 64 * NG;
+  constexpr int NW = NG;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -70,6 +75,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
   float* bufB = bufE;  // the E tile is dead once the shallow dE is formed
   float* dl = smem + L.dl;
   float* fc_s = smem + L.fc;
+  float* tailr = smem + L.tailr;
   const int64_t b0 = (int64_t)blockIdx.x * kBM;
   const int row0 = (lane >> 4) * 4;
   const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
@@ -151,19 +157,31 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
 
     const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float4*>(p.wtpack), (short)0, p.wtpack_bytes, 0x00020000);
-    LayerStream<TPW, 1> ls;
+    LayerStream<TPW, 1, NG> ls;
     f32x4 wb0[TPW], wb1[TPW], wb2[TPW];
+    TailStream<NG> ts;
+    f32x4 tw[TailStream<NG>::C];
+    const int g = wave;
     for (int l = H; l >= 1; --l) {
       const bool fromA = ((H - l) & 1) == 0;
       const float* in = fromA ? bufA : bufB;
       float* outg = fromA ? bufB : bufA;
       const int K = l == 1 ? FD : N;
       const int KT = l == 1 ? p.NC0 : NT;
-      // output tiles (the layer's inputs k) in passes of 4*TPW: layer 1 may have more tiles
+      // eight waves: the last tile of a layer with 8*TPW + 1 tiles is split by K over the waves
+      const bool ltail = NG == 8 && KT == NG * TPW + 1 && NT <= NG * TailStream<NG>::C;
+      const int KTm = ltail ? KT - 1 : KT;
+      const int T = KT - 1;  // the tail tile
+      float xt = 0.f;        // its ReLU mask source, row row0 + g
+      // output tiles (the layer's inputs k) in passes of NG*TPW: layer 1 may have more tiles
       // (ceil(F*D/16)) than the hidden width the kernel's TPW was sized for
-      for (int t0 = 0; t0 < KT; t0 += 4 * TPW) {
-        ls.init(wrsrc, p.wt_off[l] + t0 * NT * 64, NT, KT - t0, wave, 0);
+      for (int t0 = 0; t0 < KTm; t0 += NG * TPW) {
+        ls.init(wrsrc, p.wt_off[l] + t0 * NT * 64, NT, KTm - t0, g, 0);
         ls.preload(wb0, wb1, lane * 16);
+        if (ltail && t0 == 0) {
+          ts.init(p.wt_off[l], NT, T, g);
+          ts.load(wrsrc, tw, lane * 16);
+        }
         // G_l (this layer's input tile) -> workspace for the weight-gradient GEMM: coalesced rows
         // from LDS, behind the preload (stores count in vmcnt too)
         if (t0 == 0 && !(flags & (1 << 10))) store_tile(p.sv_g[l] + b0 * N, N, in, SY, nrows, N / 4, tid, NTH);
@@ -171,20 +189,27 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
         float xm[TPW][4];
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
-          const int t = t0 + wave + 4 * j;
+          const int t = t0 + g + NG * j;
           const int k = t * 16 + (lane & 15);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int64_t row = b0 + row0 + r;
-            xm[j][r] = (l > 1 && t < KT && k < K && row < p.batch) ? ((flags & (1 << 11)) ? 1.f : p.sv_x[l - 1][row * N + k]) : 0.f;
+            xm[j][r] = (l > 1 && t < KTm && k < K && row < p.batch) ? ((flags & (1 << 11)) ? 1.f : p.sv_x[l - 1][row * N + k]) : 0.f;
           }
         }
+        if (ltail && t0 == 0) {
+          const int k = T * 16 + (lane & 15);
+          const int64_t row = b0 + row0 + (g & 3);
+          xt = (l > 1 && g < 4 && k < K && row < p.batch) ? p.sv_x[l - 1][row * N + k] : 0.f;
+          // the tail's share first: its fragments are then dead during the K loop
+          reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.mma(in, SY, tw, lane);
+        }
         f32x4 acc[TPW];
-        mlp_k_loop<TPW, 1>(acc, in, SY, ls, wb0, wb1, wb2, lane);
+        mlp_k_loop<TPW, 1, NG>(acc, in, SY, ls, wb0, wb1, wb2, lane);
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
-          const int t = t0 + wave + 4 * j;
-          if (t >= KT) continue;  // wave-uniform
+          const int t = t0 + g + NG * j;
+          if (t >= KTm) continue;  // wave-uniform
           const int k = t * 16 + (lane & 15);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -201,6 +226,25 @@ __global__ void __launch_bounds__(256) bwd_kernel(BwdArgs p) {
         }
       }
       __syncthreads();
+      if (ltail) {
+        // wave g < 4 finishes row (lane>>4)*4 + g of the tail tile from the NG partial products
+        if (g < 4) {
+          const int k = T * 16 + (lane & 15);
+          const int b = row0 + g;
+          const float* tp = tailr + lane * 4 + g;
+          float sum = tp[0];
+#pragma unroll
+          for (int w = 1; w < NG; ++w) sum += tp[w * 256];
+          if (l > 1) {
+            outg[b * SY + k] = (k < K && xt > 0.f) ? sum * scale : 0.f;
+          } else if (k < FD) {
+            float gv = sum;
+            if (drop) gv = dropout_keep(dseed, 0, b0 + b, k, p.drop_p) ? gv * scale : 0.f;
+            bufD[b * SX + k] += gv;
+          }
+        }
+        __syncthreads();
+      }
       stamp(p.stamps, 4 + (H - l < 3 ? H - l : 3), tid);
     }
   }
@@ -725,40 +769,49 @@ __global__ void __launch_bounds__(256) bce_grad_kernel(const float* __restrict__
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <int D, int TPW>
+template <int D, int TPW, int NG>
 static hipError_t launch_bwd_t(const BwdArgs& a, size_t lds, hipStream_t s) {
-  auto k = bwd_kernel<D, TPW>;
+  auto k = bwd_kernel<D, TPW, NG>;
   {
     hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
     if (e != hipSuccess) return e;
   }
   const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NG), lds, s, a);
   return hipGetLastError();
 }
 
 template <int D>
-static hipError_t launch_bwd_d(const BwdArgs& a, int tpw, size_t lds, hipStream_t s) {
+static hipError_t launch_bwd_d(const BwdArgs& a, int tpw, int ng, size_t lds, hipStream_t s) {
+  if (ng == 8) {
+    switch (tpw) {
+      case 1: return launch_bwd_t<D, 1, 8>(a, lds, s);
+      case 2: return launch_bwd_t<D, 2, 8>(a, lds, s);
+      case 3: return launch_bwd_t<D, 3, 8>(a, lds, s);
+      case 4: return launch_bwd_t<D, 4, 8>(a, lds, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (tpw) {
-    case 1: return launch_bwd_t<D, 1>(a, lds, s);
-    case 2: return launch_bwd_t<D, 2>(a, lds, s);
-    case 3: return launch_bwd_t<D, 3>(a, lds, s);
-    case 4: return launch_bwd_t<D, 4>(a, lds, s);
-    case 5: return launch_bwd_t<D, 5>(a, lds, s);
-    case 6: return launch_bwd_t<D, 6>(a, lds, s);
-    case 7: return launch_bwd_t<D, 7>(a, lds, s);
-    case 8: return launch_bwd_t<D, 8>(a, lds, s);
+    case 1: return launch_bwd_t<D, 1, 4>(a, lds, s);
+    case 2: return launch_bwd_t<D, 2, 4>(a, lds, s);
+    case 3: return launch_bwd_t<D, 3, 4>(a, lds, s);
+    case 4: return launch_bwd_t<D, 4, 4>(a, lds, s);
+    case 5: return launch_bwd_t<D, 5, 4>(a, lds, s);
+    case 6: return launch_bwd_t<D, 6, 4>(a, lds, s);
+    case 7: return launch_bwd_t<D, 7, 4>(a, lds, s);
+    case 8: return launch_bwd_t<D, 8, 4>(a, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_backward(const BwdArgs& a, int D, int tpw, size_t lds, hipStream_t s) {
+hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds, hipStream_t s) {
   switch (D) {
-    case 4: return launch_bwd_d<4>(a, tpw, lds, s);
-    case 8: return launch_bwd_d<8>(a, tpw, lds, s);
-    case 10: return launch_bwd_d<10>(a, tpw, lds, s);
-    case 16: return launch_bwd_d<16>(a, tpw, lds, s);
-    case 32: return launch_bwd_d<32>(a, tpw, lds, s);
+    case 4: return launch_bwd_d<4>(a, tpw, ng, lds, s);
+    case 8: return launch_bwd_d<8>(a, tpw, ng, lds, s);
+    case 10: return launch_bwd_d<10>(a, tpw, ng, lds, s);
+    case 16: return launch_bwd_d<16>(a, tpw, ng, lds, s);
+    case 32: return launch_bwd_d<32>(a, tpw, ng, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
