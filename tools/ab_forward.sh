@@ -1,5 +1,4 @@
 #!/bin/bash
-# GPU check of the training suite, then the training step with both backward layouts.
+# dW batch-split sweep (DFWFM_DW_SPLITS, tuning only): training step time per setting.
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_gpu_train.py} -x -q --timeout 120 --timeout-method thread > gpurun_out/par.log 2>&1; rc=$?; tail -25 gpurun_out/par.log; [ $rc -ne 0 ] && exit $rc
-for ng in 8 4; do DFWFM_NG=$ng timeout -k 10 200 python tools/bench_train.py --steps 100 2>&1 | tail -1 || exit 1; done
+for sp in 2 4 7 10 14; do echo "splits=$sp $(DFWFM_DW_SPLITS=$sp timeout -k 10 200 python tools/bench_train.py --steps 100 2>&1 | tail -1 | python -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"])')" || exit 1; done

@@ -576,8 +576,10 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 // the next chunk's global loads in registers while the current chunk's MFMAs run.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
-  __shared__ __attribute__((aligned(16))) float gs[32][64 + 4];
-  __shared__ __attribute__((aligned(16))) float xs[32][64 + 4];
+  // row stride 80 = 16 mod 64 banks: the four 16-lane row groups of an MFMA fragment read hit
+  // disjoint banks (68 overlapped them ~2.3-way)
+  __shared__ __attribute__((aligned(16))) float gs[32][64 + 16];
+  __shared__ __attribute__((aligned(16))) float xs[32][64 + 16];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
