@@ -161,6 +161,17 @@ typedef struct {
  * / batch for the reference's BCE-with-logits mean, :634).  Replaces loss.backward() (:636). */
 int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads, void* stream);
 
+/* The same backward in two parts, so that a data-parallel caller can start the all-reduce of every
+ * gradient except the MLP weights' while those are still being formed (bucketed all-reduce
+ * overlapped with the weight-gradient GEMM): DFWFM_BWD_TABLES = the per-tile backward, the shallow
+ * reductions and the table scatter (every gradient but lin_w / lin_b); DFWFM_BWD_MLP_WEIGHTS =
+ * dW_l and db_l (reads what the first part saved).  Same results as dfwfm_backward when both run,
+ * in this order, on one stream. */
+#define DFWFM_BWD_TABLES 1
+#define DFWFM_BWD_MLP_WEIGHTS 2
+int dfwfm_backward_phases(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads, int32_t phases,
+                          void* stream);
+
 /* One tensor of an Adam step (device pointers; grad NULL = tensor skipped, as torch does). */
 typedef struct {
   float* param;

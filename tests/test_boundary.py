@@ -26,7 +26,8 @@ def header_functions():
 
 def test_header_declares_expected_api():
     assert header_functions() == sorted([
-        "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_bce_grad",
+        "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_backward_phases",
+        "dfwfm_bce_grad",
         "dfwfm_diag_stamps", "dfwfm_eval_metrics", "dfwfm_forward", "dfwfm_forward_workspace_bytes",
         "dfwfm_forward_ws", "dfwfm_last_error", "dfwfm_model_create", "dfwfm_model_destroy",
         "dfwfm_metrics_workspace_bytes", "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_prune_apply", "dfwfm_prune_threshold",

@@ -33,6 +33,7 @@ INGEST_HEADERS = [os.path.join("..", "..", "include", "dfwfm_ingest.h")]
 DFWFM_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported", -3: "HIP error", -4: "bad state"}
 FLAG_INDEX_OUT_OF_RANGE = 1
+BWD_TABLES, BWD_MLP_WEIGHTS = 1, 2  # dfwfm_backward_phases
 ADAM_STATE_BYTES = 48
 
 
@@ -92,6 +93,7 @@ SIGNATURES = {
     "dfwfm_train_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P,
                                            ctypes.c_float, ctypes.c_uint32, _P]),
     "dfwfm_backward": (ctypes.c_int, [_P, _P, ctypes.POINTER(dfwfm_grads), _P]),
+    "dfwfm_backward_phases": (ctypes.c_int, [_P, _P, ctypes.POINTER(dfwfm_grads), ctypes.c_int32, _P]),
     "dfwfm_adam_step": (ctypes.c_int, [ctypes.POINTER(dfwfm_adam_tensor), ctypes.c_int32, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int64, _P]),

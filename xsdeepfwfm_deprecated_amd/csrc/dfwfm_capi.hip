@@ -565,8 +565,9 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   return DFWFM_OK;
 }
 
-int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, void* stream) {
+static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, int phases, void* stream) {
   if (!m || !g) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (phases & ~(DFWFM_BWD_TABLES | DFWFM_BWD_MLP_WEIGHTS)) return fail(DFWFM_ERR_INVALID_ARG, "unknown phase bits");
   if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_backward needs a preceding dfwfm_train_forward");
   const int64_t batch = m->t_batch;
   if (batch == 0) return DFWFM_OK;
@@ -577,7 +578,7 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
   hipError_t e;
 
   // 1. per-tile backward: dE and the G chain (no atomics)
-  if (m->flags & kNeedE) {
+  if ((phases & DFWFM_BWD_TABLES) && (m->flags & kNeedE)) {
     BwdArgs a;
     memset(&a, 0, sizeof a);
     a.batch = batch;
@@ -626,7 +627,7 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
   }
 
   // 2. dense shallow reductions: per 16-row tile, then summed over tiles
-  {
+  if (phases & DFWFM_BWD_TABLES) {
     RedArgs r;
     memset(&r, 0, sizeof r);
     r.batch = batch;
@@ -659,7 +660,7 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
   }
 
   // 3. categorical tables: privatised (LDS) tasks for small tables, atomic tasks for large ones
-  if (g->fields) {
+  if ((phases & DFWFM_BWD_TABLES) && g->fields) {
     ScatterArgs priv, atom;
     memset(&priv, 0, sizeof priv);
     priv.D = D;
@@ -737,7 +738,7 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
   }
 
   // 4. dW_l += G_l^T X_{l-1}, db_l += sum_b G_l
-  if (H > 0 && (g->lin_w || g->lin_b)) {
+  if ((phases & DFWFM_BWD_MLP_WEIGHTS) && H > 0 && (g->lin_w || g->lin_b)) {
     DwArgs d;
     memset(&d, 0, sizeof d);
     d.H = H;
@@ -774,6 +775,14 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
     }
   }
   return DFWFM_OK;
+}
+
+int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, void* stream) {
+  return backward_impl(m, dlogit, g, DFWFM_BWD_TABLES | DFWFM_BWD_MLP_WEIGHTS, stream);
+}
+
+int dfwfm_backward_phases(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, int32_t phases, void* stream) {
+  return backward_impl(m, dlogit, g, phases, stream);
 }
 
 int dfwfm_adam_step(const dfwfm_adam_tensor* t, int32_t n, double lr, double beta1, double beta2, double eps,

@@ -138,7 +138,13 @@ class FusedTrainStep:
         known |= {id(t) for t in dense["lin_w"] + dense["lin_b"]}
         if any(id(p) not in known for p in params):
             raise NotImplementedError("FusedTrainStep: a trainable parameter outside the kernels' layout")
+        # gradient buffer order: every gradient the backward's first part writes (tables, shallow dense,
+        # net_1_fc), then the MLP weights / biases the weight-gradient GEMM writes last -- two
+        # contiguous buckets, so under data parallelism the first bucket's all-reduce overlaps the GEMM
+        mlp_ids = {id(t) for t in dense["lin_w"] + dense["lin_b"]}
+        params = [p for p in params if id(p) not in mlp_ids] + [p for p in params if id(p) in mlp_ids]
         total = sum(p.numel() for p in params)
+        self.n_bucket_a = sum(p.numel() for p in params if id(p) not in mlp_ids)
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -204,8 +210,18 @@ class FusedTrainStep:
         _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(self.out.data_ptr()), ctypes.c_void_p(self.y.data_ptr()), n,
                                     float(denom), ctypes.c_void_p(self.dlogit.data_ptr()),
                                     ctypes.c_void_p(self.loss_sum.data_ptr()), st), "dfwfm_bce_grad")
-        _lib.check(L.dfwfm_backward(h, ctypes.c_void_p(self.dlogit.data_ptr()), ctypes.byref(self.grads), st),
-                   "dfwfm_backward")
+        phases = _lib.BWD_TABLES if self._bucketed() else (_lib.BWD_TABLES | _lib.BWD_MLP_WEIGHTS)
+        _lib.check(L.dfwfm_backward_phases(h, ctypes.c_void_p(self.dlogit.data_ptr()), ctypes.byref(self.grads),
+                                           phases, st), "dfwfm_backward_phases")
+
+    def _part1b(self):
+        """The MLP weight gradients (dW_l, db_l): the backward's second part under data parallelism."""
+        _lib.check(self.L.dfwfm_backward_phases(self.eng.handle, ctypes.c_void_p(self.dlogit.data_ptr()),
+                                                ctypes.byref(self.grads), _lib.BWD_MLP_WEIGHTS, self._stream()),
+                   "dfwfm_backward_phases")
+
+    def _bucketed(self):
+        return self.dist is not None and self.n_bucket_a < self.grad.numel()
 
     def _part2(self):
         b1, b2 = self.betas
@@ -213,22 +229,41 @@ class FusedTrainStep:
                                               ctypes.c_void_p(self.state.data_ptr()), self._stream()),
                    "dfwfm_adam_step_dev")
 
-    def _allreduce(self):
-        if self.dist is not None:
+    def _exchange(self, run_part1b):
+        """Data parallelism: all-reduce the gradient buffer (RCCL).  Bucketed: the first bucket (every
+        gradient but the MLP weights') goes out as soon as the backward's first part is done and runs
+        while the weight-gradient GEMM (run_part1b) forms the second bucket; otherwise one call."""
+        if self.dist is None:
+            run_part1b()
+            return
+        if not self._bucketed():
+            run_part1b()
             self.dist.all_reduce(self.grad)
+            return
+        wa = self.dist.all_reduce(self.grad[:self.n_bucket_a], async_op=True)
+        run_part1b()
+        wb = self.dist.all_reduce(self.grad[self.n_bucket_a:], async_op=True)
+        wa.wait()
+        wb.wait()
 
     def _capture(self, denom):
-        """Two graphs: forward + backward, then Adam (an RCCL all-reduce runs between them under DP)."""
+        """Graphs: forward + backward (its MLP-weight part separately under DP, see _exchange), then Adam;
+        the RCCL all-reduces run between them."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s):
                 self._part1(self.B, denom)
+            if self._bucketed():
+                with torch.cuda.graph(g1b, stream=s):
+                    self._part1b()
+            else:
+                g1b = None
             with torch.cuda.graph(g2, stream=s):
                 self._part2()
         torch.cuda.current_stream(self.dev).wait_stream(s)
-        return g1, g2
+        return g1, g1b, g2
 
     def step(self, xi, xv, y, n_global=None):
         """One step on device tensors xi [n, F-num] int64, xv [n, num] f32, y [n] f32 (n <= batch_size);
@@ -248,12 +283,13 @@ class FusedTrainStep:
             if self.graphs is None or self._graph_key != (denom, self.drop):
                 self.graphs = self._capture(denom)
                 self._graph_key = (denom, self.drop)
-            self.graphs[0].replay()
-            self._allreduce()
-            self.graphs[1].replay()
+            g1, g1b, g2 = self.graphs
+            g1.replay()
+            self._exchange(lambda: g1b.replay() if g1b is not None else None)
+            g2.replay()
         else:
             self._part1(n, denom)
-            self._allreduce()
+            self._exchange(self._part1b if self._bucketed() else (lambda: None))
             self._part2()
         self.steps += 1
         self.eng._dense_key = None  # weights changed behind torch's version counters: re-pack on next use
