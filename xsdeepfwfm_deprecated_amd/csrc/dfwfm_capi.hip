@@ -674,7 +674,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     priv.dlogit = dlogit;
     priv.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
     memcpy(&atom, &priv, sizeof priv);
-    priv.chunk = 1024;  // 4 samples per lane
+    priv.chunk = 256;   // more workgroups: the privatised tasks alone would not fill the chip
     atom.chunk = 256;
     const int64_t pchunks = (batch + priv.chunk - 1) / priv.chunk;
     const int64_t achunks = (batch + atom.chunk - 1) / atom.chunk;
@@ -691,7 +691,10 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       if (!gt || rows <= 0) return DFWFM_OK;
       if (rows > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: table of more than 2^31 rows", f);
       const int w = src == 0 ? D : 1;
-      const bool is_priv = rows * (w + 1) <= kPrivFloats;
+      // tables up to kPrivRows rows (and kPrivFloats of LDS) accumulate privately; bigger ones spread
+      // their atomics well enough (DFWFM_PRIV_ROWS: tuning only)
+      static const int64_t priv_rows = getenv("DFWFM_PRIV_ROWS") ? atoll(getenv("DFWFM_PRIV_ROWS")) : kPrivRows;
+      const bool is_priv = rows * (w + 1) <= kPrivFloats && rows <= priv_rows;
       ScatterArgs& L = is_priv ? priv : atom;
       const int64_t nb = is_priv ? pchunks : achunks;
       if (L.ntasks == kScatterList || blocks[is_priv] + nb > 0x7fffffff) {

@@ -541,17 +541,34 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
     return v;
   };
   const int ne = ns * w;
+  // elements in groups of SU per thread: all SU value loads are issued before the first atomic (an
+  // atomic between two loads keeps the compiler from batching them: one memory round trip per element)
+  constexpr int SU = 8;
   if constexpr (PRIV) {
     int* flag = reinterpret_cast<int*>(acc + T.rows * w);
     const int n = T.rows * (w + 1);
     for (int i = tid; i < n; i += 256) acc[i] = 0.f;  // sums and row flags
     __syncthreads();
-    for (int i = tid; i < ne; i += 256) {
-      const int sl = i / w;
-      const int d = i - sl * w;
-      const int row = srow[sl];
-      atomicAdd(&acc[row * w + d], value(s0 + sl, spart[sl], d));
-      if (d == 0) flag[row] = 1;
+    for (int i0 = 0; i0 < ne; i0 += 256 * SU) {
+      float v[SU];
+      int at[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = i0 + tid + 256 * u;
+        at[u] = -1;
+        v[u] = 0.f;
+        if (i < ne) {
+          const int sl = i / w;
+          const int d = i - sl * w;
+          const int row = srow[sl];
+          at[u] = row * w + d;
+          v[u] = value(s0 + sl, spart[sl], d);
+          if (d == 0) flag[row] = 1;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u)
+        if (at[u] >= 0) atomicAdd(&acc[at[u]], v[u]);
     }
     __syncthreads();
     // flush every touched row once, lane per element
@@ -562,10 +579,24 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
     }
   } else {
     __syncthreads();
-    for (int i = tid; i < ne; i += 256) {
-      const int sl = i / w;
-      const int d = i - sl * w;
-      atomicAdd(T.g + (int64_t)srow[sl] * w + d, value(s0 + sl, spart[sl], d));
+    for (int i0 = 0; i0 < ne; i0 += 256 * SU) {
+      float v[SU];
+      int64_t at[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = i0 + tid + 256 * u;
+        at[u] = -1;
+        v[u] = 0.f;
+        if (i < ne) {
+          const int sl = i / w;
+          const int d = i - sl * w;
+          at[u] = (int64_t)srow[sl] * w + d;
+          v[u] = value(s0 + sl, spart[sl], d);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u)
+        if (at[u] >= 0) atomicAdd(T.g + at[u], v[u]);
     }
   }
 }
@@ -845,7 +876,14 @@ hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s)
 hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s) {
   if (total_blocks <= 0 || a.ntasks <= 0) return hipSuccess;
   if (a.chunk > 4 * 256) return hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * kPrivFloats;
+  // LDS for the largest table of this launch only (not kPrivFloats): more workgroups per CU
+  size_t floats = 0;
+  for (int i = 0; i < a.ntasks; ++i) {
+    const size_t f = (size_t)a.t[i].rows * ((a.t[i].src == 0 ? a.D : 1) + 1);
+    floats = f > floats ? f : floats;
+  }
+  if (floats > (size_t)kPrivFloats) return hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * (floats > 0 ? floats : 1);
   auto k = scatter_kernel<true>;
   hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
   if (e != hipSuccess) return e;
