@@ -285,6 +285,48 @@ __host__ __device__ inline RedLds red_layout(int F, int D, int N, int num) {
 
 // copy n contiguous floats (16-byte aligned source and destination offsets) global -> LDS, zero-filling
 // [n, ncap); U float4 per thread in flight
+// stage_linear in two halves, so that several sources' loads are in flight together: stage_issue
+// loads the first 256*U float4 into registers, stage_commit stores them and copies any remainder
+template <int U>
+__device__ __forceinline__ void stage_issue(f32x4 (&v)[U], const float* __restrict__ src, int n, int ncap, int tid) {
+  const int n4 = ncap >> 2;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int q = tid + u * 256;
+    const int e = q * 4;
+    v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (q < n4 && e + 3 < n) {
+      v[u] = *reinterpret_cast<const f32x4*>(src + e);
+    } else if (q < n4) {
+      v[u].x = e < n ? src[e] : 0.f;
+      v[u].y = e + 1 < n ? src[e + 1] : 0.f;
+      v[u].z = e + 2 < n ? src[e + 2] : 0.f;
+    }
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void stage_commit(float* __restrict__ dst, const f32x4 (&v)[U], const float* __restrict__ src,
+                                             int n, int ncap, int tid) {
+  const int n4 = ncap >> 2;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int q = tid + u * 256;
+    if (q < n4) *reinterpret_cast<f32x4*>(dst + q * 4) = v[u];
+  }
+  for (int q = tid + 256 * U; q < n4; q += 256) {
+    const int e = q * 4;
+    f32x4 w = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e + 3 < n) w = *reinterpret_cast<const f32x4*>(src + e);
+    else {
+      w.x = e < n ? src[e] : 0.f;
+      w.y = e + 1 < n ? src[e + 1] : 0.f;
+      w.z = e + 2 < n ? src[e + 2] : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(dst + q * 4) = w;
+  }
+}
+
 template <int U>
 __device__ __forceinline__ void stage_linear(float* __restrict__ dst, const float* __restrict__ src, int n, int ncap,
                                              int tid) {
@@ -335,20 +377,45 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
   const bool need_e = a.g_fwlw || a.g_R;
   const bool need_num2 = numD > 0 && a.sv_de != nullptr;
   if (tid < kBM) dl[tid] = tid < nt ? a.dlogit[rb + tid] : 0.f;
-  if (need_e) stage_linear<8>(es, a.sv_e + rb * SE, nt * SE, kBM * SE, tid);
-  if (a.g_lw) stage_linear<2>(fos, a.sv_fo + rb * F, nt * F, r4(kBM * F), tid);
-  if (a.g_fc) stage_linear<8>(xhs, a.x_h + rb * N, nt * N, r4(kBM * N), tid);
-  if (num > 0)
-    for (int i = tid; i < kBM * num; i += NTH) {
+  // every staging load is issued before any LDS store: one memory round trip instead of one per
+  // source (the tiles are contiguous rows of the workspace)
+  constexpr int UE = 8, UF = 2, UH = 8, UD = 9;
+  f32x4 ve[UE], vf[UF], vh[UH];
+  float vd[UD], vx = 0.f;
+  if (need_e) stage_issue<UE>(ve, a.sv_e + rb * SE, nt * SE, kBM * SE, tid);
+  if (a.g_lw) stage_issue<UF>(vf, a.sv_fo + rb * F, nt * F, r4(kBM * F), tid);
+  if (a.g_fc) stage_issue<UH>(vh, a.x_h + rb * N, nt * N, r4(kBM * N), tid);
+  if (num > 0 && tid < kBM * num) {
+    const int b = tid / num, c = tid - b * num;
+    vx = b < nt ? a.xv[(rb + b) * a.xv_stride + c] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < UD; ++u) {
+    const int i = tid + u * NTH;
+    const int b = i / (numD > 0 ? numD : 1), c = i - b * numD;
+    vd[u] = (need_num2 && i < kBM * numD && b < nt) ? a.sv_de[(rb + b) * FD + c] : 0.f;
+  }
+  if (need_e) stage_commit<UE>(es, ve, a.sv_e + rb * SE, nt * SE, kBM * SE, tid);
+  if (a.g_lw) stage_commit<UF>(fos, vf, a.sv_fo + rb * F, nt * F, r4(kBM * F), tid);
+  if (a.g_fc) stage_commit<UH>(xhs, vh, a.x_h + rb * N, nt * N, r4(kBM * N), tid);
+  if (num > 0) {
+    if (tid < kBM * num) xvs[tid] = vx;
+    for (int i = tid + NTH; i < kBM * num; i += NTH) {  // num > 16
       const int b = i / num, c = i - b * num;
       xvs[i] = b < nt ? a.xv[(rb + b) * a.xv_stride + c] : 0.f;
     }
-  if (need_num2)
-#pragma unroll 4
-    for (int i = tid; i < kBM * numD; i += NTH) {
+  }
+  if (need_num2) {
+#pragma unroll
+    for (int u = 0; u < UD; ++u) {
+      const int i = tid + u * NTH;
+      if (i < kBM * numD) des[i] = vd[u];
+    }
+    for (int i = tid + UD * NTH; i < kBM * numD; i += NTH) {  // wider numerical parts
       const int b = i / numD, c = i - b * numD;
       des[i] = b < nt ? a.sv_de[(rb + b) * FD + c] : 0.f;
     }
+  }
   __syncthreads();
 
   float* out = a.part + (size_t)blockIdx.x * red_outputs(F, D, N, num);
@@ -419,15 +486,34 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
       const int mk = t / MT, ml = t - mk * MT;
       const int kA = 16 * mk + (lane & 15);
       const int lB = 16 * ml + (lane & 15);
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < steps; ++s) {
+      // two accumulators, each group's eight operands read from LDS before its four MFMAs (one
+      // dependent chain over 40 steps exposed the MFMA and LDS latencies at every step)
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      int s = 0;
+      for (; s + 4 <= steps; s += 4) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int n = 4 * (s + u) + (lane >> 4);
+          const int b = n / D;
+          const int d = n - b * D;
+          av[u] = kA < F ? dl[b] * es[b * SE + kA * D + d] : 0.f;
+          bv[u] = lB < F ? es[b * SE + lB * D + d] : 0.f;
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc1, 0, 0, 0);
+      }
+      for (; s < steps; ++s) {
         const int n = 4 * s + (lane >> 4);
         const int b = n / D;
         const int d = n - b * D;
         const float av = kA < F ? dl[b] * es[b * SE + kA * D + d] : 0.f;
         const float bv = lB < F ? es[b * SE + lB * D + d] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
       }
+      const f32x4 acc = acc0 + acc1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int k = 16 * mk + (lane >> 4) * 4 + r;
