@@ -255,15 +255,17 @@ def main():
         "wall_s": round(wall, 4),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, params, sizes, a.cpu_seconds)
+        result["cpu_baseline"], result["parity"] = cpu_baseline(cfg, params, sizes, a.cpu_seconds, model, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
-def cpu_baseline(cfg, params, sizes, seconds):
-    """oracle/torch_port.py (the reference's fp32 op sequence on PyTorch-CPU) on this host's cores."""
+def cpu_baseline(cfg, params, sizes, seconds, model=None, dev=None):
+    """oracle/torch_port.py (the reference's fp32 op sequence on PyTorch-CPU) on this host's cores; and,
+    on the same batch, the HIP forward's logits and AUC against the port's (the metric's "AUC match":
+    labels drawn from the port's sigmoid, AUC of both score vectors by the on-device metrics)."""
     from oracle import torch_port
     from xsdeepfwfm_deprecated_amd import synth
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
@@ -271,7 +273,7 @@ def cpu_baseline(cfg, params, sizes, seconds):
     tp = {k: torch.from_numpy(v) for k, v in params.items()}
     xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=99)
     xi, xv = torch.from_numpy(xi), torch.from_numpy(xv)
-    torch_port.forward(cfg, tp, xi, xv)  # warm-up
+    out_cpu = torch_port.forward(cfg, tp, xi, xv)  # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
         torch_port.forward(cfg, tp, xi, xv)
@@ -287,9 +289,25 @@ def cpu_baseline(cfg, params, sizes, seconds):
                 break
     except OSError:
         pass
-    return {"value": round(n * BATCH / el, 1), "unit": "samples/s", "cores": cores, "kind": "port",
+    base = {"value": round(n * BATCH / el, 1), "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"{n} batches x {BATCH} rows of the same Criteo-39 workload, {el:.1f} s, "
                       f"torch {torch.__version__} CPU, {cores} threads, {cpu}"}
+    parity = None
+    if model is not None:
+        from xsdeepfwfm_deprecated_amd.metrics import DeviceMetrics
+        with torch.no_grad():
+            out_gpu = model(xi.to(dev), xv.to(dev))
+        ref = out_cpu.detach().to(torch.float64)
+        rel = ((out_gpu.cpu().to(torch.float64) - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
+        g = torch.Generator().manual_seed(7)
+        y = (torch.rand(BATCH, generator=g, dtype=torch.float64) < torch.sigmoid(ref)).to(torch.float32)
+        dm = DeviceMetrics(dev)
+        auc_gpu = dm(out_gpu, y.to(dev))["auc"]
+        auc_cpu = dm(out_cpu.detach().to(torch.float32).to(dev), y.to(dev))["auc"]
+        parity = {"rows": BATCH, "max_rel_logit_diff_vs_cpu_port": rel, "auc_gpu": round(auc_gpu, 6),
+                  "auc_cpu_port": round(auc_cpu, 6), "abs_auc_diff": abs(auc_gpu - auc_cpu),
+                  "bars": "logits 1e-5 * max(1, |ref|), AUC 1e-4 (BASELINE north_star)"}
+    return base, parity
 
 
 if __name__ == "__main__":
