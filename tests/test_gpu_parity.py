@@ -316,3 +316,14 @@ def test_custom_op_opcheck_and_matches_engine(gpu):
     with torch.no_grad():
         out, tok = torch.ops.dfwfm.forward(mid, xi_t, xv_t, plist, False, 0.0, 0)
     assert torch.equal(out.cpu(), ref.cpu())
+
+
+@pytest.mark.parametrize("F,num,D,N,H", [(64, 16, 10, 256, 5), (20, 0, 8, 128, 2), (39, 39, 4, 64, 1)])
+def test_forward_extreme_shapes_match_oracle(gpu, F, num, D, N, H):
+    """The limits of the layout: 64 fields (four FwFM row tiles), no numerical field, only numerical
+    fields (no Xi at all), five hidden layers."""
+    cfg, params, xi, xv = _sweep_case(F, num, D, N, H, 0, seed=F + num + D + N + H)
+    m = make_model(cfg, params, gpu)
+    got = run(m, xi, xv, gpu)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close(got, ref) < 1e-5
