@@ -14,7 +14,9 @@ kernel runs on, bracketed by barrier + synchronize, max over ranks.
 Rank 0 prints one JSON line with the throughput, the roofline of the fused
 kernel (MFMA-bound: its MLP is 98.5 % of the arithmetic) and, at N = 1, the
 host-CPU baseline (oracle/torch_port.py, the reference's op sequence in fp32
-PyTorch-CPU) timed on this machine's cores.
+PyTorch-CPU) timed on this machine's cores, with the HIP logits / AUC checked
+against that port on the same batch (``parity``).  ``--config qr|pruned`` runs
+BASELINE.json configs[2] / [3] instead of configs[1].
 """
 from __future__ import annotations
 
