@@ -41,8 +41,8 @@ PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md, HBM3E spec peak
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=600)
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
     ap.add_argument("--config", choices=["deepfwfm", "qr", "pruned"], default="deepfwfm",
                     help="BASELINE.json configs[1] (default), [2] QR embeddings (embedding_bag=1 qr_flag=1, c=4, "
@@ -144,9 +144,12 @@ def main():
             eng.forward(xi, xv, outs[k])
 
         # G consecutive forwards per captured graph (launch cost amortised: a single-kernel
-        # replay is host-bound at ~10-16 us); a remainder graph keeps the count at exactly K.
-        # With S streams each stream replays its own graphs: S batches in flight at once.
-        G = max(1, min(a.graph_steps, a.steps))
+        # replay is host-bound at ~10-16 us); remainder graphs keep the count exact.  With S streams
+        # each stream replays its own graphs (S batches in flight at once) and the K steps are split
+        # over the streams: exactly K batches are timed.
+        def per_stream(n):
+            return [n // S + (1 if k < n % S else 0) for k in range(S)]
+        G = max(1, min(a.graph_steps, max(per_stream(a.steps))))
         graphs = None
         if not a.no_graph:
             def capture(n, k):
@@ -161,29 +164,29 @@ def main():
             graphs = []
             for k in range(S):
                 gk = {G: capture(G, k)}
-                if a.steps % G:
-                    gk[a.steps % G] = capture(a.steps % G, k)
-                if a.warmup % G:
-                    gk.setdefault(a.warmup % G, capture(a.warmup % G, k))
+                for n in per_stream(a.steps) + per_stream(a.warmup):
+                    if n % G and n % G not in gk:
+                        gk[n % G] = capture(n % G, k)
                 graphs.append(gk)
 
-        def run_n(n):
+        def run_n(n_total):
             # enqueue round-robin over the streams (stream k's replays must not wait behind the host
             # enqueueing all of stream 0's first: the streams would start one after the other)
+            ns = per_stream(n_total)
             if graphs is None:
-                for i in range(n):
+                for i in range(max(ns)):
                     for k in range(S):
-                        with torch.cuda.stream(streams[k]):
-                            step(i, k)
+                        if i < ns[k]:
+                            with torch.cuda.stream(streams[k]):
+                                step(i, k)
                 return
-            for _ in range(n // G):
+            for r in range(max(ns) // G + 1):
                 for k in range(S):
+                    left = ns[k] - r * G
+                    if left <= 0:
+                        continue
                     with torch.cuda.stream(streams[k]):
-                        graphs[k][G].replay()
-            if n % G:
-                for k in range(S):
-                    with torch.cuda.stream(streams[k]):
-                        graphs[k][n % G].replay()
+                        graphs[k][G if left >= G else left].replay()
 
         run_n(a.warmup)
         torch.cuda.synchronize(dev)
@@ -213,14 +216,14 @@ def main():
         if world > 1:
             torch.distributed.barrier()
     ms = t0.elapsed_time(t1)
-    launch_ms = sum(s0[k].elapsed_time(s1[k]) for k in range(S)) / (S * a.steps)
+    launch_ms = sum(s0[k].elapsed_time(s1[k]) for k in range(S)) / a.steps  # per launch, S side by side
     if world > 1:
         t = torch.tensor([ms], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         ms = float(t.item())
 
-    ms_per_step = ms / (a.steps * S)
-    value = world * S * BATCH * a.steps / (ms / 1e3)
+    ms_per_step = ms / a.steps
+    value = world * BATCH * a.steps / (ms / 1e3)
     flops, bytes_ = algorithmic_counts(cfg, sizes)
     # achieved = algorithmic FLOP of one launch / its duration, times the launches in flight (each of
     # the S concurrent launches takes ~S x the per-batch time): the aggregate rate over the timed region
@@ -246,7 +249,7 @@ def main():
                                + f"; batch {BATCH} per GPU",
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
-                   "launch": ("eager" if a.no_graph else f"hipGraph replay, {min(a.graph_steps, a.steps)} forwards per graph")
+                   "launch": ("eager" if a.no_graph else f"hipGraph replay, {G} forwards per graph")
                              + (f", {S} streams (batches in flight)" if S > 1 else "")},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "traffic": traffic,
