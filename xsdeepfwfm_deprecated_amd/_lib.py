@@ -153,17 +153,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
     """Compile libdfwfm.so for gfx950 in-tree (hipcc cross-compiles without a GPU): one object per
     translation unit, compiled in parallel, then linked; and the host-only ingest library."""
     build_ingest(force, verbose)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"] + os.environ.get("DFWFM_HIPCC_FLAGS", "").split()
+    stamp = os.path.join(CSRC, ".build_flags")  # objects (and the library) built with other flags are stale
+    if not os.path.exists(stamp) or open(stamp).read() != " ".join(flags):
+        force = True
     if not force and not _stale():
         return LIB_PATH
     from concurrent.futures import ThreadPoolExecutor
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"] + os.environ.get("DFWFM_HIPCC_FLAGS", "").split()
     objs = [os.path.join(CSRC, os.path.splitext(s)[0] + ".o") for s in SOURCES]
-
     hdr_m = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
-    stamp = os.path.join(CSRC, ".build_flags")  # objects built with other flags are stale
-    if not os.path.exists(stamp) or open(stamp).read() != " ".join(flags):
-        force = True
 
     def compile_one(i):
         src = os.path.join(CSRC, SOURCES[i])

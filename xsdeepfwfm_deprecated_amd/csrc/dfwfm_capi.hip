@@ -767,7 +767,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       if (splits > max_splits) splits = max_splits;
       if (splits < 1) splits = 1;
       int64_t rows = (batch + splits - 1) / splits;
-      rows = (rows + 31) / 32 * 32;
+      rows = (rows + 63) / 64 * 64;  // whole dw_kernel chunks
       splits = (batch + rows - 1) / rows;
       d.splits = (int32_t)splits;
       d.rows_per_split = rows;

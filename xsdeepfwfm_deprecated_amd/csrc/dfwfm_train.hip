@@ -692,11 +692,16 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 // wave w owns n rows 16w..16w+15 and the 4 k tiles.  32-row chunks of G and X are staged in LDS,
 // the next chunk's global loads in registers while the current chunk's MFMAs run.
 // ---------------------------------------------------------------------------
+#ifndef DFWFM_DW_RB
+#define DFWFM_DW_RB 64
+#endif
+constexpr int kDwRB = DFWFM_DW_RB;   // batch rows per staged chunk (one barrier pair per chunk)
+constexpr int kDwU = kDwRB * 16 / 256;
 __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
   // row stride 80 = 16 mod 64 banks: the four 16-lane row groups of an MFMA fragment read hit
   // disjoint banks (68 overlapped them ~2.3-way)
-  __shared__ __attribute__((aligned(16))) float gs[32][64 + 16];
-  __shared__ __attribute__((aligned(16))) float xs[32][64 + 16];
+  __shared__ __attribute__((aligned(16))) float gs[kDwRB][64 + 16];
+  __shared__ __attribute__((aligned(16))) float xs[kDwRB][64 + 16];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -718,11 +723,11 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
   const float* X = a.X[l];
   const int ldx = a.ldx[l];
 
-  // staging map: 32 rows x 64 cols = 512 float4 per operand, 2 per thread
-  float4 pg[2], px[2];
+  // staging map: kDwRB rows x 64 cols = kDwRB*16 float4 per operand, kDwU per thread
+  float4 pg[kDwU], px[kDwU];
   auto fetch = [&](int64_t rbase) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kDwU; ++u) {
       const int i = tid + u * 256;
       const int rr = i >> 4;
       const int c4 = (i & 15) * 4;
@@ -752,17 +757,17 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
   float* gB = kb == 0 ? a.gB[l] : nullptr;  // db_l = sum_b G_l[b, :] rides on the k-block-0 workgroups
   float bsum = 0.f;
   fetch(r_begin);
-  for (int64_t rb = r_begin; rb < r_end; rb += 32) {
+  for (int64_t rb = r_begin; rb < r_end; rb += kDwRB) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kDwU; ++u) {
       const int i = tid + u * 256;
       *reinterpret_cast<float4*>(&gs[i >> 4][(i & 15) * 4]) = pg[u];
       *reinterpret_cast<float4*>(&xs[i >> 4][(i & 15) * 4]) = px[u];
     }
     __syncthreads();
-    if (rb + 32 < r_end) fetch(rb + 32);
+    if (rb + kDwRB < r_end) fetch(rb + kDwRB);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < kDwRB / 4; ++s) {
       const int rr = 4 * s + (lane >> 4);
       const float av = gs[rr][16 * wave + (lane & 15)];
 #pragma unroll
@@ -770,7 +775,7 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
     }
     if (gB && tid < 64)
 #pragma unroll 8
-      for (int rr = 0; rr < 32; ++rr) bsum += gs[rr][tid];
+      for (int rr = 0; rr < kDwRB; ++rr) bsum += gs[rr][tid];
     __syncthreads();
   }
   if (gB && tid < 64 && n0 + tid < N) atomicAdd(gB + n0 + tid, bsum);
