@@ -93,11 +93,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    # one process per GPU; the modulo only matters for rehearsing N > 1 on fewer GPUs (with
+    # DFWFM_BENCH_BACKEND=gloo: RCCL refuses two ranks on one device)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("DFWFM_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
     sizes = synth.CRITEO_FEATURE_SIZES
