@@ -732,21 +732,12 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
       const int rr = i >> 4;
       const int c4 = (i & 15) * 4;
       const int64_t row = rbase + rr;
+      // whole float4 loads only (N and the X row stride are multiples of 4, dfwfm_train_begin): no
+      // per-element branches, whose merges made the compiler wait for each load inside the prefetch;
+      // X columns in [K, ldx) are zeroed when the chunk is stored to LDS
       float4 vg = make_float4(0.f, 0.f, 0.f, 0.f), vx = vg;
-      if (row < r_end) {
-        const float* gp = G + row * N + n0 + c4;
-        const float* xp = X + row * ldx + k0 + c4;
-        if (n0 + c4 + 3 < N) vg = *reinterpret_cast<const float4*>(gp);
-        else {
-          vg.x = n0 + c4 < N ? gp[0] : 0.f; vg.y = n0 + c4 + 1 < N ? gp[1] : 0.f;
-          vg.z = n0 + c4 + 2 < N ? gp[2] : 0.f; vg.w = 0.f;
-        }
-        if (k0 + c4 + 3 < K) vx = *reinterpret_cast<const float4*>(xp);
-        else {
-          vx.x = k0 + c4 < K ? xp[0] : 0.f; vx.y = k0 + c4 + 1 < K ? xp[1] : 0.f;
-          vx.z = k0 + c4 + 2 < K ? xp[2] : 0.f; vx.w = 0.f;
-        }
-      }
+      if (row < r_end && n0 + c4 < N) vg = *reinterpret_cast<const float4*>(G + row * N + n0 + c4);
+      if (row < r_end && k0 + c4 < ldx) vx = *reinterpret_cast<const float4*>(X + row * ldx + k0 + c4);
       pg[u] = vg;
       px[u] = vx;
     }
@@ -756,13 +747,20 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float* gB = kb == 0 ? a.gB[l] : nullptr;  // db_l = sum_b G_l[b, :] rides on the k-block-0 workgroups
   float bsum = 0.f;
+  const bool k_edge = k0 + 64 > K;
   fetch(r_begin);
   for (int64_t rb = r_begin; rb < r_end; rb += kDwRB) {
 #pragma unroll
     for (int u = 0; u < kDwU; ++u) {
       const int i = tid + u * 256;
+      float4 vx = px[u];
+      if (k_edge) {
+        const int c = k0 + (i & 15) * 4;
+        vx.x = c < K ? vx.x : 0.f; vx.y = c + 1 < K ? vx.y : 0.f;
+        vx.z = c + 2 < K ? vx.z : 0.f; vx.w = c + 3 < K ? vx.w : 0.f;
+      }
       *reinterpret_cast<float4*>(&gs[i >> 4][(i & 15) * 4]) = pg[u];
-      *reinterpret_cast<float4*>(&xs[i >> 4][(i & 15) * 4]) = px[u];
+      *reinterpret_cast<float4*>(&xs[i >> 4][(i & 15) * 4]) = vx;
     }
     __syncthreads();
     if (rb + kDwRB < r_end) fetch(rb + kDwRB);
