@@ -764,12 +764,28 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
     }
     __syncthreads();
     if (rb + kDwRB < r_end) fetch(rb + kDwRB);
+    // fragments of k-step s+1 are read from LDS while step s's MFMAs run
+    float av = gs[lane >> 4][16 * wave + (lane & 15)];
+    float bv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bv[t] = xs[lane >> 4][16 * t + (lane & 15)];
 #pragma unroll
     for (int s = 0; s < kDwRB / 4; ++s) {
-      const int rr = 4 * s + (lane >> 4);
-      const float av = gs[rr][16 * wave + (lane & 15)];
+      float an = 0.f, bn[4] = {0.f, 0.f, 0.f, 0.f};
+      if (s + 1 < kDwRB / 4) {
+        const int rn = 4 * (s + 1) + (lane >> 4);
+        an = gs[rn][16 * wave + (lane & 15)];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xs[rr][16 * t + (lane & 15)], acc[t], 0, 0, 0);
+        for (int t = 0; t < 4; ++t) bn[t] = xs[rn][16 * t + (lane & 15)];
+      }
+      // pin the order: the next fragments' reads issue before this step's MFMAs, their wait after
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[t], acc[t], 0, 0, 0);
+      asm volatile("" ::"v"(an), "v"(bn[0]), "v"(bn[1]), "v"(bn[2]), "v"(bn[3]));
+      av = an;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bv[t] = bn[t];
     }
     if (gB && tid < 64)
 #pragma unroll 8
