@@ -16,7 +16,8 @@ kernel (MFMA-bound: its MLP is 98.5 % of the arithmetic) and, at N = 1, the
 host-CPU baseline (oracle/torch_port.py, the reference's op sequence in fp32
 PyTorch-CPU) timed on this machine's cores, with the HIP logits / AUC checked
 against that port on the same batch (``parity``).  ``--config qr|pruned`` runs
-BASELINE.json configs[2] / [3] instead of configs[1].
+BASELINE.json configs[2] / [3] instead of configs[1]; ``--config fwfm`` runs configs[0]'s model (FwFM only,
+no MLP: the HBM-bound gather path) at the Criteo-39 bench size.
 """
 from __future__ import annotations
 
@@ -44,14 +45,18 @@ def parse():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=600)
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
-    ap.add_argument("--config", choices=["deepfwfm", "qr", "pruned"], default="deepfwfm",
-                    help="BASELINE.json configs[1] (default), [2] QR embeddings (embedding_bag=1 qr_flag=1, c=4, "
-                         "threshold 200, mult), [3] pruned (sparse 0.90, emb_r 0.444, prune_r 1: the reference's "
-                         "magnitude masks applied on the device)")
+    ap.add_argument("--config", choices=["deepfwfm", "fwfm", "qr", "pruned"], default="deepfwfm",
+                    help="BASELINE.json configs[1] (default), fwfm = configs[0]'s model (use_fwfm=1 use_deep=0: the "
+                         "HBM-bound gather path) at Criteo-39 batch 4096, [2] QR embeddings (embedding_bag=1 "
+                         "qr_flag=1, c=4, threshold 200, mult), [3] pruned (sparse 0.90, emb_r 0.444, prune_r 1: "
+                         "the reference's magnitude masks applied on the device)")
+    ap.add_argument("--settle-ms", type=float, default=400.0,
+                    help="untimed back-to-back forwards for this long before the warmup steps: the chip raises its "
+                         "clock over the first ~300 forwards (DESIGN.md section 7); reported in the JSON as 'settle'")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=20, help="forwards captured per hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU sample per thread count")
     ap.add_argument("--inputs", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--streams", type=int, default=2,
                     help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
@@ -59,9 +64,11 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_name():
+def kernel_name(config="deepfwfm"):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT select the A/B variants."""
+    if config == "fwfm":
+        return "dfwfm::fwd_kernel<10,1,1,false,0,4>"
     ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
     tpw = 6 if ng == 4 else 3
     if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):
@@ -75,7 +82,8 @@ def algorithmic_counts(cfg, sizes=None):
     ncat = F - num
     flops = 0
     flops += 741 * D * 2                              # FwFM pairs
-    flops += 2 * (F * D * N + (H - 1) * N * N + N)     # MLP + fc
+    if cfg["use_deep"]:
+        flops += 2 * (F * D * N + (H - 1) * N * N + N)  # MLP + fc
     flops += F * D * 2 if cfg["use_fwlw"] else 0       # fwlw
     bytes_ = ncat * 8 + num * 4 + ncat * D * 4 + 4     # Xi + Xv + gathered rows + logit
     if not cfg["use_fwlw"]:
@@ -110,14 +118,15 @@ def main():
     sizes = synth.CRITEO_FEATURE_SIZES
     fwlw = a.first_order == "fwlw"
     qr = a.config == "qr"
-    cfg = dict(field_size=39, numerical=13, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0, use_deep=1,
+    deep = int(a.config != "fwfm")
+    cfg = dict(field_size=39, numerical=13, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0, use_deep=deep,
                use_lw=1, use_fwlw=int(fwlw), h_depth=3, deep_nodes=400, embedding_bag=int(qr), qr_flag=int(qr),
                qr_operation="mult", qr_collisions=4, qr_threshold=200)
-    model = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1,
+    model = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=deep,
                     use_lw=1, use_fwlw=fwlw, numerical=13, embedding_bag=int(qr), qr_flag=int(qr),
                     qr_operation="mult", qr_collisions=4, qr_threshold=200, use_cuda=True)
     shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
-    params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=1234)
+    params = synth.synth_state(shapes, 39, 10, 400, True, bool(deep), seed=1234)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     model = model.to(dev).eval()
     model.strict_index_check = False
@@ -195,6 +204,17 @@ def main():
                     with torch.cuda.stream(streams[k]):
                         graphs[k][G if left >= G else left].replay()
 
+        # settle: untimed back-to-back forwards until the chip has run them for --settle-ms (its clock ramps
+        # over the first few hundred forwards); then the W warmup steps, then the K timed steps
+        settle_n, settle_t0 = 0, time.perf_counter()
+        chunk = max(S * G, 8)
+        while a.settle_ms > 0:
+            run_n(chunk)
+            settle_n += chunk
+            torch.cuda.synchronize(dev)
+            if (time.perf_counter() - settle_t0) * 1e3 >= a.settle_ms:
+                break
+        settle_ms = (time.perf_counter() - settle_t0) * 1e3
         run_n(a.warmup)
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -236,13 +256,8 @@ def main():
     # the S concurrent launches takes ~S x the per-batch time): the aggregate rate over the timed region
     achieved_tf = flops * BATCH * S / (launch_ms / 1e3) / 1e12
     achieved_gbs = bytes_ * BATCH * S / (launch_ms / 1e3) / 1e9
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    kname = kernel_name(a.config)
+    traffic = pmc_traffic(kname)
 
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
@@ -250,22 +265,31 @@ def main():
         "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic Criteo-39 ({a.inputs} indices over the real field sizes, Xv integers 0..63; "
                 "deterministic hash-init weights with the reference's init_weights scales)",
-        "config": {"workload": f"DeepFwFM forward, Criteo-39, emb 10, MLP 3x400, FwFM + {a.first_order}"
-                               + {"deepfwfm": "", "qr": ", QR embeddings (c=4, mult, threshold 200)",
+        "config": {"workload": (f"DeepFwFM forward, Criteo-39, emb 10, MLP 3x400, FwFM + {a.first_order}"
+                                if deep else f"FwFM-only forward (use_deep=0), Criteo-39, emb 10, FwFM + {a.first_order}")
+                               + {"deepfwfm": "", "fwfm": "", "qr": ", QR embeddings (c=4, mult, threshold 200)",
                                   "pruned": ", pruned (sparse 0.90, emb_r 0.444, prune_r 1)"}[a.config]
                                + f"; batch {BATCH} per GPU",
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
                    "launch": ("eager" if a.no_graph else f"hipGraph replay, {G} forwards per graph")
                              + (f", {S} streams (batches in flight)" if S > 1 else "")},
-        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "traffic": traffic,
-                     "kernel": kernel_name(), "flops_per_sample": flops,
-                     "units_per_launch": BATCH, "launch_us": round(launch_ms * 1e3, 3), "launches_in_flight": S},
-        "roofline_hbm": {"achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "bytes_per_sample": bytes_},
+        "settle": {"forwards": settle_n, "ms": round(settle_ms, 1),
+                   "what": "untimed back-to-back forwards before the warmup steps (clock ramp)"},
         "wall_s": round(wall, 4),
     }
+    mfma = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "flops_per_sample": flops}
+    hbm = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "bytes_per_sample": bytes_}
+    common = {"traffic": traffic, "kernel": kname, "units_per_launch": BATCH, "launch_us": round(launch_ms * 1e3, 3),
+              "launches_in_flight": S}
+    if cfg["use_deep"]:  # 98.5 % of the arithmetic is the MLP: MFMA-bound (intensity ~690 FLOP/B)
+        result["roofline"] = {**mfma, **common}
+        result["roofline_hbm"] = hbm
+    else:                # gather + FwFM only: ~12 FLOP/B, below the f32 ridge -> HBM-bound
+        result["roofline"] = {**hbm, **common}
+        result["roofline_mfma"] = mfma
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(cfg, params, sizes, a.cpu_seconds, model, dev)
     if rank == 0:
@@ -274,25 +298,58 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def cpu_baseline(cfg, params, sizes, seconds, model=None, dev=None):
-    """oracle/torch_port.py (the reference's fp32 op sequence on PyTorch-CPU) on this host's cores; and,
-    on the same batch, the HIP forward's logits and AUC against the port's (the metric's "AUC match":
-    labels drawn from the port's sigmoid, AUC of both score vectors by the on-device metrics)."""
-    from oracle import torch_port
-    from xsdeepfwfm_deprecated_amd import synth
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
-    torch.set_num_threads(cores)
-    tp = {k: torch.from_numpy(v) for k, v in params.items()}
-    xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=99)
-    xi, xv = torch.from_numpy(xi), torch.from_numpy(xv)
-    out_cpu = torch_port.forward(cfg, tp, xi, xv)  # warm-up
+def pmc_traffic(kname):
+    """HBM bytes per launch of `kname` from the committed PMC summary (tools/pmc.sh + tools/pmc_summary.py):
+    2 x FETCH_SIZE + WRITE_SIZE, FETCH doubled per the gfx950 calibration; None when not profiled."""
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(pmc))
+    except Exception:
+        return None
+    if "kernels" in d:
+        e = d["kernels"].get(kname)
+        return None if e is None else e.get("hbm_bytes_per_launch")
+    return d.get("hbm_bytes_per_launch") if d.get("kernel") == kname else None
+
+
+def _time_port(torch_port, cfg, tp, xi, xv, seconds, threads):
+    torch.set_num_threads(threads)
+    torch_port.forward(cfg, tp, xi, xv)  # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
         torch_port.forward(cfg, tp, xi, xv)
         n += 1
         el = time.perf_counter() - t0
         if (el >= seconds and n >= 2) or n >= 400:
-            break
+            return n, el
+
+
+def _cpu_quota():
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg, params, sizes, seconds, model=None, dev=None):
+    """oracle/torch_port.py (the reference's fp32 op sequence on PyTorch-CPU) on this host: every core of this
+    process's affinity mask, and one thread; the port / reference time ratio measured in the build container
+    (tools/calibrate_cpu_port.py -> profiles/cpu_calibration.json) rides along.  On the same batch, the HIP
+    forward's logits and AUC against the port's (the metric's "AUC match": labels drawn from the port's
+    sigmoid, AUC of both score vectors by the on-device metrics)."""
+    from oracle import torch_port
+    from xsdeepfwfm_deprecated_amd import synth
+    cores = len(os.sched_getaffinity(0))
+    prev = torch.get_num_threads()
+    tp = {k: torch.from_numpy(v) for k, v in params.items()}
+    xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=99)
+    xi, xv = torch.from_numpy(xi), torch.from_numpy(xv)
+    torch.set_num_threads(cores)
+    out_cpu = torch_port.forward(cfg, tp, xi, xv)
+    n, el = _time_port(torch_port, cfg, tp, xi, xv, seconds, cores)
+    n1, el1 = _time_port(torch_port, cfg, tp, xi, xv, seconds, 1)
+    torch.set_num_threads(prev)
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -301,9 +358,26 @@ def cpu_baseline(cfg, params, sizes, seconds, model=None, dev=None):
                 break
     except OSError:
         pass
+    quota = _cpu_quota()
     base = {"value": round(n * BATCH / el, 1), "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"{n} batches x {BATCH} rows of the same Criteo-39 workload, {el:.1f} s, "
-                      f"torch {torch.__version__} CPU, {cores} threads, {cpu}"}
+                      f"torch {torch.__version__} CPU, {cores} threads (every core of the affinity mask"
+                      + (f"; cgroup CPU quota {quota}" if quota else "") + f"), {cpu}",
+            "one_thread": {"value": round(n1 * BATCH / el1, 1), "unit": "samples/s", "cores": 1,
+                           "sample": f"{n1} batches x {BATCH} rows, {el1:.1f} s"}}
+    try:
+        cal = json.load(open(os.path.join(REPO, "profiles", "cpu_calibration.json")))
+        wl = "deepfwfm_lw" if cfg["use_deep"] else "fwfm_lw"
+        ent = [e for e in cal["entries"] if e["workload"] == wl]
+        if ent and not cfg.get("qr_flag") and not cfg.get("use_fwlw"):
+            base["calibration"] = {
+                "what": "port / reference forward time, same batch, measured beside the imported reference in the "
+                        "build container (tools/calibrate_cpu_port.py); logits bit-identical",
+                "host": cal.get("host"), "entries": [{k: e[k] for k in ("threads", "ref_ms_per_batch",
+                                                                       "port_ms_per_batch", "port_over_ref_time")}
+                                                    for e in ent]}
+    except Exception:
+        pass
     parity = None
     if model is not None:
         from xsdeepfwfm_deprecated_amd.metrics import DeviceMetrics

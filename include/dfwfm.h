@@ -200,6 +200,12 @@ int dfwfm_adam_step(const dfwfm_adam_tensor* tensors, int32_t n, double lr, doub
  * read when the kernels run -- so a replayed step draws fresh masks. */
 int dfwfm_set_step_source(dfwfm_model* m, const int64_t* step_dev);
 
+/* The training activations live in model-owned memory that dfwfm_train_forward grows on demand (a
+ * larger batch frees and re-allocates it).  A captured graph bakes those pointers in: the generation
+ * counter changes on every re-allocation, so a caller replaying a graph compares it with the value at
+ * capture time and re-captures when it differs. */
+int dfwfm_workspace_generation(const dfwfm_model* m, int64_t* gen);
+
 /* dfwfm_adam_step with the step counter and bias corrections on the device: increments the counter
  * in `state_dev`, derives the scalars there (double, then f32) and updates every tensor. */
 int dfwfm_adam_step_dev(const dfwfm_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,

@@ -72,6 +72,26 @@ def test_index_out_of_range_raises(gpu, bad):
     run(m, xi[:8], xv[:8], gpu)
 
 
+def test_batched_callers_read_the_index_flag_once(gpu, monkeypatch):
+    """eval_by_batch / predict_proba / run_benchmark do not synchronise on the index flag per batch: one read
+    at the end, which still raises IndexError for a bad row in any batch."""
+    cfg, params, xi, xv, y, *_ = load_golden("deepfwfm_lw")
+    m = make_model(cfg, params, gpu)
+    reads = []
+    orig = m.check_index_errors
+    monkeypatch.setattr(m, "check_index_errors", lambda: (reads.append(1), orig())[1])
+    n = len(xi)
+    m.eval_by_batch(xi, xv, y, n)
+    assert len(reads) == 1
+    m.predict_proba(xi, xv)
+    assert len(reads) == 2
+    bad = xi.copy()
+    bad[n - 1, 2] = -1  # in the last batch
+    with pytest.raises(IndexError):
+        m.eval_by_batch(bad, xv, y, n)
+    m.eval_by_batch(xi, xv, y, n)  # the flag was cleared by the raising read
+
+
 def test_qr_index_range_follows_quotient_table(gpu):
     # QREmbeddingBag rejects only i // c >= ceil(n/c): i = n (inside the last quotient row) is valid
     cfg, params, xi, xv, l32, *_ = load_golden("deepfwfm_qr_mult")[:5]

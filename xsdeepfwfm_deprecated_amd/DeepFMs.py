@@ -19,6 +19,7 @@ Deliberate deviations (documented in DESIGN.md):
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import math
 import os
@@ -92,7 +93,8 @@ class DeepFMs(nn.Module):
         self.qr_threshold = qr_threshold
         self.md_flag = md_flag
         self.md_threshold = md_threshold
-        self.strict_index_check = True  # read the kernel's out-of-range flag after each forward
+        self.strict_index_check = True  # raise IndexError for out-of-range Xi (the kernel's sticky flag)
+        self._defer_index_check = 0     # >0 inside a batched caller: one flag read at its end, not per batch
         self._engine = None
 
         np.random.seed(self.random_seed)
@@ -289,13 +291,29 @@ class DeepFMs(nn.Module):
         from . import torch_ops  # torch.ops.dfwfm.forward (the registered custom op)
         params = [q for q in self.parameters() if q.requires_grad]
         out, _ = torch.ops.dfwfm.forward(torch_ops.register(self), xi, xv, params, False, 0.0, 0)
-        if self.strict_index_check:
-            self.check_index_errors()
+        if self.strict_index_check and not self._defer_index_check:
+            self.check_index_errors()  # reads a device word: synchronises the stream
         return out
 
     def check_index_errors(self):
         if self._engine is not None and self._engine.read_error_flag() & FLAG_INDEX_OUT_OF_RANGE:
             raise IndexError("index out of range in self (an Xi entry is outside its field's table)")
+
+    @contextlib.contextmanager
+    def deferred_index_check(self):
+        """Forwards inside the block do not read the out-of-range flag (a host synchronisation per batch);
+        it is read once when the block ends and raises IndexError there if any forward saw a bad index --
+        the reference raises from the first offending nn.Embedding call (model/DeepFMs.py:334), so a batched
+        caller (eval_by_batch, predict, run_benchmark) fails the same way, after its forwards ran."""
+        self._defer_index_check = getattr(self, "_defer_index_check", 0) + 1
+        ok = False
+        try:
+            yield
+            ok = True
+        finally:
+            self._defer_index_check -= 1
+            if ok and self.strict_index_check and not self._defer_index_check:
+                self.check_index_errors()
 
     # ------------------------------------------------------------ init/train
     def init_weights(self):
@@ -337,7 +355,7 @@ class DeepFMs(nn.Module):
         """Logits for every row, batch by batch; inputs go to the device once per batch."""
         n = Xi.shape[0]
         out = []
-        with torch.no_grad():
+        with torch.no_grad(), self.deferred_index_check():
             for off in range(0, n, batch_size):
                 out.append(self(Xi[off:off + batch_size], Xv[off:off + batch_size]))
         return torch.cat(out) if out else torch.empty(0, device=self._device())
@@ -355,7 +373,7 @@ class DeepFMs(nn.Module):
         bs = 8192
         logits = torch.empty(x_size, dtype=torch.float32, device=dev)
         total_loss = torch.zeros((), dtype=torch.float64, device=dev)
-        with torch.no_grad():
+        with torch.no_grad(), self.deferred_index_check():
             for off in range(0, x_size, bs):
                 end = min(x_size, off + bs)
                 out = self(Xi_d[off:end], Xv_d[off:end])
@@ -413,16 +431,18 @@ class DeepFMs(nn.Module):
         Xi = torch.as_tensor(self._fit_layout(Xi))
         Xv = torch.as_tensor(np.asarray(Xv), dtype=torch.float32)
         self.eval()
-        with torch.no_grad():
-            return torch.sigmoid(self(Xi, Xv)).cpu().numpy()
+        with torch.no_grad(), self.deferred_index_check():
+            p = torch.sigmoid(self(Xi, Xv))
+        return p.cpu().numpy()
 
     def inner_predict(self, Xi, Xv):
         return self.inner_predict_proba(Xi, Xv) > 0.5
 
     def inner_predict_proba(self, Xi, Xv):
         self.eval()
-        with torch.no_grad():
-            return torch.sigmoid(self(Xi, Xv)).cpu().numpy()
+        with torch.no_grad(), self.deferred_index_check():
+            p = torch.sigmoid(self(Xi, Xv))
+        return p.cpu().numpy()
 
     def evaluate(self, Xi, Xv, y):
         return self.eval_metric(y.cpu().numpy(), self.inner_predict_proba(Xi, Xv))
@@ -476,8 +496,8 @@ class DeepFMs(nn.Module):
         self.logger.info("\tPRAUC: " + str(prauc))
         self.logger.info("\tRCE: " + str(rce))
         self.eval()
-        strict, self.strict_index_check = self.strict_index_check, False
-        try:
+        # the timed forwards never synchronise on the index flag: it is read once, after the timing loops
+        with self.deferred_index_check():
             spent = []
             for off in range(0, (x_size // batch_size) * batch_size, batch_size):
                 spent.append(self.time_forward_pass(self, torch.as_tensor(Xi[off:off + batch_size]),
@@ -491,8 +511,6 @@ class DeepFMs(nn.Module):
                       for i in range(min(1000, x_size))]
             if single:
                 self.logger.info("\tAvg forward pass time (ms):\t{:.3f}".format(np.mean(single)))
-        finally:
-            self.strict_index_check = strict
         return loss, total_metric, prauc, rce
 
     def fetch_teacher_outputs(self, teacher_model, Xi, Xv, x_size):

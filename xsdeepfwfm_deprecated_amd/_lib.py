@@ -98,6 +98,7 @@ SIGNATURES = {
                                        ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int64, _P]),
     "dfwfm_set_step_source": (ctypes.c_int, [_P, _P]),
+    "dfwfm_workspace_generation": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "dfwfm_adam_step_dev": (ctypes.c_int, [ctypes.POINTER(dfwfm_adam_tensor), ctypes.c_int32, ctypes.c_double,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                            _P, _P]),

@@ -56,8 +56,10 @@ def get_parser():
     a("-quantization_aware", default=0, type=int, help="Quantization Aware Training")
     a("-kd", default=0, type=int, help="Perform knowledge distillation")
     a("-loss_type", default="logloss", type=str, help="Used loss (should be logloss but for kd we need softmax)")
-    a("-emb_bag", default=0, type=int, help="Use embedding bag")
-    a("-qr_emb", default=0, type=int, help="Use QR Embeddings")
+    # the README's spellings (-embedding_bag / -qr_flag, reference README.md:107,117) are rejected by the
+    # reference parser (probe P5); both spellings are accepted here, same destination
+    a("-emb_bag", "-embedding_bag", dest="emb_bag", default=0, type=int, help="Use embedding bag")
+    a("-qr_emb", "-qr_flag", dest="qr_emb", default=0, type=int, help="Use QR Embeddings")
     a("-qr_operation", default="mult", type=str)
     a("-qr_collisions", default=4, type=int)
     a("-qr_threshold", default=200, type=int)

@@ -48,6 +48,7 @@ struct dfwfm_model {
   float* d_rsk;        // symmetric off-diagonal (R+R^T)/2 fragments
   float* d_ws;         // activation workspace (E, fo, X_0..X_H, G_1..G_H)
   int64_t ws_batch;
+  int64_t ws_gen;      // bumped on every (re)allocation of d_ws (graphs that baked its pointers are stale)
   float* sv_e;
   float* sv_fo;
   float* sv_x[kMaxH + 1];
@@ -436,6 +437,7 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
     }
   }
   m->ws_batch = batch;
+  m->ws_gen++;
   return DFWFM_OK;
 }
 
@@ -829,6 +831,12 @@ int dfwfm_adam_step(const dfwfm_adam_tensor* t, int32_t n, double lr, double bet
     blocks += nb;
   }
   return flush();
+}
+
+int dfwfm_workspace_generation(const dfwfm_model* m, int64_t* gen) {
+  if (!m || !gen) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  *gen = m->ws_gen;
+  return DFWFM_OK;
 }
 
 int dfwfm_set_step_source(dfwfm_model* m, const int64_t* step_dev) {

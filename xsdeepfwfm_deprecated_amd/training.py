@@ -189,12 +189,29 @@ class FusedTrainStep:
         self.seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
         _lib.check(self.L.dfwfm_set_step_source(self.eng.handle, ctypes.c_void_p(self.state.data_ptr())),
                    "dfwfm_set_step_source")
+        self._attached = True
         self.graphs = None
         self.steps = 0
 
     def close(self):
-        if self.eng.handle is not None and self.eng.handle.value:
-            self.L.dfwfm_set_step_source(self.eng.handle, None)
+        """Detach the engine from this step's device counter (the engine outlives the trainer: a later
+        train forward must not read the freed counter).  Idempotent; also run by __del__."""
+        eng = getattr(self, "eng", None)
+        if eng is not None and eng.handle is not None and eng.handle.value and getattr(self, "_attached", False):
+            self.L.dfwfm_set_step_source(eng.handle, None)
+        self._attached = False
+        self.graphs = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ws_generation(self):
+        g = ctypes.c_int64(0)
+        _lib.check(self.L.dfwfm_workspace_generation(self.eng.handle, ctypes.byref(g)), "dfwfm_workspace_generation")
+        return int(g.value)
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
@@ -279,10 +296,16 @@ class FusedTrainStep:
             self.y[:n].copy_(y)
         self.drop = self.drop_train if self.model.training else 0.0  # nn.Dropout is off in eval mode
         full = n == self.B
+        if not self._attached:
+            raise RuntimeError("FusedTrainStep.step after close()")
         if self.use_graph and full and self.steps >= 1:
-            if self.graphs is None or self._graph_key != (denom, self.drop):
+            # the graphs bake in the engine's activation workspace: a train forward at a larger batch
+            # elsewhere (e.g. autograd) re-allocates it, and then the graphs are re-captured
+            key = (denom, self.drop, self._ws_generation())
+            if self.graphs is None or self._graph_key != key:
+                self.graphs = None
                 self.graphs = self._capture(denom)
-                self._graph_key = (denom, self.drop)
+                self._graph_key = (denom, self.drop, self._ws_generation())
             g1, g1b, g2 = self.graphs
             g1.replay()
             self._exchange(lambda: g1b.replay() if g1b is not None else None)
@@ -296,6 +319,7 @@ class FusedTrainStep:
         return self.loss_sum
 
     _graph_key = None
+    _attached = False
 
 
 # --------------------------------------------------------------------------------------- pruning
@@ -459,7 +483,6 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
         Xi_valid = np.asarray(Xi_valid).reshape((-1, ncat, 1))
         Xv_valid = np.asarray(Xv_valid)
         y_valid = np.asarray(y_valid)
-        x_valid_size = Xi_valid.shape[0]
 
     log.info("init_weights")
     model.init_weights()
@@ -467,6 +490,11 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
         for p in model.parameters():
             dist.broadcast(p.data, 0)
     model.train()
+    if teacher_model and dist:
+        # loss_fn_kd softmaxes over the batch dimension (dim=0, reference :1060-1061): the loss couples
+        # every sample of the batch, so a rank's shard cannot form its share of the gradient
+        raise NotImplementedError("knowledge distillation under data parallelism: the KD loss is a softmax over "
+                                  "the whole batch (model/DeepFMs.py:1060-1061) and does not split over ranks")
     # Adam without distillation (the reference default) runs as a graph-replayed fused step;
     # other optimizers / the KD loss go through autograd + the optimizer
     fused = model.optimizer_type == "adam" and not teacher_model and getattr(model, "fused_fit", True)
@@ -474,6 +502,25 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
     gbs = bs * world
     trainer = FusedTrainStep(model, bs, lr=model.learning_rate, weight_decay=model.weight_decay,
                              dist=dist) if fused else None
+    try:
+        return _fit_loop(model, trainer, dist, rank, world, Xi_train, Xv_train, y_train, x_size, ncat, is_valid,
+                         Xi_valid if is_valid else None, Xv_valid if is_valid else None,
+                         y_valid if is_valid else None, early_stopping, save_path, prune, prune_fm, prune_r,
+                         prune_deep, emb_r, emb_corr, teacher_model)
+    finally:
+        if trainer is not None:
+            trainer.close()
+
+
+def _fit_loop(model, trainer, dist, rank, world, Xi_train, Xv_train, y_train, x_size, ncat, is_valid, Xi_valid,
+              Xv_valid, y_valid, early_stopping, save_path, prune, prune_fm, prune_r, prune_deep, emb_r, emb_corr,
+              teacher_model):
+    log = model.logger
+    device = model._device()
+    fused = trainer is not None
+    bs = model.batch_size
+    gbs = bs * world
+    x_valid_size = Xi_valid.shape[0] if is_valid else 0
     optimizer = None if fused else make_optimizer(model)
     num_total, e1, e2, dnn, nz_r = _param_summary(model, log)
     log.info("========")
@@ -497,7 +544,9 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
     n_iter = 0
     for epoch in range(model.n_epochs):
         total_loss = 0.0
-        loss_mark = float(trainer.loss_sum.item()) if fused else 0.0
+        win_rows = 0  # rows this rank trained on since the last log line (fused: the device loss sum's window)
+        if fused:
+            trainer.loss_sum.zero_()
         batch_iter = x_size // gbs
         epoch_begin = batch_begin = time()
         teacher_outputs = None
@@ -517,8 +566,11 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
             hi = min(end, lo + bs)
             n_global = end - offset
             xi, xv, yb = Xi_d[lo:hi], Xv_d[lo:hi], y_d[lo:hi]
+            win_rows += hi - lo
             if fused:
                 trainer.step(xi, xv, yb, n_global if dist else None)
+                if epoch == 0 and i == 0:
+                    model.check_index_errors()  # an out-of-range Xi raises IndexError as nn.Embedding does
             else:
                 optimizer.zero_grad()
                 if hi > lo:
@@ -540,9 +592,12 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
                 if model.verbose:
                     total_loss += loss.item()
             if model.verbose and i % 100 == 99:
-                if fused:  # mean per-batch loss over the last 100 steps, from the device loss sum
-                    cur = float(trainer.loss_sum.item())
-                    total_loss, loss_mark = (cur - loss_mark) / max(hi - lo, 1), cur
+                if fused:
+                    # the window's summed per-sample BCE -> 100 x its mean (the reference prints total / 100 of
+                    # 100 batch means); the device sum restarts every window, so it never grows large in f32
+                    total_loss = float(trainer.loss_sum.item()) * 100.0 / max(win_rows, 1)
+                    trainer.loss_sum.zero_()
+                win_rows = 0
                 # (the reference's evaluate() leaves the model in eval mode -- dropout off -- for the
                 # rest of training, :627-630, :880-893; kept as is)
                 ev = model.evaluate(xi, xv, yb) if hi > lo else float("nan")
@@ -554,6 +609,7 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
                 model.adaptive_sparse = model.target_sparse * (1 - 0.99 ** (n_iter / 100.))
                 prune_step(model, model.adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb_corr)
 
+        model.check_index_errors()  # once per epoch: the sticky flag of every training forward since the last read
         no_non_sparse = sum(int((p != 0).sum().item()) for p in model.parameters())
         log.info("Model parameters %d, sparse rate %.2f%%" % (no_non_sparse, 100 - no_non_sparse * 100. / num_total))
         train_loss, train_eval, train_prauc, train_rce = model.eval_by_batch(Xi_train, Xv_train, y_train, x_size)
