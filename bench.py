@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -340,7 +341,11 @@ def cpu_baseline(cfg, params, sizes, seconds, model=None, dev=None):
     sigmoid, AUC of both score vectors by the on-device metrics)."""
     from oracle import torch_port
     from xsdeepfwfm_deprecated_amd import synth
-    cores = len(os.sched_getaffinity(0))
+    # every core this process may use: the affinity mask, capped by the cgroup CPU quota (the GPU box's
+    # share is 16 CPUs of a 256-core affinity mask; 256 threads under that quota ran ~100x slower, r02a)
+    aff = len(os.sched_getaffinity(0))
+    quota = _cpu_quota()
+    cores = max(1, min(aff, int(math.ceil(quota)))) if quota else aff
     prev = torch.get_num_threads()
     tp = {k: torch.from_numpy(v) for k, v in params.items()}
     xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=99)
@@ -358,11 +363,10 @@ def cpu_baseline(cfg, params, sizes, seconds, model=None, dev=None):
                 break
     except OSError:
         pass
-    quota = _cpu_quota()
     base = {"value": round(n * BATCH / el, 1), "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"{n} batches x {BATCH} rows of the same Criteo-39 workload, {el:.1f} s, "
-                      f"torch {torch.__version__} CPU, {cores} threads (every core of the affinity mask"
-                      + (f"; cgroup CPU quota {quota}" if quota else "") + f"), {cpu}",
+                      f"torch {torch.__version__} CPU, {cores} threads (affinity mask {aff} cores"
+                      + (f", cgroup CPU quota {quota}" if quota else "") + f"), {cpu}",
             "one_thread": {"value": round(n1 * BATCH / el1, 1), "unit": "samples/s", "cores": 1,
                            "sample": f"{n1} batches x {BATCH} rows, {el1:.1f} s"}}
     try:

@@ -20,7 +20,15 @@ STEPS=${STEPS:-"smoke pytest bench prof"}
 for s in $STEPS; do
   case $s in
     smoke)  step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    pytestk) step pytest_k 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${PYTEST_K}" ;;
+    bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
+    benchfwfm) step benchfwfm 300 python bench.py --config fwfm --steps 400 --warmup 40 --no-cpu-baseline ;;
+    benchfwfm20) step benchfwfm20 300 python bench.py --config fwfm --steps 20 --warmup 5 ;;
+    benchpruned) step benchpruned 300 python bench.py --config pruned --steps 400 --warmup 40 --no-cpu-baseline ;;
+    benchtrain) step benchtrain 300 python tools/bench_train.py ;;
+    proffwfm) step proffwfm 400 rocprofv3 --kernel-trace --stats -d gpurun_out/proffwfm_$TAG -o run --output-format csv -- python3 bench.py --config fwfm --no-cpu-baseline --steps 400 --warmup 40 ;;
+    proftrain) step proftrain 400 rocprofv3 --kernel-trace --stats -d gpurun_out/proftrain_$TAG -o run --output-format csv -- python3 tools/bench_train.py ;;
     bench)  step bench 400 python bench.py ;;
     bench_fwlw) step bench_fwlw 300 python bench.py --steps 200 --warmup 20 --first-order fwlw --no-cpu-baseline ;;
     prof)   step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
