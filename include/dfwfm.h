@@ -217,6 +217,44 @@ int dfwfm_adam_step_dev(const dfwfm_adam_tensor* tensors, int32_t n, double lr, 
 int dfwfm_bce_grad(const float* logits, const float* labels, int64_t n, double denom, float* dlogit,
                    float* loss_sum, void* stream);
 
+/* ---- touched-row gradients of the categorical tables (data-parallel exchange) --------------------
+ * The reference's tables have dense gradients (nn.Embedding(sparse=False), model/DeepFMs.py:199-210) and
+ * its Adam applies coupled L2 to every row (:553-556), so the data-parallel form of its step all-reduces
+ * every table.  Only the rows a batch touched carry a data gradient: each rank builds the list of
+ * (destination, summed gradient row) of the rows its batch touched, the ranks exchange the lists, every rank
+ * adds all lists into its own dense gradient buffer (rank 0's first, then rank 1's, ...) and runs the dense
+ * L2 + Adam step.  The lists are deterministic (stable sort, fixed-order sums, no atomics), so the replicas
+ * stay bit-identical.
+ *
+ * A family is the second-order tables (fm_2nd_embeddings, rows of width D) or the first-order tables
+ * (fm_1st_embeddings, width 1) of the categorical fields.  dest[f] (host array of field_size entries) holds
+ * the float offset, in the caller's flat gradient buffer, of field f's plain / quotient table gradient (q)
+ * and of its QR remainder table gradient (r); -1 leaves a table out (numerical fields are never listed: the
+ * backward's reductions form their gradients).  The backward must have run with DFWFM_BWD_TABLES for the
+ * last dfwfm_train_forward, with the categorical fields' gradient pointers NULL (no dense scatter); dlogit is
+ * the one that backward got. */
+#define DFWFM_FAMILY_SECOND 0
+#define DFWFM_FAMILY_FIRST 1
+typedef struct {
+  int64_t q;
+  int64_t r;
+} dfwfm_sparse_dest;
+
+/* Entries a batch of `batch` rows can produce (capacity = tables x batch), their row width and the device
+ * workspace dfwfm_sparse_grads needs. */
+int dfwfm_sparse_grads_size(dfwfm_model* m, int32_t family, int64_t batch, int64_t* capacity, int32_t* width,
+                            int64_t* ws_bytes);
+/* The list of the last training step: out_dest[e] (device int64) = float offset of entry e's row in the flat
+ * buffer, out_rows[e * width ...] its summed gradient, *out_count (device int32) the number of entries; sorted
+ * by (table, row), destinations unique.  Stream-ordered, no host synchronisation (graph-capturable). */
+int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, const dfwfm_sparse_dest* dest,
+                       int64_t capacity, int64_t* out_dest, float* out_rows, int32_t* out_count, void* ws,
+                       int64_t ws_bytes, void* stream);
+/* grad[dest[e] + j] += rows[e * width + j] for e < *count (one list; lists with shared destinations must be
+ * applied one after the other, in a fixed order, for bit-identical results). */
+int dfwfm_sparse_grads_apply(float* grad, int32_t width, const int64_t* dest, const float* rows, const int32_t* count,
+                             int64_t capacity, void* stream);
+
 /* ---- magnitude pruning (reference model/DeepFMs.py:647-673, binary_search_threshold :807-823) ----
  * The threshold whose fraction of |x| < threshold (compared in f32) hits `target`, found by the
  * reference's own bisection on (0, 100) -- same rounds, same result -- but from one radix sort of the

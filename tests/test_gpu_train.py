@@ -497,3 +497,199 @@ def _kd_dp_worker(rank, world, port, q):
             q.put((rank, "NotImplementedError"))
     finally:
         dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------------------
+# touched-row (sparse) gradients of the categorical tables: the data-parallel exchange
+def _sparse_setup(m, gpu):
+    """FusedTrainStep-free driver of the C ABI: train forward + DFWFM_BWD_TABLES backward with the categorical
+    fields' grads NULL, then dfwfm_sparse_grads for both families into per-table dense buffers."""
+    import ctypes
+    from xsdeepfwfm_deprecated_amd import _lib
+    fields, dense = m._param_layout()
+    params = [p for p in m.parameters() if p.requires_grad]
+    flat = torch.zeros(sum(p.numel() for p in params), device=gpu)
+    views, off = {}, 0
+    for p in params:
+        views[id(p)] = (off, flat[off:off + p.numel()].view_as(p))
+        off += p.numel()
+    return fields, views, flat, _lib, ctypes
+
+
+def _sparse_step(m, gpu, xi, xv, y, sparse):
+    """One backward of m on (xi, xv, y): dense scatter (sparse=False) or touched-row lists applied to a zero
+    buffer (sparse=True).  Returns {param name: grad}, the lists (for sparse) and the flat buffer."""
+    fields, views, flat, _lib, ctypes = _sparse_setup(m, gpu)
+    L, eng = _lib.lib(), m._sync_engine(gpu)
+    st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+    xi_d, xv_d, y_d = (torch.from_numpy(a).to(gpu) for a in (xi.reshape(len(xi), -1), xv, y))
+    out = torch.empty(len(xi), device=gpu)
+    eng.train_forward(xi_d, xv_d, out, 0.0, 0)
+    dl = torch.empty(len(xi), device=gpu)
+    _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(y_d.data_ptr()), len(xi),
+                                float(len(xi)), ctypes.c_void_p(dl.data_ptr()), None, st), "bce")
+    ptr = lambda t, f: None if (t is None or (sparse and f >= m.num)) else views[id(t)][1].data_ptr()  # noqa
+    fg = (_lib.dfwfm_field_grads * len(fields))(*[_lib.dfwfm_field_grads(*[ptr(t, f) for t in tup])
+                                                  for f, tup in enumerate(fields)])
+    H = len(dense["lin_w"])
+    gW = (ctypes.c_void_p * max(H, 1))(*[views[id(t)][1].data_ptr() for t in dense["lin_w"]])
+    gB = (ctypes.c_void_p * max(H, 1))(*[views[id(t)][1].data_ptr() for t in dense["lin_b"]])
+    dp = lambda k: None if dense[k] is None else views[id(dense[k])][1].data_ptr()  # noqa
+    grads = _lib.dfwfm_grads(fg, dp("field_cov"), dp("fwfm_lin"), dp("fm_1st"), dp("bias"), gW if H else None,
+                             gB if H else None, dp("fc_w"))
+    _lib.check(L.dfwfm_backward(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), st), "bwd")
+    lists = []
+    if sparse:
+        for fam, (iq, ir) in ((0, (0, 1)), (1, (2, 3))):
+            o = lambda t: -1 if t is None else views[id(t)][0]  # noqa
+            dest = (_lib.dfwfm_sparse_dest * len(fields))(
+                *[_lib.dfwfm_sparse_dest(o(tup[iq]) if f >= m.num else -1, o(tup[ir]) if f >= m.num else -1)
+                  for f, tup in enumerate(fields)])
+            cap, w, wsb = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int64(0)
+            _lib.check(L.dfwfm_sparse_grads_size(eng.handle, fam, len(xi), ctypes.byref(cap), ctypes.byref(w),
+                                                 ctypes.byref(wsb)), "size")
+            if cap.value == 0:
+                continue
+            ws = torch.empty(wsb.value, dtype=torch.uint8, device=gpu)
+            od = torch.full((cap.value,), -7, dtype=torch.int64, device=gpu)
+            orow = torch.zeros(cap.value * w.value, device=gpu)
+            cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+            _lib.check(L.dfwfm_sparse_grads(eng.handle, fam, ctypes.c_void_p(dl.data_ptr()), dest, cap.value,
+                                            ctypes.c_void_p(od.data_ptr()), ctypes.c_void_p(orow.data_ptr()),
+                                            ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                            wsb.value, st), "sparse")
+            _lib.check(L.dfwfm_sparse_grads_apply(ctypes.c_void_p(flat.data_ptr()), w.value,
+                                                  ctypes.c_void_p(od.data_ptr()), ctypes.c_void_p(orow.data_ptr()),
+                                                  ctypes.c_void_p(cnt.data_ptr()), cap.value, st), "apply")
+            lists.append((fam, w.value, od, orow, cnt))
+    torch.cuda.synchronize()
+    names = {id(p): k for k, p in m.named_parameters()}
+    g = {names[i]: v.detach().cpu().numpy().copy() for i, (o, v) in views.items()}
+    return g, lists, out.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult", "train_deepfwfm_fwlw", "train_fwfm_nolw"])
+def test_sparse_row_lists_equal_dense_table_grads(gpu, name):
+    """dfwfm_sparse_grads + apply give the categorical tables' dense gradients (to fp32 reassociation: the
+    dense scatter adds atomically in any order), the lists are sorted, unique and exactly the touched rows,
+    and two runs give the same bits (fixed-order sums, no atomics)."""
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    gd, _, out_d = _sparse_step(m, gpu, xi, xv, y, sparse=False)
+    gs, lists, out_s = _sparse_step(m, gpu, xi, xv, y, sparse=True)
+    gs2, lists2, _ = _sparse_step(m, gpu, xi, xv, y, sparse=True)
+    assert np.array_equal(out_d, out_s)
+    for k in gd:
+        sc = np.abs(gd[k]).max()
+        assert np.abs(gs[k] - gd[k]).max() <= G_TOL * sc + 1e-12, k
+        assert np.array_equal(gs[k], gs2[k]), k  # deterministic
+    assert lists, "no list produced"
+    ncat = cfg["field_size"] - cfg["numerical"]
+    for (fam, w, od, orow, cnt), (_, _, od2, orow2, cnt2) in zip(lists, lists2):
+        n = int(cnt.item())
+        d = od[:n].cpu().numpy()
+        assert n > 0 and np.all(np.diff(d) > 0), "destinations ascending and unique"
+        assert np.array_equal(d, od2[:n].cpu().numpy()) and torch.equal(orow[:n * w], orow2[:n * w])
+        assert n <= len(xi) * ncat * 2
+
+
+def test_sparse_rows_hot_rows_cross_blocks(gpu):
+    """A field where every sample hits one of 3 rows (segments of ~B/3 positions, across many 64-position
+    blocks) and one with all-distinct rows: the carried block partials are summed right."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = [1] * 13 + [3] + [5000] * 25
+    B = 3000
+    xi, xv = synth.synth_inputs(sizes, 13, B, seed=4)
+    xi[:, 1] = np.arange(B)  # field 14: every sample its own row
+    y = (np.arange(B) % 2).astype(np.float32)
+    m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1, h_depth=1,
+                deep_nodes=32, is_deep_dropout=False).to(gpu).train()
+    m.init_weights()
+    gd, _, _ = _sparse_step(m, gpu, xi, xv, y, sparse=False)
+    gs, lists, _ = _sparse_step(m, gpu, xi, xv, y, sparse=True)
+    for k in gd:
+        sc = np.abs(gd[k]).max()
+        assert np.abs(gs[k] - gd[k]).max() <= G_TOL * sc + 1e-12, k
+    fam0 = lists[0]
+    assert fam0[0] == 0 and int(fam0[4].item()) == sum(len(np.unique(xi[:, j])) for j in range(26))
+
+
+def _dp_step_worker(rank, world, port, q, name, sparse, steps):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _dp_steps(name, sparse, steps, dist, rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _dp_steps(name, sparse, steps, dist, rank, world):
+    """`steps` FusedTrainSteps on the global batches of train golden `name` (64 rows each), this rank taking
+    its contiguous share; returns first-step grads / logits and the final parameters."""
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    dev = torch.device("cuda:0")
+    G = 64
+    bs = G // world
+    m = build(cfg, params, dev, is_deep_dropout=False)
+    t = FusedTrainStep(m, bs, lr=1e-3, weight_decay=3e-7, dist=dist, sparse_exchange=sparse)
+    first = None
+    for k in range(steps):
+        lo = k * G + rank * bs
+        xb, vb, yb = (torch.from_numpy(a[lo:lo + bs]).to(dev) for a in (xi, xv, y))
+        t.step(xb, vb, yb, G if dist is not None else None)
+        if k == 0:
+            torch.cuda.synchronize()
+            first = ({n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters()},
+                     t.out[:bs].detach().cpu().numpy().copy())
+    torch.cuda.synchronize()
+    t.close()
+    return first, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}
+
+
+def _run_dp(name, sparse, steps, world=2):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_step_worker, args=(r, world, port, q, name, sparse, steps)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult"])
+def test_data_parallel_step_equals_single_process_global_batch(gpu, name):
+    """configs[4] semantics, tight: two gloo ranks (both on cuda:0), each with half of every
+    64-row global batch, through FusedTrainStep with the touched-row exchange.  After step 1 every gradient
+    equals one process's on the whole batch to 2e-5 of the tensor's largest entry and the ranks' logits equal
+    its rows to 1e-5 * max(1, |ref|); the two replicas' gradients and, after 3 steps, parameters are
+    bit-identical; the dense all-reduce exchange gives the same gradients to fp32 reassociation."""
+    steps = 3
+    res = _run_dp(name, True, steps)
+    (g0, o0), p0 = res[0]
+    (g1, o1), p1 = res[1]
+    for k in g0:
+        assert np.array_equal(g0[k], g1[k]), k
+        assert np.array_equal(p0[k], p1[k]), k
+    (gs, os_), ps = _dp_steps(name, True, steps, None, 0, 1)  # one process, global batch (no exchange)
+    assert logit_close(np.concatenate([o0, o1]), os_) < 1e-5
+    for k in gs:
+        sc = np.abs(gs[k]).max()
+        assert np.abs(g0[k] - gs[k]).max() <= G_TOL * sc + 1e-12, k
+    e = np.concatenate([np.abs(p0[k] - ps[k]).reshape(-1) / 1e-3 for k in ps])
+    assert np.median(e) < 1e-4 and np.quantile(e, 0.999) < 0.02, (np.median(e), np.quantile(e, 0.999))
+    resd = _run_dp(name, False, 1)  # dense exchange (all-reduce of the whole buffer)
+    (gd, od), _ = resd[0]
+    for k in gs:
+        sc = np.abs(gs[k]).max()
+        assert np.abs(gd[k] - g0[k]).max() <= G_TOL * sc + 1e-12, k

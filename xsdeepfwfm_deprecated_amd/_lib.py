@@ -23,7 +23,8 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
 # A/B of build variants only (e.g. libdfwfm_ns4.so built with DFWFM_HIPCC_FLAGS=-DDFWFM_NSETS=4)
 LOAD_PATH = os.path.join(PKG_DIR, os.environ["DFWFM_LIB"]) if os.environ.get("DFWFM_LIB") else LIB_PATH
-SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_capi.hip"]
+SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_sparse.hip",
+           "dfwfm_capi.hip"]
 HEADERS = ["dfwfm_internal.h", "dfwfm_device.h", os.path.join("..", "..", "include", "dfwfm.h")]
 ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
 INGEST_PATH = os.path.join(PKG_DIR, "libdfwfm_ingest.so")
@@ -34,6 +35,7 @@ DFWFM_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported", -3: "HIP error", -4: "bad state"}
 FLAG_INDEX_OUT_OF_RANGE = 1
 BWD_TABLES, BWD_MLP_WEIGHTS = 1, 2  # dfwfm_backward_phases
+FAMILY_SECOND, FAMILY_FIRST = 0, 1  # dfwfm_sparse_grads
 ADAM_STATE_BYTES = 48
 
 
@@ -74,6 +76,10 @@ class dfwfm_adam_tensor(ctypes.Structure):
                 ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64)]
 
 
+class dfwfm_sparse_dest(ctypes.Structure):
+    _fields_ = [("q", ctypes.c_int64), ("r", ctypes.c_int64)]
+
+
 class dfwfm_prune_source(ctypes.Structure):
     _fields_ = [("values", ctypes.c_void_p), ("numel", ctypes.c_int64), ("sym_f", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
@@ -103,6 +109,11 @@ SIGNATURES = {
                                            ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                            _P, _P]),
     "dfwfm_bce_grad": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_double, _P, _P, _P]),
+    "dfwfm_sparse_grads_size": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]),
+    "dfwfm_sparse_grads": (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.POINTER(dfwfm_sparse_dest), ctypes.c_int64,
+                                          _P, _P, _P, _P, ctypes.c_int64, _P]),
+    "dfwfm_sparse_grads_apply": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, _P, ctypes.c_int64, _P]),
     "dfwfm_prune_workspace_bytes": (ctypes.c_int64, [ctypes.c_int64]),
     "dfwfm_prune_threshold": (ctypes.c_int, [ctypes.POINTER(dfwfm_prune_source), ctypes.c_int32, ctypes.c_double,
                                              _P, _P, ctypes.c_int64, _P]),

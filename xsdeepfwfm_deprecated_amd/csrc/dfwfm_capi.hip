@@ -67,6 +67,7 @@ struct dfwfm_model {
   uint32_t t_seed;
   const int64_t* step_src;  // dfwfm_set_step_source
   bool trained;
+  bool bwd_tables;  // the per-tile backward (sv_de) ran for the last dfwfm_train_forward
   bool tables_set;
   bool dense_set;
 };
@@ -526,6 +527,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
                         int64_t batch, float* out, float dropout_p, uint32_t seed, void* stream) {
   if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
   m->trained = false;
+  m->bwd_tables = false;
   int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
   if (rc != DFWFM_OK) return rc;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(DFWFM_ERR_INVALID_ARG, "dropout_p outside [0, 1)");
@@ -626,6 +628,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     const int tpw = ng8 ? (NT % 8 == 1 && NT >= 9 ? NT / 8 : (NT + 7) / 8) : (m->TPW > 0 ? m->TPW : 1);
     e = launch_backward(a, D, tpw > 0 ? tpw : 1, ng8 ? 8 : 4, lds, s);
     if (e != hipSuccess) return hip_fail(e, "backward launch");
+    m->bwd_tables = true;
   }
 
   // 2. dense shallow reductions: per 16-row tile, then summed over tiles
@@ -831,6 +834,100 @@ int dfwfm_adam_step(const dfwfm_adam_tensor* t, int32_t n, double lr, double bet
     blocks += nb;
   }
   return flush();
+}
+
+}  // extern "C"
+
+namespace {
+
+// the sparse-gradient tasks of one table family: per categorical field its plain / quotient table, then its
+// remainder table (QR); dest == NULL lists every table (capacity), else only those with an offset >= 0
+int sparse_tasks(const dfwfm_model* m, int family, const dfwfm_sparse_dest* dest, SparseArgs* a) {
+  int n = 0;
+  const bool has = family == DFWFM_FAMILY_SECOND ? (m->flags & kNeedE) != 0 : (m->flags & kFoTables) != 0;
+  if (!has) return 0;
+  for (int f = m->num; f < m->F; ++f) {
+    const FieldDev& fd = m->h_fields[f];
+    const float* tq = family == DFWFM_FAMILY_SECOND ? fd.emb2 : fd.emb1;
+    const float* tr = family == DFWFM_FAMILY_SECOND ? fd.emb2_r : fd.emb1_r;
+    for (int part = 0; part < (fd.c > 0 ? 2 : 1); ++part) {
+      const int64_t off = dest ? (part == 0 ? dest[f].q : dest[f].r) : 0;
+      if (off < 0) continue;
+      if (a) {
+        SparseTask& t = a->t[n];
+        t.dest = off;
+        t.field = (int16_t)f;
+        t.c = (int32_t)fd.c;
+        t.kind = (int8_t)(fd.c == 0 ? 0 : 1 + part);
+        t.other = (fd.c > 0 && fd.op == 0) ? (part == 0 ? tr : tq) : nullptr;
+      }
+      ++n;
+    }
+  }
+  return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfwfm_sparse_grads_size(dfwfm_model* m, int32_t family, int64_t batch, int64_t* capacity, int32_t* width,
+                            int64_t* ws_bytes) {
+  if (!m || !capacity || !width || !ws_bytes || batch < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (family != DFWFM_FAMILY_SECOND && family != DFWFM_FAMILY_FIRST) return fail(DFWFM_ERR_INVALID_ARG, "bad family");
+  if (!m->tables_set) return fail(DFWFM_ERR_STATE, "set_tables must precede dfwfm_sparse_grads_size");
+  const int nt = sparse_tasks(m, family, nullptr, nullptr);
+  *width = family == DFWFM_FAMILY_SECOND ? m->D : 1;
+  *capacity = (int64_t)nt * batch;
+  if (*capacity > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "more than 2^31 (table, sample) pairs");
+  *ws_bytes = nt ? (int64_t)sparse_workspace_bytes(*capacity, *width, nt) : 0;
+  return DFWFM_OK;
+}
+
+int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, const dfwfm_sparse_dest* dest,
+                       int64_t capacity, int64_t* out_dest, float* out_rows, int32_t* out_count, void* ws,
+                       int64_t ws_bytes, void* stream) {
+  if (!m || !dest || !out_count) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (family != DFWFM_FAMILY_SECOND && family != DFWFM_FAMILY_FIRST) return fail(DFWFM_ERR_INVALID_ARG, "bad family");
+  if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_sparse_grads needs a preceding dfwfm_train_forward");
+  if (family == DFWFM_FAMILY_SECOND && m->t_batch > 0 && !m->bwd_tables)
+    return fail(DFWFM_ERR_STATE, "dfwfm_sparse_grads (second-order tables) needs the DFWFM_BWD_TABLES backward");
+  SparseArgs a;
+  memset(&a, 0, sizeof a);
+  a.ntasks = sparse_tasks(m, family, dest, &a);
+  a.D = m->D;
+  a.F = m->F;
+  a.num = m->num;
+  a.w = family == DFWFM_FAMILY_SECOND ? m->D : 1;
+  a.src = family == DFWFM_FAMILY_SECOND ? 0 : 1;
+  a.fields = m->d_fields;
+  a.xi = m->t_xi;
+  a.xi_stride = m->t_xs;
+  a.batch = m->t_batch;
+  a.sv_de = m->sv_de;
+  a.dlogit = dlogit;
+  a.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
+  const int64_t n = (int64_t)a.ntasks * a.batch;
+  if (n > capacity) return fail(DFWFM_ERR_INVALID_ARG, "capacity %lld < %lld entries", (long long)capacity, (long long)n);
+  if (n > 0 && (!dlogit || !out_dest || !out_rows || !ws)) return fail(DFWFM_ERR_INVALID_ARG, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    HIP_TRY(hipMemsetAsync(out_count, 0, sizeof(int32_t), s));
+    return DFWFM_OK;
+  }
+  const size_t need = sparse_workspace_bytes(n, a.w, a.ntasks);
+  if (ws_bytes < (int64_t)need)
+    return fail(DFWFM_ERR_INVALID_ARG, "workspace of %lld bytes < %zu", (long long)ws_bytes, need);
+  hipError_t e = launch_sparse_grads(a, out_dest, out_rows, out_count, ws, (size_t)ws_bytes, s);
+  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "sparse grads");
+}
+
+int dfwfm_sparse_grads_apply(float* grad, int32_t width, const int64_t* dest, const float* rows, const int32_t* count,
+                             int64_t capacity, void* stream) {
+  if (capacity < 0 || width < 1) return fail(DFWFM_ERR_INVALID_ARG, "bad size");
+  if (capacity > 0 && (!grad || !dest || !rows || !count)) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  hipError_t e = launch_sparse_apply(grad, width, dest, rows, count, capacity, (hipStream_t)stream);
+  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "sparse apply");
 }
 
 int dfwfm_workspace_generation(const dfwfm_model* m, int64_t* gen) {

@@ -120,7 +120,7 @@ class FusedTrainStep:
     around an RCCL all-reduce of the gradient buffer."""
 
     def __init__(self, model, batch_size, lr=1e-3, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8,
-                 use_graph=True, dist=None):
+                 use_graph=True, dist=None, sparse_exchange=True):
         dev = model._device()
         if dev.type != "cuda":
             raise _lib.DfwfmError("FusedTrainStep runs only on a HIP device")
@@ -138,13 +138,21 @@ class FusedTrainStep:
         known |= {id(t) for t in dense["lin_w"] + dense["lin_b"]}
         if any(id(p) not in known for p in params):
             raise NotImplementedError("FusedTrainStep: a trainable parameter outside the kernels' layout")
-        # gradient buffer order: every gradient the backward's first part writes (tables, shallow dense,
-        # net_1_fc), then the MLP weights / biases the weight-gradient GEMM writes last -- two
-        # contiguous buckets, so under data parallelism the first bucket's all-reduce overlaps the GEMM
+        # gradient buffer order: [categorical tables | the rest of what the backward's first part writes
+        # (numerical-field tables, shallow dense, net_1_fc) | the MLP weights / biases the weight-gradient
+        # GEMM writes last].  Under data parallelism the tables go over the sparse touched-row exchange
+        # (sparse_exchange, dfwfm_sparse_grads) and the two dense buckets over all-reduces, the first one
+        # overlapping the GEMM; with sparse_exchange=False the tables join the first all-reduce (dense, like
+        # the reference's nn.Embedding(sparse=False) gradients)
         mlp_ids = {id(t) for t in dense["lin_w"] + dense["lin_b"]}
-        params = [p for p in params if id(p) not in mlp_ids] + [p for p in params if id(p) in mlp_ids]
+        cat_ids = {id(t) for f, tup in enumerate(fields) if f >= model.num for t in tup if t is not None}
+        params = [p for p in params if id(p) in cat_ids] + \
+            [p for p in params if id(p) not in mlp_ids and id(p) not in cat_ids] + \
+            [p for p in params if id(p) in mlp_ids]
         total = sum(p.numel() for p in params)
+        self.n_tables = sum(p.numel() for p in params if id(p) in cat_ids)
         self.n_bucket_a = sum(p.numel() for p in params if id(p) not in mlp_ids)
+        self.sparse = dist is not None and bool(sparse_exchange) and self.n_tables > 0
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -160,8 +168,11 @@ class FusedTrainStep:
             off += n
         self.params, self.adam, self.n_adam = params, adam, len(params)
         ptr = lambda t: None if t is None else views[id(t)].data_ptr()  # noqa: E731
+        # sparse exchange: the backward leaves the categorical tables alone (no dense scatter); their rows
+        # come from every rank's touched-row lists (_apply_sparse)
         self.fg = (_lib.dfwfm_field_grads * len(fields))(
-            *[_lib.dfwfm_field_grads(*[ptr(t) for t in tup]) for tup in fields])
+            *[_lib.dfwfm_field_grads(*[None if (self.sparse and f >= model.num) else ptr(t) for t in tup])
+              for f, tup in enumerate(fields)])
         H = len(dense["lin_w"])
         self.gW = (ctypes.c_void_p * max(H, 1))(*[ptr(t) for t in dense["lin_w"]])
         self.gB = (ctypes.c_void_p * max(H, 1))(*[ptr(t) for t in dense["lin_b"]])
@@ -192,6 +203,75 @@ class FusedTrainStep:
         self._attached = True
         self.graphs = None
         self.steps = 0
+        if self.sparse:
+            self._setup_sparse(fields, views)
+
+    # -- touched-row exchange of the categorical tables' gradients (data parallelism) ------------------
+    def _setup_sparse(self, fields, views):
+        """Per table family (second-order rows of width D, first-order rows of width 1) the list buffers of
+        dfwfm_sparse_grads, packed into ONE byte buffer per rank so the exchange is one all-gather:
+        [dest int64 per family | rows f32 per family | counts int32]."""
+        L, h = self.L, self.eng.handle
+        base = self.grad.data_ptr()
+
+        def off(t):
+            return -1 if t is None else (views[id(t)].data_ptr() - base) // 4
+        fams = []
+        for fam, (iq, ir) in ((_lib.FAMILY_SECOND, (0, 1)), (_lib.FAMILY_FIRST, (2, 3))):
+            dest = (_lib.dfwfm_sparse_dest * len(fields))(
+                *[_lib.dfwfm_sparse_dest(off(tup[iq]) if f >= self.model.num else -1,
+                                         off(tup[ir]) if f >= self.model.num else -1)
+                  for f, tup in enumerate(fields)])
+            cap, w, ws = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int64(0)
+            _lib.check(L.dfwfm_sparse_grads_size(h, fam, self.B, ctypes.byref(cap), ctypes.byref(w), ctypes.byref(ws)),
+                       "dfwfm_sparse_grads_size")
+            if cap.value > 0:
+                fams.append(dict(fam=fam, dest=dest, cap=int(cap.value), w=int(w.value), ws_bytes=int(ws.value)))
+        nbytes = 0
+        for f in fams:
+            f["o_dest"] = nbytes
+            nbytes += 8 * f["cap"]
+        for f in fams:
+            f["o_rows"] = nbytes
+            nbytes += 4 * f["cap"] * f["w"]
+        o_cnt = nbytes
+        nbytes += 8 * ((4 * len(fams) + 7) // 8)
+        world = self.dist.get_world_size()
+        self.sp_send = torch.zeros(nbytes, dtype=torch.uint8, device=self.dev)
+        self.sp_recv = torch.zeros(world, nbytes, dtype=torch.uint8, device=self.dev)
+        self.sp_ws = torch.empty(max([f["ws_bytes"] for f in fams] + [1]), dtype=torch.uint8, device=self.dev)
+        for i, f in enumerate(fams):
+            f["o_cnt"] = o_cnt + 4 * i
+        self.sp_fams = fams
+        self.sp_bytes = nbytes
+
+    def _sparse_lists(self, st):
+        """This rank's touched-row lists of the step just run (part of the first graph)."""
+        for f in self.sp_fams:
+            sb = self.sp_send.data_ptr()
+            _lib.check(self.L.dfwfm_sparse_grads(
+                self.eng.handle, f["fam"], ctypes.c_void_p(self.dlogit.data_ptr()), f["dest"], f["cap"],
+                ctypes.c_void_p(sb + f["o_dest"]), ctypes.c_void_p(sb + f["o_rows"]), ctypes.c_void_p(sb + f["o_cnt"]),
+                ctypes.c_void_p(self.sp_ws.data_ptr()), self.sp_ws.numel(), st), "dfwfm_sparse_grads")
+
+    def _gather_sparse(self):
+        d = self.dist
+        if d.get_backend() == "nccl":
+            return d.all_gather_into_tensor(self.sp_recv.view(-1), self.sp_send, async_op=True)
+        return d.all_gather(list(self.sp_recv.unbind(0)), self.sp_send, async_op=True)
+
+    def _apply_sparse(self):
+        """Every rank adds rank 0's lists, then rank 1's, ... into its dense table gradients (zeroed at the
+        step's start): the same additions in the same order on every rank -> bit-identical replicas."""
+        st = self._stream()
+        g = ctypes.c_void_p(self.grad.data_ptr())
+        for r in range(self.sp_recv.shape[0]):
+            rb = self.sp_recv[r].data_ptr()
+            for f in self.sp_fams:
+                _lib.check(self.L.dfwfm_sparse_grads_apply(g, f["w"], ctypes.c_void_p(rb + f["o_dest"]),
+                                                           ctypes.c_void_p(rb + f["o_rows"]),
+                                                           ctypes.c_void_p(rb + f["o_cnt"]), f["cap"], st),
+                           "dfwfm_sparse_grads_apply")
 
     def close(self):
         """Detach the engine from this step's device counter (the engine outlives the trainer: a later
@@ -230,6 +310,8 @@ class FusedTrainStep:
         phases = _lib.BWD_TABLES if self._bucketed() else (_lib.BWD_TABLES | _lib.BWD_MLP_WEIGHTS)
         _lib.check(L.dfwfm_backward_phases(h, ctypes.c_void_p(self.dlogit.data_ptr()), ctypes.byref(self.grads),
                                            phases, st), "dfwfm_backward_phases")
+        if self.sparse:
+            self._sparse_lists(st)
 
     def _part1b(self):
         """The MLP weight gradients (dW_l, db_l): the backward's second part under data parallelism."""
@@ -246,12 +328,26 @@ class FusedTrainStep:
                                               ctypes.c_void_p(self.state.data_ptr()), self._stream()),
                    "dfwfm_adam_step_dev")
 
-    def _exchange(self, run_part1b):
+    def _exchange(self, run_part1b, run_apply=None):
         """Data parallelism: all-reduce the gradient buffer (RCCL).  Bucketed: the first bucket (every
         gradient but the MLP weights') goes out as soon as the backward's first part is done and runs
         while the weight-gradient GEMM (run_part1b) forms the second bucket; otherwise one call."""
         if self.dist is None:
             run_part1b()
+            return
+        if self.sparse:
+            # dense bucket (everything but the categorical tables and the MLP) and the touched-row lists go
+            # out while the weight-gradient GEMM runs; then the MLP bucket; then every rank's lists are added
+            lo, hi = self.n_tables, self.n_bucket_a
+            works = [self._gather_sparse()]
+            if hi > lo:
+                works.append(self.dist.all_reduce(self.grad[lo:hi], async_op=True))
+            run_part1b()
+            if self.grad.numel() > hi:
+                works.append(self.dist.all_reduce(self.grad[hi:], async_op=True))
+            for w in works:
+                w.wait()
+            run_apply()
             return
         if not self._bucketed():
             run_part1b()
@@ -269,6 +365,7 @@ class FusedTrainStep:
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        ga = None
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s):
                 self._part1(self.B, denom)
@@ -277,10 +374,14 @@ class FusedTrainStep:
                     self._part1b()
             else:
                 g1b = None
+            if self.sparse:
+                ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga, stream=s):
+                    self._apply_sparse()
             with torch.cuda.graph(g2, stream=s):
                 self._part2()
         torch.cuda.current_stream(self.dev).wait_stream(s)
-        return g1, g1b, g2
+        return g1, g1b, ga, g2
 
     def step(self, xi, xv, y, n_global=None):
         """One step on device tensors xi [n, F-num] int64, xv [n, num] f32, y [n] f32 (n <= batch_size);
@@ -306,13 +407,14 @@ class FusedTrainStep:
                 self.graphs = None
                 self.graphs = self._capture(denom)
                 self._graph_key = (denom, self.drop, self._ws_generation())
-            g1, g1b, g2 = self.graphs
+            g1, g1b, ga, g2 = self.graphs
             g1.replay()
-            self._exchange(lambda: g1b.replay() if g1b is not None else None)
+            self._exchange(lambda: g1b.replay() if g1b is not None else None,
+                           lambda: ga.replay() if ga is not None else None)
             g2.replay()
         else:
             self._part1(n, denom)
-            self._exchange(self._part1b if self._bucketed() else (lambda: None))
+            self._exchange(self._part1b if self._bucketed() else (lambda: None), self._apply_sparse)
             self._part2()
         self.steps += 1
         self.eng._dense_key = None  # weights changed behind torch's version counters: re-pack on next use
