@@ -513,13 +513,13 @@ def _sparse_setup(m, gpu):
     for p in params:
         views[id(p)] = (off, flat[off:off + p.numel()].view_as(p))
         off += p.numel()
-    return fields, views, flat, _lib, ctypes
+    return fields, dense, views, flat, _lib, ctypes
 
 
 def _sparse_step(m, gpu, xi, xv, y, sparse):
     """One backward of m on (xi, xv, y): dense scatter (sparse=False) or touched-row lists applied to a zero
     buffer (sparse=True).  Returns {param name: grad}, the lists (for sparse) and the flat buffer."""
-    fields, views, flat, _lib, ctypes = _sparse_setup(m, gpu)
+    fields, dense, views, flat, _lib, ctypes = _sparse_setup(m, gpu)
     L, eng = _lib.lib(), m._sync_engine(gpu)
     st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
     xi_d, xv_d, y_d = (torch.from_numpy(a).to(gpu) for a in (xi.reshape(len(xi), -1), xv, y))
