@@ -113,3 +113,72 @@ def test_dp_grad_allreduce_gloo_world2():
         (a1, b1), (a2, b2) = res[r]
         assert torch.equal(a1, base[:3]) and torch.equal(b1, base[3:].view(2, 2))
         assert torch.equal(a2, torch.full((3,), 3.0)) and torch.equal(b2, torch.full((2, 2), 30.0))
+
+
+def _sparse_protocol_worker(rank, world, port, q):
+    """One rank of the touched-row exchange at oracle level: its local table gradients (torch_port, loss
+    normalised by the global batch) -> (dest, row) list at fixed capacity packed into one byte buffer ->
+    training.gather_packed over gloo -> every rank's lists added in rank order."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from xsdeepfwfm_deprecated_amd.training import gather_packed
+        cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_lw")
+        n = 64
+        lo = rank * (n // world)
+        hi = lo + n // world
+        _, _, g, _ = torch_port.train_step(cfg, params, xi[lo:hi], xv[lo:hi], y[lo:hi], 1e-3, 0.0)
+        scale = (hi - lo) / n  # the rank's mean-loss gradient -> its share of the global mean
+        num, D = cfg["numerical"], cfg["embedding_size"]
+        names = [f"fm_2nd_embeddings.{f}.weight" for f in range(num, cfg["field_size"])]
+        offs = np.cumsum([0] + [params[k].shape[0] for k in names])
+        cap = len(names) * (n // world)
+        dest = np.full(cap, -1, np.int64)
+        rows = np.zeros((cap, D), np.float32)
+        c = 0
+        for j, k in enumerate(names):
+            touched = np.unique(xi[lo:hi, j])
+            dest[c:c + len(touched)] = offs[j] + touched
+            rows[c:c + len(touched)] = g[k][touched] * scale
+            c += len(touched)
+        send = torch.cat([torch.from_numpy(dest).view(torch.uint8), torch.from_numpy(rows).view(-1).view(torch.uint8),
+                          torch.tensor([c, 0], dtype=torch.int32).view(torch.uint8)])
+        recv = torch.zeros(world, send.numel(), dtype=torch.uint8)
+        gather_packed(dist, send, recv, async_op=False)
+        flat = torch.zeros(int(offs[-1]), D)
+        for r in range(world):
+            b = recv[r]
+            cnt = int(b[-8:].view(torch.int32)[0])
+            d = b[:8 * cap].view(torch.int64)[:cnt]
+            v = b[8 * cap:8 * cap + 4 * cap * D].view(torch.float32).view(cap, D)[:cnt]
+            flat[d] += v  # destinations unique within one list
+        q.put((rank, flat.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_touched_row_exchange_protocol_gloo_world2():
+    """configs[4] exchange at oracle level on CPU: two gloo ranks' touched-row lists, all-gathered at fixed
+    capacity and added in rank order, equal the dense table gradients of one process on the global batch,
+    identically on both ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sparse_protocol_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0], res[1])
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_lw")
+    _, _, g, _ = torch_port.train_step(cfg, params, xi[:64], xv[:64], y[:64], 1e-3, 0.0)
+    dense = np.concatenate([g[f"fm_2nd_embeddings.{f}.weight"] for f in range(13, 39)])
+    assert np.abs(res[0] - dense).max() <= 2e-5 * np.abs(dense).max()

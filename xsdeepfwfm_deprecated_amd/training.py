@@ -108,6 +108,15 @@ class Adam(torch.optim.Optimizer):
 
 
 # --------------------------------------------------------------------------------------- fused step
+def gather_packed(dist, send, recv, async_op=True):
+    """All-gather of one packed byte buffer per rank (touched-row lists: [dest | rows | counts], fixed
+    capacity, so no size exchange and no host synchronisation) into recv [world, nbytes]: one collective
+    (RCCL all_gather_into_tensor; gloo: the list form)."""
+    if dist.get_backend() == "nccl":
+        return dist.all_gather_into_tensor(recv.view(-1), send, async_op=async_op)
+    return dist.all_gather(list(recv.unbind(0)), send, async_op=async_op)
+
+
 class FusedTrainStep:
     """One reference training step -- fit()'s inner-loop body (:619-637): zero_grad, forward,
     BCE-with-logits, backward, Adam(lr, weight_decay) -- as HIP launches on pre-built pointers, captured
@@ -255,10 +264,7 @@ class FusedTrainStep:
                 ctypes.c_void_p(self.sp_ws.data_ptr()), self.sp_ws.numel(), st), "dfwfm_sparse_grads")
 
     def _gather_sparse(self):
-        d = self.dist
-        if d.get_backend() == "nccl":
-            return d.all_gather_into_tensor(self.sp_recv.view(-1), self.sp_send, async_op=True)
-        return d.all_gather(list(self.sp_recv.unbind(0)), self.sp_send, async_op=True)
+        return gather_packed(self.dist, self.sp_send, self.sp_recv)
 
     def _apply_sparse(self):
         """Every rank adds rank 0's lists, then rank 1's, ... into its dense table gradients (zeroed at the
