@@ -25,6 +25,18 @@ LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
 LOAD_PATH = os.path.join(PKG_DIR, os.environ["DFWFM_LIB"]) if os.environ.get("DFWFM_LIB") else LIB_PATH
 SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_sparse.hip",
            "dfwfm_capi.hip"]
+# the forward / backward kernel templates are instantiated once per embedding size, each size in its own
+# translation unit (-DDFWFM_KD=<D>) so they compile in parallel; the plain object holds everything else
+EMB_SIZES = (4, 8, 10, 16, 32)
+PER_D_SOURCES = ["dfwfm_kernels.hip", "dfwfm_train.hip"]
+
+
+def _units():
+    """(source, object, extra flags) of every translation unit of libdfwfm.so."""
+    u = [(s, os.path.splitext(s)[0] + ".o", []) for s in SOURCES]
+    for s in PER_D_SOURCES:
+        u += [(s, f"{os.path.splitext(s)[0]}_d{d}.o", [f"-DDFWFM_KD={d}"]) for d in EMB_SIZES]
+    return u
 HEADERS = ["dfwfm_internal.h", "dfwfm_device.h", os.path.join("..", "..", "include", "dfwfm.h")]
 ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
 INGEST_PATH = os.path.join(PKG_DIR, "libdfwfm_ingest.so")
@@ -173,21 +185,24 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB_PATH
     from concurrent.futures import ThreadPoolExecutor
-    objs = [os.path.join(CSRC, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+    units = _units()
+    objs = [os.path.join(CSRC, o) for _, o, _ in units]
     hdr_m = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
 
     def compile_one(i):
-        src = os.path.join(CSRC, SOURCES[i])
+        src, _, extra = units[i]
+        src = os.path.join(CSRC, src)
         if not force and os.path.exists(objs[i]) and \
                 os.path.getmtime(objs[i]) >= max(os.path.getmtime(src), hdr_m):
             return  # object up to date (kept between builds; *.o is git- and gpurun-ignored)
-        cmd = [hipcc] + flags + ["-c", "-o", objs[i], os.path.join(CSRC, SOURCES[i])]
+        cmd = [hipcc] + flags + extra + ["-c", "-o", objs[i], src]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True, cwd=CSRC)
 
-    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        list(ex.map(compile_one, range(len(SOURCES))))
+    jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(units), max(1, len(os.sched_getaffinity(0))))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(compile_one, range(len(units))))
     with open(stamp, "w") as f:
         f.write(" ".join(flags))
     tmp = LIB_PATH + ".tmp"

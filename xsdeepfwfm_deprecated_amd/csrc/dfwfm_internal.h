@@ -313,6 +313,19 @@ bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s);
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
+// per-embedding-size launchers, each compiled in its own translation unit (-DDFWFM_KD=<D>)
+#define DFWFM_PER_D_CAT2(a, b) a##b
+#define DFWFM_PER_D_CAT(a, b) DFWFM_PER_D_CAT2(a, b)
+#define DFWFM_PER_D(name) DFWFM_PER_D_CAT(name, DFWFM_KD)
+#define DFWFM_DECL_PER_D(D)                                                                                   \
+  hipError_t launch_forward_d##D(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s);        \
+  hipError_t launch_forward_split_d##D(const FwdArgs& a, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s); \
+  hipError_t launch_backward_d##D(const BwdArgs& a, int tpw, int ng, size_t lds, hipStream_t s);
+DFWFM_DECL_PER_D(4)
+DFWFM_DECL_PER_D(8)
+DFWFM_DECL_PER_D(10)
+DFWFM_DECL_PER_D(16)
+DFWFM_DECL_PER_D(32)
 hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds, hipStream_t s);
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
 hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s);

@@ -611,6 +611,7 @@ fwd_kernel(FwdArgs p) {
   stamp_end_rt(p.stamps, tid);
 }
 
+#ifndef DFWFM_KD  // packing: the common translation unit only
 // ---------------------------------------------------------------------------
 // dense-parameter packing (run on weight updates, not per forward)
 // ---------------------------------------------------------------------------
@@ -682,6 +683,8 @@ __global__ void __launch_bounds__(256) pack_dense_kernel(const PackList L) {
   const int64_t i = (int64_t)(bid - j.block0) * 256 + threadIdx.x;
   if (i < j.total) pack_elem(j, i);
 }
+
+#endif  // DFWFM_KD
 
 // ---------------------------------------------------------------------------
 // launchers
@@ -757,13 +760,23 @@ static hipError_t launch_split_d(const FwdArgs& a, int tpw, int ng, size_t lds1,
   }
 }
 
+#ifdef DFWFM_KD
+// one translation unit per embedding size (parallel build): this one's launchers
+hipError_t DFWFM_PER_D(launch_forward_d)(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
+  return launch_fwd_d<DFWFM_KD>(a, tpw, ks, ng, lds, s);
+}
+hipError_t DFWFM_PER_D(launch_forward_split_d)(const FwdArgs& a, int tpw, int ng, size_t lds1, size_t lds2,
+                                               hipStream_t s) {
+  return launch_split_d<DFWFM_KD>(a, tpw, ng, lds1, lds2, s);
+}
+#else
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s) {
   switch (D) {
-    case 4: return launch_split_d<4>(a, tpw, ng, lds1, lds2, s);
-    case 8: return launch_split_d<8>(a, tpw, ng, lds1, lds2, s);
-    case 10: return launch_split_d<10>(a, tpw, ng, lds1, lds2, s);
-    case 16: return launch_split_d<16>(a, tpw, ng, lds1, lds2, s);
-    case 32: return launch_split_d<32>(a, tpw, ng, lds1, lds2, s);
+    case 4: return launch_forward_split_d4(a, tpw, ng, lds1, lds2, s);
+    case 8: return launch_forward_split_d8(a, tpw, ng, lds1, lds2, s);
+    case 10: return launch_forward_split_d10(a, tpw, ng, lds1, lds2, s);
+    case 16: return launch_forward_split_d16(a, tpw, ng, lds1, lds2, s);
+    case 32: return launch_forward_split_d32(a, tpw, ng, lds1, lds2, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -772,11 +785,11 @@ bool supported_embedding_size(int D) { return D == 4 || D == 8 || D == 10 || D =
 
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
   switch (D) {
-    case 4: return launch_fwd_d<4>(a, tpw, ks, ng, lds, s);
-    case 8: return launch_fwd_d<8>(a, tpw, ks, ng, lds, s);
-    case 10: return launch_fwd_d<10>(a, tpw, ks, ng, lds, s);
-    case 16: return launch_fwd_d<16>(a, tpw, ks, ng, lds, s);
-    case 32: return launch_fwd_d<32>(a, tpw, ks, ng, lds, s);
+    case 4: return launch_forward_d4(a, tpw, ks, ng, lds, s);
+    case 8: return launch_forward_d8(a, tpw, ks, ng, lds, s);
+    case 10: return launch_forward_d10(a, tpw, ks, ng, lds, s);
+    case 16: return launch_forward_d16(a, tpw, ks, ng, lds, s);
+    case 32: return launch_forward_d32(a, tpw, ks, ng, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -786,5 +799,6 @@ hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s) 
   hipLaunchKernelGGL(pack_dense_kernel, dim3(total_blocks), dim3(256), 0, s, L);
   return hipGetLastError();
 }
+#endif  // DFWFM_KD
 
 }  // namespace dfwfm

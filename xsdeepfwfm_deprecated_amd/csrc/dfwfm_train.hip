@@ -42,9 +42,11 @@ __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX
   return L;
 }
 
+#ifndef DFWFM_KD
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY) {
   return sizeof(float) * (size_t)bwd_layout(F, D, MT, S, SX, SY).total;
 }
+#endif
 
 // NG: waves = output-tile groups of the MLP chain.  4: one wave per SIMD, TPW tiles each; 8: two
 // per SIMD (256 registers, one workgroup per CU) with the 8*TPW+1-th tile of a layer split by K over
@@ -287,6 +289,7 @@ __host__ __device__ inline RedLds red_layout(int F, int D, int N, int num) {
 // [n, ncap); U float4 per thread in flight
 // stage_linear in two halves, so that several sources' loads are in flight together: stage_issue
 // loads the first 256*U float4 into registers, stage_commit stores them and copies any remainder
+#ifndef DFWFM_KD  // the non-templated kernels: the common translation unit only
 template <int U>
 __device__ __forceinline__ void stage_issue(f32x4 (&v)[U], const float* __restrict__ src, int n, int ncap, int tid) {
   const int n4 = ncap >> 2;
@@ -904,6 +907,8 @@ __global__ void __launch_bounds__(256) bce_grad_kernel(const float* __restrict__
   }
 }
 
+#endif  // DFWFM_KD
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
@@ -943,13 +948,19 @@ static hipError_t launch_bwd_d(const BwdArgs& a, int tpw, int ng, size_t lds, hi
   }
 }
 
+#ifdef DFWFM_KD
+// one translation unit per embedding size (parallel build): this one's backward launcher
+hipError_t DFWFM_PER_D(launch_backward_d)(const BwdArgs& a, int tpw, int ng, size_t lds, hipStream_t s) {
+  return launch_bwd_d<DFWFM_KD>(a, tpw, ng, lds, s);
+}
+#else
 hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds, hipStream_t s) {
   switch (D) {
-    case 4: return launch_bwd_d<4>(a, tpw, ng, lds, s);
-    case 8: return launch_bwd_d<8>(a, tpw, ng, lds, s);
-    case 10: return launch_bwd_d<10>(a, tpw, ng, lds, s);
-    case 16: return launch_bwd_d<16>(a, tpw, ng, lds, s);
-    case 32: return launch_bwd_d<32>(a, tpw, ng, lds, s);
+    case 4: return launch_backward_d4(a, tpw, ng, lds, s);
+    case 8: return launch_backward_d8(a, tpw, ng, lds, s);
+    case 10: return launch_backward_d10(a, tpw, ng, lds, s);
+    case 16: return launch_backward_d16(a, tpw, ng, lds, s);
+    case 32: return launch_backward_d32(a, tpw, ng, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1028,5 +1039,7 @@ hipError_t launch_bce_grad(const float* z, const float* y, int64_t n, float deno
                      loss_sum);
   return hipGetLastError();
 }
+
+#endif  // DFWFM_KD
 
 }  // namespace dfwfm
