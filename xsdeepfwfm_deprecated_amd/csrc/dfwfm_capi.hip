@@ -26,6 +26,8 @@ struct dfwfm_model {
   int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
   size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
   int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
+  uint8_t fw_list4[kMaxPieces], fw_off4[5];  // FwFM pieces per wave, 4- and 8-wave launches (fw_schedule)
+  uint8_t fw_list8[kMaxPieces], fw_off8[9];
   // device state (owned)
   FieldDev* d_fields;
   float* d_upack;  // FwFM A-operand fragments [MT][S][64]
@@ -116,6 +118,29 @@ void free_model(dfwfm_model* m) {
 
 }  // namespace
 
+// FwFM second-order pieces (row tile m, column tile nt; S - 4m MFMA steps each) balanced over `nw` waves:
+// largest first, each to the least-loaded wave; a wave's list is in ascending piece order.  The pieces'
+// results do not depend on the assignment, so 4- and 8-wave launches give identical logits.
+static void fw_schedule(int MT, int D, int S, int nw, uint8_t* list, uint8_t* off) {
+  int load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int owner[kMaxPieces];
+  for (int m = 0; m < MT; ++m)  // sizes fall with m: row tile order is largest first
+    for (int nt = 0; nt < D; ++nt) {
+      int w = 0;
+      for (int k = 1; k < nw; ++k)
+        if (load[k] < load[w]) w = k;
+      owner[m * D + nt] = w;
+      load[w] += S - 4 * m;
+    }
+  int o = 0;
+  for (int w = 0; w < nw; ++w) {
+    off[w] = (uint8_t)o;
+    for (int pc = 0; pc < MT * D; ++pc)
+      if (owner[pc] == w) list[o++] = (uint8_t)pc;
+  }
+  off[nw] = (uint8_t)o;
+}
+
 extern "C" {
 
 const char* dfwfm_last_error(void) { return g_last_error.c_str(); }
@@ -173,6 +198,8 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   m->NC0 = (F * D + 15) / 16;
   m->MT = (F + 15) / 16;
   m->S = (F + 3) / 4;
+  fw_schedule(m->MT, D, m->S, 4, m->fw_list4, m->fw_off4);
+  fw_schedule(m->MT, D, m->S, 8, m->fw_list8, m->fw_off8);
   // E-tile columns read by the MLP (NC0*16) and by the FwFM contraction (4*S fields)
   m->W0 = m->NC0 * 16 > 4 * m->S * D ? m->NC0 * 16 : 4 * m->S * D;
   const int kx = m->W0 > NT * 16 ? m->W0 : NT * 16;
@@ -408,6 +435,10 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
+  memcpy(a.fw_list4, m->fw_list4, sizeof a.fw_list4);
+  memcpy(a.fw_list8, m->fw_list8, sizeof a.fw_list8);
+  memcpy(a.fw_off4, m->fw_off4, sizeof a.fw_off4);
+  memcpy(a.fw_off8, m->fw_off8, sizeof a.fw_off8);
 }
 
 // Activation workspace for `batch` rows: E [B][F*D], fo [B][F], X_0 [B][r4(F*D)], X_h and G_h [B][N].
@@ -485,6 +516,7 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, out);
   // diagnostics only (phase timing): DFWFM_DIAG_DROP_FLAGS clears flag bits, results become invalid
   if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
+  if (const char* pr = getenv("DFWFM_PRIO")) a.flags |= atoi(pr) ? kPrio : 0;
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;

@@ -15,6 +15,7 @@ constexpr int kMaxTPW = 8;  // MLP output tiles per wave group => deep_nodes <= 
 constexpr int kMaxMT = 4;   // FwFM row tiles => field_size <= 64
 constexpr int kStampSlots = 16;  // diagnostic phase stamps per workgroup
 constexpr int kTailC = 8;        // split tail tile: K chunks per wave (layer widths <= 4*8*16 = 512)
+constexpr int kMaxPieces = kMaxMT * 32;  // FwFM work pieces (row tile m, column tile nt): MT * D
 
 // flags
 constexpr int kHasSecond = 1;  // FwFM / FM second order
@@ -25,6 +26,7 @@ constexpr int kFoLw = 16;      // project first order with fm_1st.weight
 constexpr int kNeedE = 32;     // second-order / deep embeddings are gathered
 constexpr int kTrain = 64;     // save the activations the backward needs (FwdArgs::sv_*)
 constexpr int kDrop = 128;     // dropout on the deep tower (train only)
+constexpr int kPrio = 256;     // raise the wave priority for the phases before the MLP (A/B: DFWFM_PRIO)
 constexpr int kMaxH = 16;      // hidden layers
 
 // Device copy of dfwfm_field_tables (same field order and sizes); for QR fields
@@ -80,6 +82,12 @@ struct FwdArgs {
   float* part_e;            // [B][part_stride] E tile rows (W0 columns, zero padded past F*D)
   float* part_fs;           // [B] first + second order
   int32_t part_stride;      // floats per row (W0, a multiple of 4)
+  // FwFM second order: the pieces (row tile m, column tile nt) -> pc = m * D + nt each wave runs, for 4- and
+  // 8-wave launches: wave w takes fw_list{4,8}[fw_off{4,8}[w] .. fw_off{4,8}[w + 1]) (balanced on the host)
+  uint8_t fw_list4[kMaxPieces];
+  uint8_t fw_list8[kMaxPieces];
+  uint8_t fw_off4[5];
+  uint8_t fw_off8[9];
 };
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.
@@ -102,7 +110,7 @@ __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int
   L.red = o;   o += (deep && KS == 2) ? 4 * TPW * 64 * 4 : 0;
   L.tailr = o; o += (deep && tail) ? NG * 64 * 4 + kBM : 0;  // partials + per-row deep sums of the tail
   L.fo = o;    o += kBM * r4(F);
-  L.part2 = o; o += r4(kBM * D);
+  L.part2 = o; o += MT * D * 16;  // per FwFM piece, its 16 column sums
   L.dsum = o;  o += NG * kBM;
   L.fs = o;    o += kBM;
   L.total = r4(o);

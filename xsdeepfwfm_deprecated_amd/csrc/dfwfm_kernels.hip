@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dfwfm_device.h"
 #include "dfwfm_internal.h"
 
@@ -85,6 +87,9 @@ fwd_kernel(FwdArgs p) {
   const int64_t b0 = (int64_t)blockIdx.x * kBM;
   stamp(p.stamps, 0, tid);
   stamp_start_rt(p.stamps, tid);
+  // gather / shallow phases at a raised priority: beside a co-resident workgroup's MLP they would otherwise
+  // lose every issue arbitration (A/B switch, kPrio)
+  if (flags & kPrio) __builtin_amdgcn_s_setprio(1);
   const int g = wave & (NG - 1);  // MLP output-tile group
   const int kh = wave / NG;       // MLP K half (KS == 2)
 
@@ -262,16 +267,12 @@ fwd_kernel(FwdArgs p) {
         if (mode[k] != 0) fb[k] = *qb[k];
       }
     }
-    // layer-0 weights: the first two chunks go out behind the row loads (vmcnt retires in issue
-    // order, so issuing them earlier would make every gather wait for 56 KB of weights) and land
-    // during the combine, the shallow part and the barriers
+    // layer-0 weights: the first two chunks go out behind the row loads (vmcnt retires in issue order, so
+    // issuing them earlier would make every gather wait for 56 KB of weights) and land during the combine,
+    // the shallow part and the barriers
     if (deep) {
       ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
       DFWFM_PRELOAD(ls);
-      if (tail) {
-        ts.init(0, p.NC0, TT, g);
-        ts.load(wrsrc, tw, lane * 16);
-      }
     }
     // ... the shallow parameters go to LDS while the row loads are in flight ...
 #pragma unroll
@@ -336,65 +337,59 @@ fwd_kernel(FwdArgs p) {
   }
   stamp(p.stamps, 9, tid);
   if (flags & kHasSecond) {
-    // Y = U * E_b on MFMA: rows k (fields, MT tiles), columns n = b*D + d (D tiles of 16),
-    // contraction over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].
-    const int MT = p.MT, S = p.S;
-    constexpr int NTW = (D + NW - 1) / NW;  // column tiles per wave
-    const float* ecol[NTW];
-    float v[NTW];
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      int nt = wave + NW * j;
-      nt = nt < D ? nt : D - 1;  // clamped duplicate, discarded below
+    // Y = U * E_b on MFMA: rows k (fields, MT tiles of 16), columns n = b*D + d (D tiles of 16), contraction
+    // over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].  The work is cut into
+    // pieces pc = (row tile m, column tile nt) of S - 4m steps each (U's rows 16m.. vanish for l <= 16m); the
+    // host balances the pieces over the waves (fw_list), and every piece leaves its 16 column sums in
+    // part2[pc] -- so the result does not depend on the wave count.
+    const int S = p.S;
+    const uint8_t* plist = NW == 8 ? p.fw_list8 : p.fw_list4;
+    const int p_lo = NW == 8 ? p.fw_off8[wave] : p.fw_off4[wave];
+    const int p_hi = NW == 8 ? p.fw_off8[wave + 1] : p.fw_off4[wave + 1];
+    for (int pi = p_lo; pi < p_hi; ++pi) {
+      const int pc = plist[pi];
+      const int m = pc / D;
+      const int nt = pc - m * D;
       const int n = nt * 16 + (lane & 15);
       const int b = n / D;
-      ecol[j] = bufX + b * SX + (n - b * D);  // E[b][l][d] = ecol[l * D]
-      v[j] = 0.f;
-    }
-    // one row tile at a time keeps the accumulators in fixed registers (guarded MFMAs make hipcc
-    // shuttle every accumulator between AGPRs and VGPRs); U's rows 16m.. vanish for l <= 16m.
-    // Steps go in groups of 4 with every operand of the group read from LDS before its MFMAs.
-    for (int m = 0; m < MT; ++m) {
-      f32x4 acc[NTW];
+      const float* ecol = bufX + b * SX + (n - b * D);  // E[b][l][d] = ecol[l * D]
+      const float* ua = upk + m * S * 64 + lane;        // A fragment of step s: ua[s * 64]
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      // steps in groups: every operand of a group is read from LDS before its MFMAs
+      auto group = [&](int s0, auto U_) {
+        constexpr int U = decltype(U_)::value;
+        float av[U], bv[U];
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int s0 = (16 * m + 1) >> 2; s0 < S; s0 += 4) {
-        float av[4], bv[4][NTW];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int s = s0 + u < S ? s0 + u : S - 1;  // clamped reads; the MFMA is skipped below
-          av[u] = upk[(m * S + s) * 64 + lane];
-          const int l = 4 * s + (lane >> 4);
-#pragma unroll
-          for (int j = 0; j < NTW; ++j) bv[u][j] = ecol[j][l * D];
+        for (int u = 0; u < U; ++u) {
+          av[u] = ua[(s0 + u) * 64];
+          bv[u] = ecol[(4 * (s0 + u) + (lane >> 4)) * D];
         }
-        __builtin_amdgcn_sched_barrier(0);  // all 16 LDS reads issue before the group's MFMAs
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float a_eff = s0 + u < S ? av[u] : 0.f;  // a zero A fragment adds exactly 0
-#pragma unroll
-          for (int j = 0; j < NTW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_eff, bv[u][j], acc[j], 0, 0, 0);
-        }
-      }
+        for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+      };
+      int s0 = 4 * m;
+      for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
+      const int rem = S - s0;
+      if (rem == 3) group(s0, std::integral_constant<int, 3>{});
+      else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
+      else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
+      float v = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int k = 16 * m + 4 * (lane >> 4) + r;
-        const int kk = k < F ? k : 0;
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const float e = ecol[j][kk * D];
-          v[j] = fmaf(k < F ? e : 0.f, acc[j][r], v[j]);
-        }
+        const float e = ecol[(k < F ? k : 0) * D];
+        v = fmaf(k < F ? e : 0.f, acc[r], v);
       }
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) part2[pc * 16 + lane] = v;
     }
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      float x = v[j];
-      x += __shfl_xor(x, 16);
-      x += __shfl_xor(x, 32);
-      const int nt = wave + NW * j;
-      if (lane < 16 && nt < D) part2[nt * 16 + lane] = x;
-    }
+  }
+  // layer 0's tail fragments once the gather rows are dead (live across the gather, they spilled)
+  if (deep && tail) {
+    ts.init(0, p.NC0, TT, g);
+    ts.load(wrsrc, tw, lane * 16);
   }
   stamp(p.stamps, 10, tid);
   __syncthreads();
@@ -426,7 +421,10 @@ fwd_kernel(FwdArgs p) {
       first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
     }
     if (flags & kHasSecond) {
-      for (int d = q; d < D; d += 16) second += part2[b * D + d];  // D = 32: two terms per lane
+      for (int d = q; d < D; d += 16) {  // D = 32: two terms per lane
+        const int n = b * D + d;
+        for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
+      }
     }
 #pragma unroll
     for (int o = 8; o >= 1; o >>= 1) {
@@ -448,6 +446,7 @@ fwd_kernel(FwdArgs p) {
   }  // PART != 2
 
   stamp(p.stamps, 3, tid);
+  if (flags & kPrio) __builtin_amdgcn_s_setprio(0);
   if constexpr (train) __syncthreads();  // the dropped X_0 tile is complete before layer 1 reads it
   // ---- phase M: MLP on MFMA -------------------------------------------------
   const int row0 = (lane >> 4) * 4;
