@@ -92,18 +92,26 @@ __device__ __forceinline__ float combine(int mode, float a, float b, float scale
 // Fragment algebra (16x16x4 f32): in sub-step s of chunk c lane l supplies
 //   A = act[l&15][16c + 4(l>>4) + s],  B = W[n0 + (l&15)][16c + 4(l>>4) + s].
 // ---------------------------------------------------------------------------
-template <int TPW>
+// WA: the weights are the A operand and the activations B, so the accumulator comes out transposed:
+// lane l holds neurons 4(l>>4) + r of row l&15 -- four consecutive outputs of one sample, stored as one
+// 16-byte LDS write (same products, same k order: bit-identical sums)
+template <bool WA>
+__device__ __forceinline__ f32x4 mfma_wa(float a, float w, f32x4 c) {
+  return WA ? __builtin_amdgcn_mfma_f32_16x16x4f32(w, a, c, 0, 0, 0) : __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, c, 0, 0, 0);
+}
+
+template <int TPW, bool WA = false>
 __device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[TPW], const float4& a, const f32x4 (&b)[TPW]) {
   // sub-step-major: consecutive MFMAs hit different accumulators (16x16x4 f32 has a 40-cycle
   // dependent latency against a 32-cycle issue interval)
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[j].x, acc[j], 0, 0, 0);
+  for (int j = 0; j < TPW; ++j) acc[j] = mfma_wa<WA>(a.x, b[j].x, acc[j]);
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[j].y, acc[j], 0, 0, 0);
+  for (int j = 0; j < TPW; ++j) acc[j] = mfma_wa<WA>(a.y, b[j].y, acc[j]);
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[j].z, acc[j], 0, 0, 0);
+  for (int j = 0; j < TPW; ++j) acc[j] = mfma_wa<WA>(a.z, b[j].z, acc[j]);
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[j].w, acc[j], 0, 0, 0);
+  for (int j = 0; j < TPW; ++j) acc[j] = mfma_wa<WA>(a.w, b[j].w, acc[j]);
 }
 
 // One layer's weight stream for one wave: output tiles g, g+4, ... (clamped to NT-1) and K chunks
@@ -140,6 +148,70 @@ struct LayerStream {
   }
 };
 
+// The split tail tile: when the layer has 4*TPW + 1 output tiles, tile T = 4*TPW is shared by the
+// four waves, wave g taking K chunks [NC*g/4, NC*(g+1)/4) of it, so every SIMD carries 6.25 tiles
+// instead of one carrying 7.  All of a wave's tail fragments are loaded with the layer's preload
+// (kTailC <= 8 chunks per wave, NC <= 32) and consumed after the main K loop.
+template <int NG = 4>
+struct TailStream {
+  static constexpr int C = kTailC * 4 / NG;  // K chunks per wave at most (layer widths <= 512)
+  int sbase, c_lo, cnt;
+  __device__ __forceinline__ void init(int layer_off, int NC, int T, int g) {
+    sbase = __builtin_amdgcn_readfirstlane((layer_off + T * NC * 64) * 16);
+    c_lo = (NC * g) / NG;
+    cnt = (NC * (g + 1)) / NG - c_lo;
+  }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, f32x4 (&tw)[C], int voff) const {
+#pragma unroll
+    for (int u = 0; u < C; ++u)
+      if (u < cnt)
+        tw[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, sbase + (c_lo + u) * 1024, 0));
+  }
+  // this wave's partial product of the tail tile (two accumulators: no back-to-back dependent MFMAs)
+  template <bool WA = false>
+  __device__ __forceinline__ f32x4 mma(const float* __restrict__ act, int SA, const f32x4 (&tw)[C], int lane) const {
+    const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
+    f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+    for (int u = 0; u < C; ++u) {
+      if (u < cnt) {
+        const float4 a = *reinterpret_cast<const float4*>(arow + 16 * (c_lo + u));
+        f32x4& c = (u & 1) ? a1 : a0;
+        c = mfma_wa<WA>(a.x, tw[u].x, c);
+        c = mfma_wa<WA>(a.y, tw[u].y, c);
+        c = mfma_wa<WA>(a.z, tw[u].z, c);
+        c = mfma_wa<WA>(a.w, tw[u].w, c);
+      }
+    }
+    return a0 + a1;
+  }
+  // mlp_k_loop_s form: fragments [u0, u0 + TPW) of this wave's share go into a weight register set the
+  // K loop has just freed (its drain steps), and are multiplied after its last step
+  template <int TPW>
+  __device__ __forceinline__ void load_set(__amdgpu_buffer_rsrc_t r, f32x4 (&b)[TPW], int u0, int voff) const {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+      if (u0 + j < cnt)
+        b[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, sbase + (c_lo + u0 + j) * 1024, 0));
+  }
+  template <int TPW, bool WA>
+  __device__ __forceinline__ void mma_set(const float* __restrict__ arow, const f32x4 (&b)[TPW], int u0, f32x4& c0,
+                                          f32x4& c1) const {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int u = u0 + j;
+      if (u < cnt) {
+        const float4 a = *reinterpret_cast<const float4*>(arow + 16 * (c_lo + u));
+        f32x4& c = (u & 1) ? c1 : c0;
+        c = mfma_wa<WA>(a.x, b[j].x, c);
+        c = mfma_wa<WA>(a.y, b[j].y, c);
+        c = mfma_wa<WA>(a.z, b[j].z, c);
+        c = mfma_wa<WA>(a.w, b[j].w, c);
+      }
+    }
+  }
+};
+
 // K loop of one layer, entered with chunks 0 and 1 already in b0 / b1.  Weight fragments rotate
 // through three register sets, each refilled two chunks ahead of its MFMAs (the loop is unrolled
 // by 3 so no set is ever copied: a copy makes hipcc wait for the load it copies).  The activation
@@ -148,12 +220,15 @@ struct LayerStream {
 // them and the next step's first MFMA waited out the LDS latency.  Within a step the LDS read goes
 // first, then the refill loads interleave with the MFMAs (sched_group_barrier: 2 MFMA, 1 load,
 // ...), and a sched_barrier closes the step so hipcc cannot sink them to their use.
-template <int TPW, int KS, int NG = 4>
+// SEEDED: acc arrives holding the initial values (e.g. the bias), else it starts from zero
+template <int TPW, int KS, int NG = 4, bool WA = false, bool SEEDED = false>
 __device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __restrict__ act, int SA,
                                            const LayerStream<TPW, KS, NG>& ls, f32x4 (&b0)[TPW],
                                            f32x4 (&b1)[TPW], f32x4 (&b2)[TPW], int lane) {
+  if constexpr (!SEEDED) {
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const int n = ls.n;
   if (n == 0) return;
   const int voff = lane * 16;
@@ -162,7 +237,7 @@ __device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __res
   float4 a1 = *reinterpret_cast<const float4*>(arow + 16 * ls.chunk(1));
   float4 a2;
 #define DFWFM_MFMA_STEP(X, AX)                                                         \
-  mfma_chunk<TPW>(acc, AX, X);                                                         \
+  mfma_chunk<TPW, WA>(acc, AX, X);                                                     \
   __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                   \
   for (int q = 0; q < TPW; ++q) {                                                      \
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                 \
@@ -208,43 +283,49 @@ __device__ __forceinline__ void mlp_k_loop(f32x4 (&acc)[TPW], const float* __res
 #undef DFWFM_MFMA_STEP
 }
 
-// The split tail tile: when the layer has 4*TPW + 1 output tiles, tile T = 4*TPW is shared by the
-// four waves, wave g taking K chunks [NC*g/4, NC*(g+1)/4) of it, so every SIMD carries 6.25 tiles
-// instead of one carrying 7.  All of a wave's tail fragments are loaded with the layer's preload
-// (kTailC <= 8 chunks per wave, NC <= 32) and consumed after the main K loop.
-template <int NG = 4>
-struct TailStream {
-  static constexpr int C = kTailC * 4 / NG;  // K chunks per wave at most (layer widths <= 512)
-  int sbase, c_lo, cnt;
-  __device__ __forceinline__ void init(int layer_off, int NC, int T, int g) {
-    sbase = __builtin_amdgcn_readfirstlane((layer_off + T * NC * 64) * 16);
-    c_lo = (NC * g) / NG;
-    cnt = (NC * (g + 1)) / NG - c_lo;
-  }
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, f32x4 (&tw)[C], int voff) const {
+// mlp_k_loop with the chunk count NS fixed at compile time (every step unrolled, so each step's register
+// sets are static) and the wave's share of the split tail tile riding on the same sets: the two drain steps
+// (which fetch no chunk) fetch its fragments into the sets just freed, multiplied after the last step into
+// tpart.  Nothing of the tail is held across the layer boundary (preloaded tail fragments spilled, and a
+// spill store after the next layer's preload waits for all of it).  Needs 2 * TPW >= the wave's tail share.
+template <int TPW, int NG, int NS, bool WA>
+__device__ __forceinline__ void mlp_k_loop_s(f32x4 (&acc)[TPW], const float* __restrict__ act, int SA,
+                                             const LayerStream<TPW, 1, NG>& ls, f32x4 (&b0)[TPW],
+                                             f32x4 (&b1)[TPW], f32x4 (&b2)[TPW], int lane,
+                                             const TailStream<NG>& ts, f32x4& tpart) {
+  static_assert(NS >= 3, "static K loop: at least 3 chunks");
+  const int voff = lane * 16;
+  const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
+  float4 a0 = *reinterpret_cast<const float4*>(arow);
+  float4 a1 = *reinterpret_cast<const float4*>(arow + 16);
+  float4 a2;
 #pragma unroll
-    for (int u = 0; u < C; ++u)
-      if (u < cnt)
-        tw[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, sbase + (c_lo + u) * 1024, 0));
-  }
-  // this wave's partial product of the tail tile (two accumulators: no back-to-back dependent MFMAs)
-  __device__ __forceinline__ f32x4 mma(const float* __restrict__ act, int SA, const f32x4 (&tw)[C], int lane) const {
-    const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
-    f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
-#pragma unroll
-    for (int u = 0; u < C; ++u) {
-      if (u < cnt) {
-        const float4 a = *reinterpret_cast<const float4*>(arow + 16 * (c_lo + u));
-        f32x4& c = (u & 1) ? a1 : a0;
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, tw[u].x, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, tw[u].y, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, tw[u].z, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, tw[u].w, c, 0, 0, 0);
-      }
+  for (int i = 0; i < NS; ++i) {
+    f32x4 (&X)[TPW] = (i % 3 == 0) ? b0 : ((i % 3 == 1) ? b1 : b2);
+    f32x4 (&Z)[TPW] = (i % 3 == 0) ? b2 : ((i % 3 == 1) ? b0 : b1);
+    float4& AX = (i % 3 == 0) ? a0 : ((i % 3 == 1) ? a1 : a2);
+    float4& AZ = (i % 3 == 0) ? a2 : ((i % 3 == 1) ? a0 : a1);
+    if (i + 2 < NS) {
+      AZ = *reinterpret_cast<const float4*>(arow + 16 * (i + 2));
+      ls.load(Z, ls.c0 + i + 2, voff);
+    } else {
+      ts.template load_set<TPW>(ls.rsrc, Z, i + 2 == NS ? 0 : TPW, voff);
     }
-    return a0 + a1;
+    mfma_chunk<TPW, WA>(acc, AX, X);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    for (int q = 0; q < TPW; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TPW, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
-};
+  f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  ts.template mma_set<TPW, WA>(arow, NS % 3 == 0 ? b0 : (NS % 3 == 1 ? b1 : b2), 0, c0, c1);
+  ts.template mma_set<TPW, WA>(arow, (NS + 1) % 3 == 0 ? b0 : ((NS + 1) % 3 == 1 ? b1 : b2), TPW, c0, c1);
+  tpart = c0 + c1;
+}
+
 
 // Counter-based dropout mask (deep tower; reference nn.Dropout(0.5), model/DeepFMs.py:260-282):
 // keep element (layer, row, col) of a step iff the top 24 bits of a murmur3-finalised key

@@ -67,6 +67,7 @@ struct FwdArgs {
   int32_t SX, SY;      // LDS row strides (floats) of the two activation tiles
   int32_t W0;          // E-tile columns that must be valid (zero padded past F*D)
   int32_t tail;        // 1: NT == 4*TPW + 1 and tile 4*TPW is split by K over the four waves
+  int32_t ns;          // 25: every layer has 25 K chunks and 25 output tiles (static K loop), else 0
   int32_t flags;
   uint64_t* stamps;    // diagnostics only: [grid][kStampSlots] shader-clock stamps, normally null
   // training (flags & kTrain): activations kept for the backward
@@ -108,7 +109,7 @@ __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int
   L.bufX = o;  o += kBM * SX;
   L.bufY = o;  o += deep ? kBM * SY : 0;
   L.red = o;   o += (deep && KS == 2) ? 4 * TPW * 64 * 4 : 0;
-  L.tailr = o; o += (deep && tail) ? NG * 64 * 4 + kBM : 0;  // partials + per-row deep sums of the tail
+  L.tailr = o; o += (deep && tail) ? NG * 64 * 4 + 4 * kBM : 0;  // partials + per-(wave, row) deep sums of the tail
   L.fo = o;    o += kBM * r4(F);
   L.part2 = o; o += MT * D * 16;  // per FwFM piece, its 16 column sums
   L.dsum = o;  o += NG * kBM;

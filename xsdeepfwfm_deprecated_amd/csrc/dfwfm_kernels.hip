@@ -50,7 +50,9 @@ namespace dfwfm {
 // NG: MLP output-tile groups = waves (4: one wave per SIMD, <= 256 registers; 8: two per SIMD, <= 128
 // registers, so one workgroup issues MFMAs from two waves per SIMD while a second batch's workgroup
 // on the same CU runs its gather; the training variant, one batch in flight, keeps 256 registers)
-template <int D, int TPW, int KS, bool TRAIN, int PART, int NG>
+// NS: every layer has NS K chunks and NS output tiles (0: any) -- the K loop is then fully static and the
+// split tail tile rides on its register sets (mlp_k_loop_s)
+template <int D, int TPW, int KS, bool TRAIN, int PART, int NG, int NS>
 __global__ void __launch_bounds__(64 * NG * KS)
 __attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE))))
 fwd_kernel(FwdArgs p) {
@@ -107,7 +109,7 @@ fwd_kernel(FwdArgs p) {
   const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.fc), (short)0, p.NT * 16 * 4, 0x00020000);
   TailStream<NG> ts;
-  f32x4 tw[TailStream<NG>::C];
+  f32x4 tw[NS ? 1 : TailStream<NG>::C];  // preloaded tail fragments (NS == 0)
   constexpr int TT = NG * TPW;  // the tail tile (when p.tail)
 
   constexpr bool train = TRAIN;
@@ -131,9 +133,11 @@ fwd_kernel(FwdArgs p) {
     const float fsv = tid < nrows ? p.part_fs[b0 + tid] : 0.f;
     ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
     DFWFM_PRELOAD(ls);
-    if (tail) {
-      ts.init(0, p.NC0, TT, g);
-      ts.load(wrsrc, tw, lane * 16);
+    if constexpr (NS == 0) {
+      if (tail) {
+        ts.init(0, p.NC0, TT, g);
+        ts.load(wrsrc, tw, lane * 16);
+      }
     }
 #pragma unroll
     for (int k = 0; k < kEPT; ++k) {
@@ -387,9 +391,11 @@ fwd_kernel(FwdArgs p) {
     }
   }
   // layer 0's tail fragments once the gather rows are dead (live across the gather, they spilled)
-  if (deep && tail) {
-    ts.init(0, p.NC0, TT, g);
-    ts.load(wrsrc, tw, lane * 16);
+  if constexpr (NS == 0) {
+    if (deep && tail) {
+      ts.init(0, p.NC0, TT, g);
+      ts.load(wrsrc, tw, lane * 16);
+    }
   }
   stamp(p.stamps, 10, tid);
   __syncthreads();
@@ -449,11 +455,34 @@ fwd_kernel(FwdArgs p) {
   if (flags & kPrio) __builtin_amdgcn_s_setprio(0);
   if constexpr (train) __syncthreads();  // the dropped X_0 tile is complete before layer 1 reads it
   // ---- phase M: MLP on MFMA -------------------------------------------------
-  const int row0 = (lane >> 4) * 4;
+  // Weights are the MFMA A operand (mlp_k_loop WA): lane l holds neurons 4(l>>4) + r of sample row l&15, so
+  // a tile's four outputs of a sample leave as one 16-byte LDS store.  The accumulators start from the bias.
   const bool drop = train && (flags & kDrop) != 0;
   const uint32_t hseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
+  // this wave's biases (four per tile, 16-byte buffer loads), fetched one layer ahead: they seed the
+  // accumulators at the start of the K loop (so they are dead during it)
+  auto load_bias = [&](f32x4 (&bq)[TPW], int h, int nq) {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      int t = g + NG * j;
+      t = t < p.NT ? t : p.NT - 1;
+      // lane part nq*4 in a VGPR, the tile / layer part in the scalar offset (per-tile lane offsets were
+      // hoisted out of the layer loop, spilled, and every reload waited for the whole preload)
+      bq[j] = kh == 0 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                            brsrc, nq * 4, __builtin_amdgcn_readfirstlane((h * p.NT + t) * 64), 0))
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  f32x4 bq[TPW];
+  load_bias(bq, 0, 4 * (lane >> 4));
   int layer_off = 0;  // float4 offset of layer h in wpack
   for (int h = 0; h < p.H; ++h) {
+    // the lane-derived epilogue values are recomputed per layer: hoisted out of the loop they stay live across
+    // it and spill, and a reload after the next layer's preload waits for the whole preload (vmcnt order)
+    int lv = lane;
+    asm volatile("" : "+v"(lv));
+    const int rowl = lv & 15;
+    const int nq = 4 * (lv >> 4);
     const bool even = (h & 1) == 0;
     const float* in = even ? bufX : bufY;
     const int SA = even ? SX : SY;
@@ -461,31 +490,27 @@ fwd_kernel(FwdArgs p) {
     const int SO = even ? SY : SX;
     const int NC = h == 0 ? p.NC0 : p.NT;
     const bool last = h == p.H - 1;
-    // epilogue operands, fetched before the K loop so they arrive under it; buffer loads (scalar layer
-    // offset, 32-bit lane offset): per-tile 64-bit addresses would be kept across the layer loop
-    const int boff = h * p.NT * 16 * 4;
-    float bn[TPW], wf[TPW];
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      int t = g + NG * j;
-      t = t < p.NT ? t : p.NT - 1;
-      const int n4 = (t * 16 + (lane & 15)) * 4;
-      bn[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, n4, boff, 0));
-      wf[j] = last ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(frsrc, n4, 0, 0)) : 0.f;
-    }
+    // the tail tile's bias (one neuron per lane of waves 0..3), fetched before the K loop
+    const int boff = __builtin_amdgcn_readfirstlane((h * p.NT + TT) * 64 + (g & 3) * 4);
+    const int ntail = TT * 16 + nq + (g & 3);
+    const float bn_t = tail ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, nq * 4, boff, 0))
+                            : 0.f;
 
-    float bn_t = 0.f, wf_t = 0.f;
-    if (tail) {
-      const int n4 = (TT * 16 + (lane & 15)) * 4;
-      bn_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, n4, boff, 0));
-      wf_t = last ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(frsrc, n4, 0, 0)) : 0.f;
-    }
-
-    // the tail tile's share first: its fragments (loaded with the preload) are then dead during the
-    // K loop, which runs at the register budget
-    if (tail) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.mma(in, SA, tw, lane);
     f32x4 acc[TPW];
-    DFWFM_KLOOP(acc, in, SA, ls);
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) acc[j] = bq[j];  // the K loop accumulates onto the bias
+    if constexpr (NS > 0) {
+      // the tail tile's share rides on the K loop's register sets
+      if (tail) ts.init(layer_off, NC, TT, g);
+      else ts.cnt = 0;
+      f32x4 tp;
+      mlp_k_loop_s<TPW, NG, NS, true>(acc, in, SA, ls, wb0, wb1, wb2, lane, ts, tp);
+      if (tail) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = tp;
+    } else {
+      // the tail tile's share first: its fragments (loaded with the preload) are then dead during the K loop
+      if (tail) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.template mma<true>(in, SA, tw, lane);
+      mlp_k_loop<TPW, KS, NG, true, true>(acc, in, SA, ls, wb0, wb1, wb2, lane);
+    }
     if (h == 0) stamp(p.stamps, 12, tid);
     if constexpr (KS == 2) {
       if (kh == 1) {
@@ -498,58 +523,62 @@ fwd_kernel(FwdArgs p) {
         for (int j = 0; j < TPW; ++j) acc[j] += red[(g * TPW + j) * 64 + lane];
       }
     }
-    float dpart[4] = {0.f, 0.f, 0.f, 0.f};  // last layer: this lane's share of deep[b] (not live across layers)
+    float dpart = 0.f;  // last layer: this lane's share of deep[row] (not live across layers)
     if (kh == 0) {
-      // C/D layout: col = lane&15 (neuron), row = (lane>>4)*4 + r (sample)
+      float* orow = outa + rowl * SO + nq;  // + t*16 (wave-uniform) per tile
 #pragma unroll
       for (int j = 0; j < TPW; ++j) {
-        const int t = g + NG * j;
+        const int t = g + NG * j;  // wave-uniform
         if (t < p.NT) {
-          const int n = t * 16 + (lane & 15);
-          const bool valid = n < p.N;  // padded neurons stay exactly 0 (bias/fc pads are 0)
+          float v[4];
+          if (t * 16 + 16 <= p.N) {  // no padded neuron in this tile
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = relu_keep_nan(acc[j][r]);
+          } else {  // padded neurons stay exactly 0 (bias / fc pads are 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = nq + r < p.N - t * 16 ? relu_keep_nan(acc[j][r]) : 0.f;
+          }
           if constexpr (train) {
+            // dropout after the ReLU (net_1_linear_{h}_dropout, :416-426)
+            if (drop) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              // dropout after the ReLU (net_1_linear_{h}_dropout, :416-426); the tile goes to LDS also
-              // in the last layer, from where X_H is saved for the backward
-              float v = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
-              if (drop) v = dropout_keep(hseed, h + 1, b0 + row0 + r, n, p.drop_p) ? v * p.drop_scale : 0.f;
-              outa[(row0 + r) * SO + n] = v;
-              if (last) dpart[r] = fmaf(v, wf[j], dpart[r]);
+              for (int r = 0; r < 4; ++r)
+                v[r] = dropout_keep(hseed, h + 1, b0 + rowl, t * 16 + nq + r, p.drop_p) ? v[r] * p.drop_scale : 0.f;
             }
-          } else if (!last) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) outa[(row0 + r) * SO + n] = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float v = valid ? relu_keep_nan(acc[j][r] + bn[j]) : 0.f;
-              dpart[r] = fmaf(v, wf[j], dpart[r]);
-            }
+          }
+          // the tile goes to LDS also in the last layer of a training step, from where X_H is saved
+          if (!last || train) *reinterpret_cast<f32x4*>(orow + t * 16) = f32x4{v[0], v[1], v[2], v[3]};
+          if (last) {
+            const f32x4 wf =
+                __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(frsrc, nq * 4, t * 64, 0));
+            dpart = fmaf(v[0], wf[0], dpart);
+            dpart = fmaf(v[1], wf[1], dpart);
+            dpart = fmaf(v[2], wf[2], dpart);
+            dpart = fmaf(v[3], wf[3], dpart);
           }
         }
       }
     }
     if (last && kh == 0) {
-      // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the 16 lanes sharing (lane>>4), then (after the
-      // final barrier) the NG groups
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dpart[r] = sum16(dpart[r]);
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dsum[g * kBM + row0 + r] = dpart[r];
-      }
+      // deep[b] = sum_n h_last[b, n] * fc[n]: reduce the four lanes sharing the row, then (after the final
+      // barrier) the NG groups
+      dpart += __shfl_xor(dpart, 16);
+      dpart += __shfl_xor(dpart, 32);
+      if (lane < 16) dsum[g * kBM + rowl] = dpart;
     }
-    // next layer's first chunks go out now, ahead of the barrier -- but after the epilogue: once they
-    // are issued, any wait on a vector-memory result (a bias, a spill reload) waits for them too
+    // next layer's first chunks and biases go out now, ahead of the barrier -- but after the epilogue: once
+    // they are issued, any wait on a vector-memory result (a spill reload) waits for them too
     layer_off += p.NT * NC * 64;
     if (!last) {
       ls.init(wrsrc, layer_off, p.NT, p.NT, g, kh);
       DFWFM_PRELOAD(ls);
-      if (tail) {
-        ts.init(layer_off, p.NT, TT, g);
-        ts.load(wrsrc, tw, lane * 16);
+      if constexpr (NS == 0) {
+        if (tail) {
+          ts.init(layer_off, p.NT, TT, g);
+          ts.load(wrsrc, tw, lane * 16);
+        }
       }
+      load_bias(bq, h + 1, nq);
     }
     if constexpr (train) {
       // this layer's input X_h for the backward, from LDS (intact until the next layer's epilogue):
@@ -562,27 +591,30 @@ fwd_kernel(FwdArgs p) {
     if (h == 0) stamp(p.stamps, 13, tid);
     __syncthreads();
     if (tail) {
-      // the tail tile: wave g < 4 finishes row (lane>>4)*4 + g of it from the NG partial products
+      // the tail tile: wave g < 4 finishes neuron TT*16 + nq + g of row rowl from the NG partial products
       if (g < 4) {
-        const int n = TT * 16 + (lane & 15);
-        const bool valid = n < p.N;
-        const int rr = row0 + g;
+        float* orow_t = outa + rowl * SO + nq;
+        const bool valid = ntail < p.N;
         const float* tp = tailr + lane * 4 + g;
         float sum = tp[0];
 #pragma unroll
         for (int w = 1; w < NG; ++w) sum += tp[w * 256];
         float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
         if constexpr (train) {
-          if (drop) v = dropout_keep(hseed, h + 1, b0 + rr, n, p.drop_p) ? v * p.drop_scale : 0.f;
-          if (last) outa[rr * SO + n] = v;  // X_H is saved from LDS
+          if (drop) v = dropout_keep(hseed, h + 1, b0 + rowl, ntail, p.drop_p) ? v * p.drop_scale : 0.f;
+          if (last) orow_t[TT * 16 + g] = v;  // X_H is saved from LDS
         }
         if (!last) {
-          outa[rr * SO + n] = v;
+          orow_t[TT * 16 + g] = v;
         } else {
-          // the tail's share of deep[b] for row rr, summed over its 16 columns; added last in the final
-          // combine, so a row's logit does not depend on its slot in the tile
-          const float c = sum16(v * wf_t);
-          if ((lane & 15) == 0) tailr[NG * 64 * 4 + rr] = c;
+          // the tail's share of deep[b]: its four neurons of this wave, reduced over the lane groups, one slot
+          // per (wave, row); added last in the final combine, so a row's logit does not depend on its slot
+          const float wf_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                 frsrc, nq * 4, __builtin_amdgcn_readfirstlane(TT * 64 + g * 4), 0));
+          float c = v * wf_t;
+          c += __shfl_xor(c, 16);
+          c += __shfl_xor(c, 32);
+          if (lane < 16) tailr[NG * 64 * 4 + g * kBM + rowl] = c;
         }
       }
       if (!last) __syncthreads();
@@ -603,7 +635,8 @@ fwd_kernel(FwdArgs p) {
     float deepv = dsum[tid];
 #pragma unroll
     for (int w = 1; w < NG; ++w) deepv += dsum[w * kBM + tid];
-    if (tail) deepv += tailr[NG * 64 * 4 + tid];
+    if (tail) deepv += ((tailr[NG * 64 * 4 + tid] + tailr[NG * 64 * 4 + kBM + tid]) +
+                        tailr[NG * 64 * 4 + 2 * kBM + tid]) + tailr[NG * 64 * 4 + 3 * kBM + tid];
     p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
   stamp(p.stamps, 8, tid);
@@ -690,7 +723,10 @@ __global__ void __launch_bounds__(256) pack_dense_kernel(const PackList L) {
 // ---------------------------------------------------------------------------
 template <int D, int TPW, int KS, bool TRAIN, int PART = 0, int NG = 4>
 static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, hipStream_t s) {
-  auto k = fwd_kernel<D, TPW, KS, TRAIN, PART, NG>;
+  // the static 25-chunk form (3x400 MLP over 39x10 embeddings: 25 tiles = 8 waves x 3 + the split 25th)
+  constexpr bool S25 = NG == 8 && TPW == 3 && KS == 1 && PART != 1;
+  auto k = (S25 && a.ns == 25) ? fwd_kernel<D, TPW, KS, TRAIN, PART, NG, S25 ? 25 : 0>
+                               : fwd_kernel<D, TPW, KS, TRAIN, PART, NG, 0>;
   {
     hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
     if (e != hipSuccess) return e;
