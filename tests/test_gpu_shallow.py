@@ -1,0 +1,104 @@
+"""GPU: the forward without a deep tower (shallow_kernel, csrc/dfwfm_shallow.hip) -- the FwFM-only config
+of BASELINE configs[0] -- against the oracle, and bit-identical to the fused kernel's shallow path
+(DFWFM_SHALLOW=0, read at model creation)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import logit_close_scaled, model_kwargs
+from oracle import dfwfm_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(F, num, D, *, fwlw=0, lw=1, qr=0, qr_op="mult", fm=0, logit=0, bag=0, B=300, seed=0, big=False):
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    if big:
+        sizes = [1] * num + list(synth.CRITEO_FEATURE_SIZES[13:13 + F - num])
+    else:
+        sizes = [1] * num + [int(x) for x in 40 + (np.arange(F - num) * 53) % 700]
+    second = not logit
+    cfg = dict(field_size=F, feature_sizes=sizes, embedding_size=D, use_fwfm=int(second and not fm),
+               use_fm=int(fm), use_logit=int(logit), use_deep=0, use_lw=lw, use_fwlw=fwlw, h_depth=3,
+               deep_nodes=400, numerical=num, embedding_bag=int(bag or qr), qr_flag=qr, qr_operation=qr_op,
+               qr_collisions=4, qr_threshold=200)
+    m = DeepFMs(**model_kwargs(cfg))
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    params = synth.synth_state(shapes, F, D, 400, second, False, seed=seed)
+    xi, xv = synth.synth_inputs(sizes, num, B, seed=seed + 1)
+    return cfg, params, xi, xv
+
+
+def _model(cfg, params, dev, monkeypatch, shallow):
+    from xsdeepfwfm_deprecated_amd import DeepFMs
+    monkeypatch.setenv("DFWFM_SHALLOW", "1" if shallow else "0")
+    m = DeepFMs(**model_kwargs(cfg))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        m._sync_engine(dev)  # the engine (and its kernel choice) is created here
+    return m
+
+
+def _run(m, xi, xv, dev):
+    with torch.no_grad():
+        out = m(torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev))
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+CASES = [
+    dict(F=39, num=13, D=10),                           # BASELINE configs[0]: FwFM + lw
+    dict(F=39, num=13, D=10, lw=0),                     # FwFM, plain first-order sum
+    dict(F=39, num=13, D=10, fwlw=1),                   # fwlw first order
+    dict(F=39, num=13, D=10, fwlw=1, lw=0),
+    dict(F=39, num=13, D=10, qr=1),                     # QR mult (tables of > 200 rows)
+    dict(F=39, num=13, D=10, qr=1, qr_op="add", fwlw=1),
+    dict(F=39, num=13, D=10, bag=1),                    # EmbeddingBag
+    dict(F=39, num=13, D=10, fm=1),                     # FM second order
+    dict(F=39, num=13, D=10, logit=1),                  # first order only (no E gather)
+    dict(F=39, num=13, D=4), dict(F=39, num=13, D=8), dict(F=39, num=13, D=16), dict(F=39, num=13, D=32),
+    dict(F=39, num=13, D=32, qr=1),
+    dict(F=64, num=16, D=10), dict(F=64, num=0, D=10),  # four FwFM row tiles; no numerical field
+    dict(F=20, num=20, D=10),                           # only numerical fields (no Xi)
+    dict(F=5, num=2, D=10), dict(F=48, num=13, D=16, qr=1),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_shallow_kernel_matches_oracle_and_fused(gpu, monkeypatch, case):
+    cfg, params, xi, xv = _case(**case, seed=len(str(case)))
+    got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    fused = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
+    assert np.array_equal(got, fused)
+
+
+@pytest.mark.parametrize("B", [1, 15, 16, 17, 255, 4096 + 3])
+def test_shallow_kernel_ragged_batches(gpu, monkeypatch, B):
+    cfg, params, xi, xv = _case(39, 13, 10, B=B, seed=B)
+    got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    # a row's logit does not depend on its tile or slot
+    one = _run(_model(cfg, params, gpu, monkeypatch, True), xi[B - 1:], xv[B - 1:], gpu)
+    assert one[0] == got[B - 1]
+
+
+def test_shallow_kernel_full_size_tables(gpu, monkeypatch):
+    """Criteo-39 field sizes (1.33 M rows), B = 4096: the bench workload."""
+    cfg, params, xi, xv = _case(39, 13, 10, B=4096, big=True, seed=7)
+    got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+
+
+@pytest.mark.parametrize("bad", [-1, "n"])
+def test_shallow_kernel_index_out_of_range_raises(gpu, monkeypatch, bad):
+    cfg, params, xi, xv = _case(39, 13, 10, B=64, seed=3)
+    xi = xi.copy()
+    xi[37, 5] = -1 if bad == -1 else cfg["feature_sizes"][13 + 5]
+    m = _model(cfg, params, gpu, monkeypatch, True)
+    with pytest.raises(IndexError):
+        _run(m, xi, xv, gpu)

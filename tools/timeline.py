@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--streams", type=int, default=2)
 ap.add_argument("--graph-steps", type=int, default=20)
 ap.add_argument("--replays", type=int, default=5)
+ap.add_argument("--fwfm", action="store_true", help="FwFM-only model (use_deep=0)")
 a = ap.parse_args()
 os.environ["DFWFM_DIAG_STAMPS"] = "1"
 os.environ["DFWFM_DIAG_RING"] = str(a.streams * a.graph_steps)
@@ -26,10 +27,11 @@ from xsdeepfwfm_deprecated_amd import DeepFMs, _lib, synth  # noqa: E402
 B = 4096
 dev = torch.device("cuda:0")
 sizes = synth.CRITEO_FEATURE_SIZES
-m = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1,
+m = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=0 if a.fwfm else 1, use_lw=1,
             numerical=13, use_cuda=True)
 shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
-m.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_state(shapes, 39, 10, 400, True, True).items()})
+m.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_state(shapes, 39, 10, 400, True, True).items()
+                   if k in shapes})
 m = m.to(dev).eval()
 m.strict_index_check = False
 S, G = a.streams, a.graph_steps
@@ -72,7 +74,7 @@ base = t0.min()
 t0 = (t0 - base) * 10  # ns
 t1 = (t1 - base) * 10
 mt = st[:, :, :14].astype(np.int64)
-frac_mlp = (mt[:, :, 3] - mt[:, :, 0]) / np.maximum(1, mt[:, :, 8] - mt[:, :, 0])
+frac_mlp = ((mt[:, :, 3] - mt[:, :, 0]) / np.maximum(1, mt[:, :, 8] - mt[:, :, 0])) if not a.fwfm else np.ones_like(mt[:, :, 0], dtype=float)
 tm = t0 + (t1 - t0) * frac_mlp  # MLP start, ns
 
 print(f"launches {S}x{G}, {grid} workgroups each, distinct CUs seen {len(np.unique(cu))}")
@@ -112,6 +114,9 @@ print(f"  workgroups per CU over all launches: min {per_cu.min()} max {per_cu.ma
 names = [("stage", 0, 1), ("gather", 1, 2), ("fwlw", 2, 9), ("FwFM MFMA", 9, 10), ("barrier", 10, 11),
          ("sums", 11, 3), ("MLP L1 K loop", 3, 12), ("L1 epilogue", 12, 13), ("L1 barrier", 13, 4),
          ("MLP L2", 4, 5), ("MLP L3", 5, 6), ("combine", 6, 8)]
+if a.fwfm:
+    names = [("stage", 0, 1), ("gather", 1, 2), ("fwlw", 2, 9), ("FwFM MFMA", 9, 10), ("barrier", 10, 11),
+             ("sums + store", 11, 8)]
 sel = mt[2 * S:(G - 2) * S]
 tot = np.median(sel[:, :, 8] - sel[:, :, 0])
 print(f"phase medians (shader cycles), total {tot:.0f}:")

@@ -26,6 +26,8 @@ struct dfwfm_model {
   int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
   size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
   int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
+  int shallow;         // no deep tower: shallow_kernel (dfwfm_shallow.hip) runs the inference forward
+  int big_tables;      // some table has >= 2^31 rows (shallow_kernel then yields to fwd_kernel)
   uint8_t fw_list4[kMaxPieces], fw_off4[5];  // FwFM pieces per wave, 4- and 8-wave launches (fw_schedule)
   uint8_t fw_list8[kMaxPieces], fw_off8[9];
   // device state (owned)
@@ -247,6 +249,10 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   // fused launch (50.4 vs 43.0 us per batch alone, 43.4 vs 35.5 with two batches in flight): under a
   // co-resident MLP's weight stream the gather launch's dependent loads wait ~3x longer, and in the
   // fused kernel that wait is hidden behind the other workgroup's MLP instead of serialised
+  // no deep tower: the latency-oriented shallow kernel (dfwfm_shallow.hip); DFWFM_SHALLOW=0 keeps the
+  // fused kernel's four-wave shallow path (A/B and the bit-identity test)
+  const char* sh = getenv("DFWFM_SHALLOW");
+  m->shallow = (!c.use_deep && (!sh || atoi(sh) != 0)) ? 1 : 0;
   const char* sp = getenv("DFWFM_SPLIT");
   m->split = (c.use_deep && m->KS == 1 && sp && atoi(sp) != 0) ? 1 : 0;
   if (m->lds_bytes > 160 * 1024 || m->lds_inf > 160 * 1024) {
@@ -324,6 +330,12 @@ int dfwfm_model_set_tables(dfwfm_model* m, const dfwfm_field_tables* t, int32_t 
   for (int f = 0; f < n; ++f)
     if (host[f].c > 0) host[f].n = (host[f].n + host[f].c - 1) / host[f].c * host[f].c;
   memcpy(m->h_fields, host, sizeof(FieldDev) * n);
+  m->flags &= ~kHasQR;
+  m->big_tables = 0;
+  for (int f = 0; f < n; ++f) {
+    if (host[f].c > 0) m->flags |= kHasQR;
+    if (host[f].n > 0x7fffffff) m->big_tables = 1;  // shallow_kernel indexes rows in 32 bits
+  }
   HIP_TRY(hipMemcpyAsync(m->d_fields, host, sizeof(FieldDev) * n, hipMemcpyHostToDevice, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // `host` is a stack buffer
   m->tables_set = true;
@@ -522,7 +534,9 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
-  hipError_t e = launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf, (hipStream_t)stream);
+  hipError_t e = (m->shallow && !m->big_tables) ? launch_shallow(a, m->D, m->lds_gather, (hipStream_t)stream)
+                            : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
+                                             (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
 }

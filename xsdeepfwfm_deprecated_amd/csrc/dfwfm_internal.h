@@ -27,6 +27,7 @@ constexpr int kNeedE = 32;     // second-order / deep embeddings are gathered
 constexpr int kTrain = 64;     // save the activations the backward needs (FwdArgs::sv_*)
 constexpr int kDrop = 128;     // dropout on the deep tower (train only)
 constexpr int kPrio = 256;     // raise the wave priority for the phases before the MLP (A/B: DFWFM_PRIO)
+constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables; shallow_kernel's QR loads)
 constexpr int kMaxH = 16;      // hidden layers
 
 // Device copy of dfwfm_field_tables (same field order and sizes); for QR fields
@@ -321,6 +322,8 @@ hipError_t launch_metrics(const float* z, const float* y, int64_t n, double* out
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s);
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
+// the forward without a deep tower (dfwfm_shallow.hip); lds: lds_layout(..., deep = false)
+hipError_t launch_shallow(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 // per-embedding-size launchers, each compiled in its own translation unit (-DDFWFM_KD=<D>)
 #define DFWFM_PER_D_CAT2(a, b) a##b

@@ -447,6 +447,8 @@ fwd_kernel(FwdArgs p) {
     } else {
       if (tid < kBM && b0 + tid < p.batch) p.out[b0 + tid] = fs[tid] + p.bias[0];
     }
+    stamp(p.stamps, 8, tid);
+    stamp_end_rt(p.stamps, tid);
     return;
   }
   }  // PART != 2
