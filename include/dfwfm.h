@@ -125,6 +125,17 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
                      int64_t xv_stride, int64_t batch, float* out, void* workspace, size_t ws_bytes,
                      void* stream);
 
+/* Pruned deep tower (BASELINE configs[3]; reference masks model/DeepFMs.py:647-673, whose forward stays
+ * dense): compacts every hidden layer's nonzero weights (the tensors of the last
+ * dfwfm_model_set_dense) into a per-neuron (k, w) list on the device and, when the nonzero fraction
+ * of the hidden layers is <= max_density, makes dfwfm_forward_ws run the gather launch followed by a
+ * sparse MLP over those lists (dfwfm_forward_workspace_bytes then reports the gather workspace).
+ * *enabled = 1 when the sparse path is on.  Synchronises `stream` (reads the nonzero count); call it
+ * after a weight update, not per forward.  dfwfm_model_set_dense turns the path off again until the
+ * next call; max_density <= 0 turns it off.  Logits agree with the dense forward to fp32 summation
+ * order (1e-5 bar). */
+int dfwfm_model_build_sparse_mlp(dfwfm_model* m, double max_density, int32_t* enabled, void* stream);
+
 /* ---- training step (reference model/DeepFMs.py:553-637) ---------------------------------- */
 
 /* Forward of a training step: as dfwfm_forward, and additionally keeps (in model-owned device

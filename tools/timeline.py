@@ -115,7 +115,8 @@ names = [("stage", 0, 1), ("gather", 1, 2), ("fwlw", 2, 9), ("FwFM MFMA", 9, 10)
          ("sums", 11, 3), ("MLP L1 K loop", 3, 12), ("L1 epilogue", 12, 13), ("L1 barrier", 13, 4),
          ("MLP L2", 4, 5), ("MLP L3", 5, 6), ("combine", 6, 8)]
 if a.fwfm:
-    names = [("stage", 0, 1), ("gather", 1, 2), ("fwlw", 2, 9), ("FwFM MFMA", 9, 10), ("barrier", 10, 11),
+    names = [("stage", 0, 1), ("gather", 1, 2), ("fwlw", 2, 9), ("FwFM MFMA", 9, 10), ("  piece 1 loads+MFMA issue", 9, 3),
+             ("  piece 1 epilogue", 3, 4), ("  piece 2", 4, 5), ("  piece 3", 5, 6), ("barrier", 10, 11),
              ("sums + store", 11, 8)]
 sel = mt[2 * S:(G - 2) * S]
 tot = np.median(sel[:, :, 8] - sel[:, :, 0])

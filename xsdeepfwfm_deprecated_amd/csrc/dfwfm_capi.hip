@@ -28,6 +28,15 @@ struct dfwfm_model {
   int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
   int shallow;         // no deep tower: shallow_kernel (dfwfm_shallow.hip) runs the inference forward
   int big_tables;      // some table has >= 2^31 rows (shallow_kernel then yields to fwd_kernel)
+  // sparse deep tower (dfwfm_model_build_sparse_mlp): ELL of the pruned weights, used by dfwfm_forward_ws
+  int sp;                          // enabled (cleared by set_dense: the ELL is then stale)
+  const float* lin_w[kMaxH];       // the caller's weights from the last set_dense
+  int2* d_ell;
+  int32_t* d_cnt;                  // [H][N]
+  int32_t* d_spstat;               // [2]
+  int spW[kMaxH];
+  int64_t spoff[kMaxH];
+  double sp_density;               // nonzero fraction of the last build
   uint8_t fw_list4[kMaxPieces], fw_off4[5];  // FwFM pieces per wave, 4- and 8-wave launches (fw_schedule)
   uint8_t fw_list8[kMaxPieces], fw_off8[9];
   // device state (owned)
@@ -112,7 +121,8 @@ int dev_alloc(T** p, size_t count) {
 void free_model(dfwfm_model* m) {
   if (!m) return;
   void* ptrs[] = {m->d_fields, m->d_upack, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
-                  m->d_lw,     m->d_bias,  m->d_stamps,  m->d_wtpack, m->d_rsk,   m->d_ws};
+                  m->d_lw,     m->d_bias,  m->d_stamps,  m->d_wtpack, m->d_rsk,   m->d_ws,
+                  m->d_ell,    m->d_cnt,   m->d_spstat};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -393,6 +403,8 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
   hipError_t e = launch_pack_list(L, blocks, s);
   if (e != hipSuccess) return hip_fail(e, "pack launch");
   m->dense_set = true;
+  m->sp = 0;  // new weights: the sparse tower's ELL is stale until rebuilt
+  for (int h = 0; h < m->H; ++h) m->lin_w[h] = lin_w ? lin_w[h] : nullptr;
   return DFWFM_OK;
 }
 
@@ -543,14 +555,14 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
 
 int dfwfm_forward_workspace_bytes(dfwfm_model* m, int64_t batch, size_t* bytes) {
   if (!m || !bytes || batch < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
-  *bytes = m->split ? split_ws_bytes(m, batch) : 0;
+  *bytes = (m->split || m->sp) ? split_ws_bytes(m, batch) : 0;
   return DFWFM_OK;
 }
 
 int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
                      int64_t batch, float* out, void* workspace, size_t ws_bytes, void* stream) {
   if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
-  if (!m->split || !workspace) return dfwfm_forward(m, xi, xi_stride, xv, xv_stride, batch, out, stream);
+  if ((!m->split && !m->sp) || !workspace) return dfwfm_forward(m, xi, xi_stride, xv, xv_stride, batch, out, stream);
   int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
   if (rc != DFWFM_OK || batch == 0) return rc;
   if (ws_bytes < split_ws_bytes(m, batch))
@@ -565,9 +577,83 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
   a.part_fs = a.part_e + split_e_floats(m, batch);
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
+  if (m->sp) {
+    // pruned deep tower: the gather launch, then the sparse MLP over the ELL (dfwfm_spmlp.hip)
+    hipError_t e = launch_forward_gather(a, m->D, m->lds_gather, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gather launch");
+    SpMlpArgs sa;
+    memset(&sa, 0, sizeof sa);
+    sa.part_e = a.part_e;
+    sa.part_fs = a.part_fs;
+    sa.part_stride = a.part_stride;
+    sa.K0p = a.part_stride;
+    sa.ell = m->d_ell;
+    sa.cnt = m->d_cnt;
+    for (int h = 0; h < m->H; ++h) {
+      sa.W[h] = m->spW[h];
+      sa.off[h] = m->spoff[h];
+    }
+    sa.mlp_b = m->d_mlp_b;
+    sa.fc = m->d_fc;
+    sa.bias = m->d_bias;
+    sa.out = out;
+    sa.batch = batch;
+    sa.H = m->H;
+    sa.N = m->N;
+    sa.NT = m->NT;
+    e = launch_sparse_mlp(sa, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "sparse MLP launch");
+    return DFWFM_OK;
+  }
   hipError_t e = launch_forward_split(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->NG, m->lds_gather, m->lds_inf,
                                       (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
+  return DFWFM_OK;
+}
+
+int dfwfm_model_build_sparse_mlp(dfwfm_model* m, double max_density, int32_t* enabled, void* stream) {
+  if (!m || !enabled) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  *enabled = 0;
+  m->sp = 0;
+  if (!m->dense_set) return fail(DFWFM_ERR_STATE, "set_dense must precede build_sparse_mlp");
+  if (m->H == 0 || max_density <= 0.0) return DFWFM_OK;
+  for (int h = 0; h < m->H; ++h)
+    if (!m->lin_w[h]) return fail(DFWFM_ERR_STATE, "layer %d weight unknown", h);
+  if (sparse_mlp_lds_bytes(m->NC0 * 16, m->N) > 160 * 1024) return DFWFM_OK;  // tile does not fit: dense
+  hipStream_t s = (hipStream_t)stream;
+  EllArgs a;
+  memset(&a, 0, sizeof a);
+  int64_t total = 0, dense = 0;
+  for (int h = 0; h < m->H; ++h) {
+    const int K = h == 0 ? m->F * m->D : m->N;
+    a.w[h] = m->lin_w[h];
+    a.K[h] = K;
+    a.W[h] = (K + kEllPad - 1) / kEllPad * kEllPad;
+    a.off[h] = total;
+    m->spW[h] = a.W[h];
+    m->spoff[h] = total;
+    total += (int64_t)m->N * a.W[h];
+    dense += (int64_t)m->N * K;
+  }
+  if (!m->d_ell) {
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_ell), sizeof(int2) * (size_t)total));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_cnt), sizeof(int32_t) * (size_t)m->H * m->N));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_spstat), sizeof(int32_t) * 2));
+  }
+  a.ell = m->d_ell;
+  a.cnt = m->d_cnt;
+  a.stat = m->d_spstat;
+  a.N = m->N;
+  a.H = m->H;
+  HIP_TRY(hipMemsetAsync(m->d_spstat, 0, sizeof(int32_t) * 2, s));
+  hipError_t e = launch_ell_build(a, m->H * m->N, s);
+  if (e != hipSuccess) return hip_fail(e, "ELL build launch");
+  int32_t st[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(st, m->d_spstat, sizeof st, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  m->sp_density = dense > 0 ? (double)st[1] / (double)dense : 1.0;
+  m->sp = m->sp_density <= max_density ? 1 : 0;
+  *enabled = m->sp;
   return DFWFM_OK;
 }
 

@@ -236,6 +236,38 @@ hipError_t launch_sparse_grads(const SparseArgs& a, int64_t* out_dest, float* ou
 hipError_t launch_sparse_apply(float* grad, int w, const int64_t* dest, const float* rows, const int32_t* count,
                                int64_t cap, hipStream_t s);
 
+// Sparse deep tower (dfwfm_spmlp.hip): per layer, each neuron's nonzero (k, w bits) pairs in k order,
+// padded with (0, 0) to a multiple of kEllPad entries; row stride W[l] entries.
+constexpr int kEllPad = 16;
+struct EllArgs {
+  const float* w[kMaxH];   // nn.Linear weights [N][K_l], row-major (the caller's tensors)
+  int32_t K[kMaxH];
+  int32_t W[kMaxH];        // entries per row of layer l (>= K_l, multiple of kEllPad)
+  int64_t off[kMaxH];      // first entry of layer l
+  int2* ell;
+  int32_t* cnt;            // [H][N] padded pair counts
+  int32_t* stat;           // [2]: max row count, total nonzeros (atomics; zeroed by the caller)
+  int32_t N, H;
+};
+struct SpMlpArgs {
+  const float* part_e;     // [B][part_stride] E rows of the gather launch (zero padded past F*D)
+  const float* part_fs;    // [B] first + second order
+  int32_t part_stride, K0p;  // K0p = columns of part_e the first layer may read (part_stride)
+  const int2* ell;
+  const int32_t* cnt;
+  int32_t W[kMaxH];
+  int64_t off[kMaxH];
+  const float* mlp_b;      // [H][NT*16] padded biases
+  const float* fc;         // [NT*16]
+  const float* bias;       // [1]
+  float* out;
+  int64_t batch;
+  int32_t H, N, NT;
+};
+hipError_t launch_ell_build(const EllArgs& a, int rows, hipStream_t s);
+hipError_t launch_sparse_mlp(const SpMlpArgs& a, hipStream_t s);
+size_t sparse_mlp_lds_bytes(int K0p, int N);
+
 // dW_l += G_l^T X_{l-1} and db_l += sum_b G_l for every layer in one launch.
 struct DwArgs {
   const float* G[kMaxH + 1];
@@ -322,6 +354,8 @@ hipError_t launch_metrics(const float* z, const float* y, int64_t n, double* out
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s);
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
+// the split forward's first launch alone (gather + shallow part -> a.part_e / a.part_fs)
+hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream_t s);
 // the forward without a deep tower (dfwfm_shallow.hip); lds: lds_layout(..., deep = false)
 hipError_t launch_shallow(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
@@ -332,6 +366,7 @@ hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 #define DFWFM_DECL_PER_D(D)                                                                                   \
   hipError_t launch_forward_d##D(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s);        \
   hipError_t launch_forward_split_d##D(const FwdArgs& a, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s); \
+  hipError_t launch_forward_gather_d##D(const FwdArgs& a, size_t lds1, hipStream_t s);                      \
   hipError_t launch_backward_d##D(const BwdArgs& a, int tpw, int ng, size_t lds, hipStream_t s);
 DFWFM_DECL_PER_D(4)
 DFWFM_DECL_PER_D(8)

@@ -806,6 +806,9 @@ hipError_t DFWFM_PER_D(launch_forward_split_d)(const FwdArgs& a, int tpw, int ng
                                                hipStream_t s) {
   return launch_split_d<DFWFM_KD>(a, tpw, ng, lds1, lds2, s);
 }
+hipError_t DFWFM_PER_D(launch_forward_gather_d)(const FwdArgs& a, size_t lds1, hipStream_t s) {
+  return launch_fwd_t<DFWFM_KD, 1, 1, false, 1, 4>(a, lds1, s);
+}
 #else
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s) {
   switch (D) {
@@ -814,6 +817,17 @@ hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t
     case 10: return launch_forward_split_d10(a, tpw, ng, lds1, lds2, s);
     case 16: return launch_forward_split_d16(a, tpw, ng, lds1, lds2, s);
     case 32: return launch_forward_split_d32(a, tpw, ng, lds1, lds2, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream_t s) {
+  switch (D) {
+    case 4: return launch_forward_gather_d4(a, lds1, s);
+    case 8: return launch_forward_gather_d8(a, lds1, s);
+    case 10: return launch_forward_gather_d10(a, lds1, s);
+    case 16: return launch_forward_gather_d16(a, lds1, s);
+    case 32: return launch_forward_gather_d32(a, lds1, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -309,6 +309,7 @@ shallow_kernel(FwdArgs p) {
 #pragma unroll
       for (int s = 0; s < kSMax; ++s)
         if (s >= 4 * m && s < S) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+      if (pi == p_lo) stamp(p.stamps, 3, tid);  // diagnostics: first piece's MFMAs issued
       float v = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -319,6 +320,7 @@ shallow_kernel(FwdArgs p) {
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
       if (lane < 16) part2[pc * 16 + lane] = v;
+      if (pi - p_lo < 4) stamp(p.stamps, 4 + pi - p_lo, tid);  // diagnostics: piece ends (slots 4-7)
     }
   }
   stamp(p.stamps, 10, tid);

@@ -94,11 +94,28 @@ class ForwardEngine:
         H = len(lin_w)
         W = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_w])
         B = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_b])
+        self.__dict__.pop("_ws_cache", None)  # set_dense turns the sparse tower off until sync_sparse
         _lib.check(_lib.lib().dfwfm_model_set_dense(
             self.handle, _ptr(field_cov), _ptr(fwfm_lin), _ptr(fm_1st), _ptr(bias),
             W if H else None, B if H else None, _ptr(fc_w), _stream_handle(self.device)),
             "dfwfm_model_set_dense")
         self._dense_key = key
+
+    def sync_sparse(self, max_density: float) -> bool:
+        """(Re)build the pruned deep tower's nonzero lists after a weight update (inference only; syncs
+        the stream once per update): dfwfm_forward_ws then runs the sparse MLP when the hidden layers'
+        nonzero fraction is <= max_density.  Returns whether the sparse path is on."""
+        key = (self._dense_key, float(max_density))
+        if key == getattr(self, "_sparse_key", None):
+            return self._sparse_on
+        en = ctypes.c_int32(0)
+        _lib.check(_lib.lib().dfwfm_model_build_sparse_mlp(self.handle, float(max_density), ctypes.byref(en),
+                                                           _stream_handle(self.device)),
+                   "dfwfm_model_build_sparse_mlp")
+        self._sparse_on = bool(en.value)
+        self._sparse_key = key
+        self.__dict__.pop("_ws_cache", None)  # the workspace a batch needs changes with the path
+        return self._sparse_on
 
     # -- hot path ----------------------------------------------------------
     def forward(self, xi: torch.Tensor, xv: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
