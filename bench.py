@@ -59,10 +59,43 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU sample per thread count")
     ap.add_argument("--inputs", choices=["uniform", "zipf"], default="uniform")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--no-gate", action="store_true",
+                    help="start the timed region without holding the streams until all K steps are enqueued")
+    ap.add_argument("--sparse-mlp", type=float, default=None,
+                    help="DeepFMs.sparse_mlp_max_density for this run (pruned config: the sparse deep tower when "
+                         "the hidden layers' nonzero fraction is at most this); default: the model's")
+    ap.add_argument("--streams", type=int, default=None,
                     help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
                          "batch's workgroup shares each CU, hiding the gather / FwFM phases)")
     return ap.parse_args()
+
+
+class _HostGate:
+    """hipStreamWaitValue32 on a coherent pinned host word: the stream waits until release() writes 1."""
+
+    def __init__(self, stream):
+        import ctypes
+        self._hip = ctypes.CDLL("libamdhip64.so.7")
+        self._p = ctypes.c_void_p()
+        rc = self._hip.hipHostMalloc(ctypes.byref(self._p), ctypes.c_size_t(64), ctypes.c_uint(0x40000000))
+        if rc != 0:
+            raise RuntimeError(f"hipHostMalloc: {rc}")
+        self._word = ctypes.cast(self._p, ctypes.POINTER(ctypes.c_uint32))
+        self._word[0] = 0
+        # flags 0 = hipStreamWaitValueGte
+        rc = self._hip.hipStreamWaitValue32(ctypes.c_void_p(stream.cuda_stream), self._p, ctypes.c_uint32(1),
+                                            ctypes.c_uint(0), ctypes.c_uint32(0xFFFFFFFF))
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWaitValue32: {rc}")
+
+    def release(self):
+        self._word[0] = 1
+
+    def __del__(self):
+        try:
+            self._hip.hipHostFree(self._p)
+        except Exception:
+            pass
 
 
 def kernel_name(config="deepfwfm"):
@@ -147,11 +180,15 @@ def main():
         else:
             xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=seed)
         batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
-    S = max(1, a.streams)
+    # batches in flight: 2 fill the CUs' register files for the deep configs (two eight-wave workgroups per
+    # CU); the FwFM-only forward is latency-bound and gains from a third (5.2 vs 7.4 us per batch)
+    S = max(1, a.streams if a.streams is not None else (3 if a.config == "fwfm" else 2))
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
 
     with torch.no_grad():
         eng = model._sync_engine(dev)
+        if a.sparse_mlp is not None:
+            model.sparse_mlp_max_density = a.sparse_mlp
         sparse_on = eng.sync_sparse(model.sparse_mlp_max_density) if deep else False
         streams = [torch.cuda.Stream(dev) for _ in range(S)]
         for st in streams:
@@ -228,6 +265,10 @@ def main():
         s0 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
         s1 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
         wall0 = time.perf_counter()
+        # the K steps are enqueued behind a device-side wait on a host flag, released once everything is
+        # queued: the timed region measures the GPU running K forwards back to back, not the host
+        # submitting the graphs (at K = 20 that submission added ~3 us per step)
+        gate = _HostGate(streams[0]) if not a.no_gate else None
         t0.record(streams[0])
         for k, st in enumerate(streams):
             if k:
@@ -239,6 +280,8 @@ def main():
             if k:
                 streams[0].wait_stream(st)
         t1.record(streams[0])
+        if gate is not None:
+            gate.release()
         streams[0].synchronize()
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - wall0

@@ -101,6 +101,7 @@ def test_full_size_pruned_batch(gpu):
     shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
     m.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_state(shapes, 39, 10, 400, True, True).items()})
     m = m.to(gpu).eval()
+    m.sparse_mlp_max_density = 0.25
     prune_step(m, 0.90, 1, 1, 1, 0.444, 1.0)
     params = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
     xi, xv = synth.synth_inputs(sizes, 13, 4096, seed=11)

@@ -32,7 +32,7 @@ struct dfwfm_model {
   int sp;                          // enabled (cleared by set_dense: the ELL is then stale)
   const float* lin_w[kMaxH];       // the caller's weights from the last set_dense
   int2* d_ell;
-  int32_t* d_cnt;                  // [H][N]
+  int32_t* d_cnt;                  // [H][N] + [H][ceil(N/4)] (row, group counts)
   int32_t* d_spstat;               // [2]
   int spW[kMaxH];
   int64_t spoff[kMaxH];
@@ -259,10 +259,11 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   // fused launch (50.4 vs 43.0 us per batch alone, 43.4 vs 35.5 with two batches in flight): under a
   // co-resident MLP's weight stream the gather launch's dependent loads wait ~3x longer, and in the
   // fused kernel that wait is hidden behind the other workgroup's MLP instead of serialised
-  // no deep tower: the latency-oriented shallow kernel (dfwfm_shallow.hip); DFWFM_SHALLOW=0 keeps the
-  // fused kernel's four-wave shallow path (A/B and the bit-identity test)
+  // no deep tower: fwd_kernel's four-wave shallow path; DFWFM_SHALLOW=1 selects shallow_kernel
+  // (dfwfm_shallow.hip, bit-identical; measured slower at three batches in flight: 6.8 vs 5.2 us per
+  // batch)
   const char* sh = getenv("DFWFM_SHALLOW");
-  m->shallow = (!c.use_deep && (!sh || atoi(sh) != 0)) ? 1 : 0;
+  m->shallow = (!c.use_deep && sh && atoi(sh) != 0) ? 1 : 0;
   const char* sp = getenv("DFWFM_SPLIT");
   m->split = (c.use_deep && m->KS == 1 && sp && atoi(sp) != 0) ? 1 : 0;
   if (m->lds_bytes > 160 * 1024 || m->lds_inf > 160 * 1024) {
@@ -588,7 +589,7 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
     sa.part_stride = a.part_stride;
     sa.K0p = a.part_stride;
     sa.ell = m->d_ell;
-    sa.cnt = m->d_cnt;
+    sa.gcnt = m->d_cnt + m->H * m->N;
     for (int h = 0; h < m->H; ++h) {
       sa.W[h] = m->spW[h];
       sa.off[h] = m->spoff[h];
@@ -632,21 +633,22 @@ int dfwfm_model_build_sparse_mlp(dfwfm_model* m, double max_density, int32_t* en
     a.off[h] = total;
     m->spW[h] = a.W[h];
     m->spoff[h] = total;
-    total += (int64_t)m->N * a.W[h];
+    total += (int64_t)((m->N + 3) / 4) * 4 * a.W[h];
     dense += (int64_t)m->N * K;
   }
   if (!m->d_ell) {
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_ell), sizeof(int2) * (size_t)total));
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_cnt), sizeof(int32_t) * (size_t)m->H * m->N));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_cnt), sizeof(int32_t) * (size_t)m->H * (m->N + (m->N + 3) / 4)));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_spstat), sizeof(int32_t) * 2));
   }
   a.ell = m->d_ell;
   a.cnt = m->d_cnt;
+  a.gcnt = m->d_cnt + m->H * m->N;
   a.stat = m->d_spstat;
   a.N = m->N;
   a.H = m->H;
   HIP_TRY(hipMemsetAsync(m->d_spstat, 0, sizeof(int32_t) * 2, s));
-  hipError_t e = launch_ell_build(a, m->H * m->N, s);
+  hipError_t e = launch_ell_build(a, m->H * ((m->N + 3) / 4), s);
   if (e != hipSuccess) return hip_fail(e, "ELL build launch");
   int32_t st[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(st, m->d_spstat, sizeof st, hipMemcpyDeviceToHost, s));

@@ -236,16 +236,18 @@ hipError_t launch_sparse_grads(const SparseArgs& a, int64_t* out_dest, float* ou
 hipError_t launch_sparse_apply(float* grad, int w, const int64_t* dest, const float* rows, const int32_t* count,
                                int64_t cap, hipStream_t s);
 
-// Sparse deep tower (dfwfm_spmlp.hip): per layer, each neuron's nonzero (k, w bits) pairs in k order,
-// padded with (0, 0) to a multiple of kEllPad entries; row stride W[l] entries.
-constexpr int kEllPad = 16;
+// Sparse deep tower (dfwfm_spmlp.hip): per layer, neurons in groups of four; a group's slot holds its rows'
+// nonzero (k, w bits) pairs in k order, interleaved [entry j][neuron u], padded with (0, 0) to the
+// group's longest row rounded up to kEllPad; slot capacity W[l] entries per row.
+constexpr int kEllPad = 8;
 struct EllArgs {
   const float* w[kMaxH];   // nn.Linear weights [N][K_l], row-major (the caller's tensors)
   int32_t K[kMaxH];
   int32_t W[kMaxH];        // entries per row of layer l (>= K_l, multiple of kEllPad)
   int64_t off[kMaxH];      // first entry of layer l
   int2* ell;
-  int32_t* cnt;            // [H][N] padded pair counts
+  int32_t* cnt;            // [H][N] nonzeros per row
+  int32_t* gcnt;           // [H][ceil(N/4)] padded entries per group
   int32_t* stat;           // [2]: max row count, total nonzeros (atomics; zeroed by the caller)
   int32_t N, H;
 };
@@ -254,7 +256,7 @@ struct SpMlpArgs {
   const float* part_fs;    // [B] first + second order
   int32_t part_stride, K0p;  // K0p = columns of part_e the first layer may read (part_stride)
   const int2* ell;
-  const int32_t* cnt;
+  const int32_t* gcnt;     // [H][ceil(N/4)]
   int32_t W[kMaxH];
   int64_t off[kMaxH];
   const float* mlp_b;      // [H][NT*16] padded biases

@@ -6,12 +6,14 @@
 // matrix cores cannot skip anything.  This path instead runs the MLP on the vector ALUs over the
 // nonzeros only:
 //
-//   ell_build_kernel   per layer, each neuron's nonzero (k, w) pairs compacted in k order (one wave per
-//                      row, ballot + mbcnt), padded with (0, 0) to a multiple of kEllPad; run once per
-//                      weight update (dfwfm_model_build_sparse_mlp), not per forward;
+//   ell_build_kernel   per layer and group of four neurons, each neuron's nonzero (k, w) pairs compacted
+//                      in k order (one wave per group, ballot + mbcnt), interleaved [entry][neuron] and
+//                      padded with (0, 0) to the group's longest row; run once per weight update
+//                      (dfwfm_model_build_sparse_mlp), not per forward;
 //   sparse_mlp_kernel  64 samples per workgroup (lane = sample), the E tile of the gather launch
-//                      (fwd_kernel PART = 1) transposed into LDS as x[k][64]; eight waves own neurons
-//                      n = wave + 8i, each neuron's pairs come in as scalar loads (wave-uniform), and a
+//                      (fwd_kernel PART = 1) transposed into LDS as x[k][64]; eight waves own neuron
+//                      groups g = wave + 8i, a group's pairs come in as scalar loads (wave-uniform, 32 per
+//                      step: eight entries of four neurons, so 32 LDS reads are in flight per wait), and a
 //                      pair costs one LDS read of x[k][lane] plus one FMA -- 47.6 k FMAs per sample at
 //                      Criteo-39 / 90 % instead of the dense 476 k; a layer's outputs stay in registers
 //                      until every wave has finished reading x, then overwrite it in place; net_1_fc and
@@ -31,42 +33,70 @@ constexpr int kSpS = 64;  // samples per workgroup (lane = sample)
 constexpr int kSpW = 8;   // waves per workgroup
 }  // namespace
 
+// one wave per group of four neurons 4g..4g+3: each row's nonzeros compacted in k order (ballot + mbcnt),
+// written interleaved [entry j][neuron u] into the group's fixed slot, the shorter rows padded with
+// (0, 0) up to the group's longest row rounded to kEllPad
 __global__ void __launch_bounds__(64) ell_build_kernel(const EllArgs a) {
+  const int G = (a.N + 3) / 4;
   const int row = blockIdx.x;
-  const int l = row / a.N;
-  const int n = row - l * a.N;
+  const int l = row / G;
+  const int g = row - l * G;
   const int lane = threadIdx.x;
   const int K = a.K[l];
-  const float* w = a.w[l] + (int64_t)n * K;
-  int2* e = a.ell + a.off[l] + (int64_t)n * a.W[l];
-  int c = 0;
-  for (int k0 = 0; k0 < K; k0 += 64) {
-    const int k = k0 + lane;
-    const float v = k < K ? w[k] : 0.f;
-    const bool nz = v != 0.f;  // NaN is kept, +-0 dropped
-    const uint64_t mask = __builtin_amdgcn_ballot_w64(nz);
-    const int pos = c + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-    if (nz) e[pos] = make_int2(k, __float_as_int(v));
-    c += __builtin_popcountll(mask);
+  int2* e = a.ell + a.off[l] + (int64_t)g * a.W[l] * 4;
+  int cnt[4];  // wave-uniform (popcounts of ballots)
+  int cmax = 0, total = 0;
+  for (int u = 0; u < 4; ++u) {
+    const int n = 4 * g + u;
+    int c = 0;
+    if (n < a.N) {
+      const float* w = a.w[l] + (int64_t)n * K;
+      for (int k0 = 0; k0 < K; k0 += 64) {
+        const int k = k0 + lane;
+        const float v = k < K ? w[k] : 0.f;
+        const bool nz = v != 0.f;  // NaN is kept, +-0 dropped
+        const uint64_t mask = __builtin_amdgcn_ballot_w64(nz);
+        const int pos = c + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+        if (nz) {
+          int* slot = reinterpret_cast<int*>(e) + (pos * 2 + (u >> 1)) * 4 + (u & 1);
+          slot[0] = k;
+          slot[2] = __float_as_int(v);
+        }
+        c += __builtin_popcountll(mask);
+      }
+      if (lane == 0) a.cnt[l * a.N + n] = c;
+    }
+    cnt[u] = c;
+    cmax = c > cmax ? c : cmax;
+    total += c;
   }
-  const int cp = (c + kEllPad - 1) / kEllPad * kEllPad;
-  for (int j = c + lane; j < cp; j += 64) e[j] = make_int2(0, 0);
+  const int cp = (cmax + kEllPad - 1) / kEllPad * kEllPad;
+  // pad every row of the group from its own count up to cp
+  for (int u = 0; u < 4; ++u)
+    for (int j = cnt[u] + lane; j < cp; j += 64) {
+      int* slot = reinterpret_cast<int*>(e) + (j * 2 + (u >> 1)) * 4 + (u & 1);
+      slot[0] = 0;
+      slot[2] = 0;
+    }
   if (lane == 0) {
-    a.cnt[l * a.N + n] = cp;
-    atomicMax(&a.stat[0], c);
-    atomicAdd(&a.stat[1], c);
+    a.gcnt[l * G + g] = cp;
+    atomicMax(&a.stat[0], cmax);
+    atomicAdd(&a.stat[1], total);
   }
 }
 
-template <int NPW>
-__global__ void __launch_bounds__(64 * kSpW) sparse_mlp_kernel(const SpMlpArgs p) {
+// NGW: neuron groups (of four) per wave, >= ceil(ceil(N/4) / kSpW)
+template <int NGW>
+__global__ void __launch_bounds__(64 * kSpW) __attribute__((amdgpu_waves_per_eu(2)))
+sparse_mlp_kernel(const SpMlpArgs p) {
   extern __shared__ __attribute__((aligned(16))) float x[];  // [max(K0p, N)][64], then red [kSpW][64]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t b0 = (int64_t)blockIdx.x * kSpS;
   const int nrows = (int)((p.batch - b0) < kSpS ? (p.batch - b0) : kSpS);
   const int N = p.N;
+  const int G = (N + 3) / 4;
   const int XK = p.K0p > N ? p.K0p : N;
   float* red = x + XK * kSpS;
 
@@ -102,37 +132,82 @@ __global__ void __launch_bounds__(64 * kSpW) sparse_mlp_kernel(const SpMlpArgs p
   float dpart = 0.f;
   for (int h = 0; h < p.H; ++h) {
     const int2* ell = p.ell + p.off[h];
-    const int W = p.W[h];
-    const int* cnt = p.cnt + h * N;
+    const int W4 = p.W[h] * 4;
+    const int* gcnt = p.gcnt + h * G;
     const float* bh = p.mlp_b + h * p.NT * 16;
     const bool last = h == p.H - 1;
-    float acc[NPW];
+    float acc[NGW][4];
 #pragma unroll
-    for (int i = 0; i < NPW; ++i) {
-      const int n = wave + kSpW * i;
-      acc[i] = 0.f;
-      if (n < N) {
-        float a = bh[n];
-        const int2* e = ell + (int64_t)n * W;
-        const int c = cnt[n];
-        for (int j = 0; j < c; j += kEllPad) {
-          int2 q[kEllPad];
+    for (int i = 0; i < NGW; ++i) {
+      const int g = wave + kSpW * i;
 #pragma unroll
-          for (int u = 0; u < kEllPad; ++u) q[u] = e[j + u];
+      for (int u = 0; u < 4; ++u) acc[i][u] = 0.f;
+      if (g < G) {
+        // four neurons at once: eight entries of each per step (32 scalar pairs), 32 LDS reads in flight
+        float a[4];
 #pragma unroll
-          for (int u = 0; u < kEllPad; ++u) a = fmaf(__int_as_float(q[u].y), x[q[u].x * kSpS + lane], a);
+        for (int u = 0; u < 4; ++u) a[u] = bh[4 * g + u];  // padded biases: zero past N
+        // entries as vector loads (every lane the same 16 bytes: {k, k', w, w'} of a neuron pair), the next
+        // step's in flight while this step's LDS reads and FMAs run -- scalar loads of these lists miss the
+        // scalar cache (1.3 MB per layer) and serialised the loop on their latency
+        int vz = 0;
+        asm volatile("" : "+v"(vz));  // a VGPR offset: keeps these loads on the vector path (uniform
+                                      // addresses would otherwise become scalar loads)
+        const int4* e = reinterpret_cast<const int4*>(ell + (int64_t)g * W4) + vz;
+        const int c = gcnt[g];
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        f32x2 a01 = {a[0], a[1]}, a23 = {a[2], a[3]};
+        auto step = [&](const int4 (&q)[2 * kEllPad]) {
+          f32x2 xv[2 * kEllPad];
+#pragma unroll
+          for (int t = 0; t < 2 * kEllPad; ++t)
+            xv[t] = f32x2{x[q[t].x * kSpS + lane], x[q[t].y * kSpS + lane]};
+#pragma unroll
+          for (int t = 0; t < 2 * kEllPad; ++t) {
+            const f32x2 w = {__int_as_float(q[t].z), __int_as_float(q[t].w)};
+            if (t & 1) a23 = __builtin_elementwise_fma(w, xv[t], a23);
+            else a01 = __builtin_elementwise_fma(w, xv[t], a01);
+          }
+        };
+        int4 qa[2 * kEllPad], qb[2 * kEllPad];
+        if (c > 0) {
+#pragma unroll
+          for (int t = 0; t < 2 * kEllPad; ++t) qa[t] = e[t];
         }
-        const float r = a < 0.f ? 0.f : a;  // ReLU (NaN kept, as relu_keep_nan)
-        acc[i] = r;
-        if (last) dpart = fmaf(r, p.fc[n], dpart);
+        for (int j = 0; j < c; j += 2 * kEllPad) {
+          if (j + kEllPad < c) {
+#pragma unroll
+            for (int t = 0; t < 2 * kEllPad; ++t) qb[t] = e[2 * (j + kEllPad) + t];
+          }
+          step(qa);
+          if (j + kEllPad >= c) break;
+          if (j + 2 * kEllPad < c) {
+#pragma unroll
+            for (int t = 0; t < 2 * kEllPad; ++t) qa[t] = e[2 * (j + 2 * kEllPad) + t];
+          }
+          step(qb);
+        }
+        a[0] = a01.x;
+        a[1] = a01.y;
+        a[2] = a23.x;
+        a[3] = a23.y;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int n = 4 * g + u;
+          const float r = a[u] < 0.f ? 0.f : a[u];  // ReLU (NaN kept, as relu_keep_nan)
+          acc[i][u] = n < N ? r : 0.f;
+          if (last && n < N) dpart = fmaf(r, p.fc[n], dpart);
+        }
       }
     }
     if (!last) {
       __syncthreads();  // every wave has finished reading this layer's input
 #pragma unroll
-      for (int i = 0; i < NPW; ++i) {
-        const int n = wave + kSpW * i;
-        if (n < N) x[n * kSpS + lane] = acc[i];
+      for (int i = 0; i < NGW; ++i) {
+        const int g = wave + kSpW * i;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (g < G && 4 * g + u < N) x[(4 * g + u) * kSpS + lane] = acc[i][u];
       }
       __syncthreads();
     }
@@ -147,7 +222,7 @@ __global__ void __launch_bounds__(64 * kSpW) sparse_mlp_kernel(const SpMlpArgs p
   }
 }
 
-hipError_t launch_ell_build(const EllArgs& a, int rows, hipStream_t s) {
+hipError_t launch_ell_build(const EllArgs& a, int rows, hipStream_t s) {  // rows = H * ceil(N/4) groups
   if (rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(ell_build_kernel, dim3(rows), dim3(64), 0, s, a);
   return hipGetLastError();
@@ -158,10 +233,10 @@ size_t sparse_mlp_lds_bytes(int K0p, int N) {
   return sizeof(float) * ((size_t)XK * kSpS + kSpW * kSpS);
 }
 
-template <int NPW>
+template <int NGW>
 static hipError_t launch_sp_t(const SpMlpArgs& a, hipStream_t s) {
   const size_t lds = sparse_mlp_lds_bytes(a.K0p, a.N);
-  auto k = sparse_mlp_kernel<NPW>;
+  auto k = sparse_mlp_kernel<NGW>;
   hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
   if (e != hipSuccess) return e;
   const unsigned grid = (unsigned)((a.batch + kSpS - 1) / kSpS);
@@ -170,11 +245,11 @@ static hipError_t launch_sp_t(const SpMlpArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_sparse_mlp(const SpMlpArgs& a, hipStream_t s) {
-  const int npw = (a.N + kSpW - 1) / kSpW;
-  if (npw <= 16) return launch_sp_t<16>(a, s);
-  if (npw <= 32) return launch_sp_t<32>(a, s);
-  if (npw <= 48) return launch_sp_t<48>(a, s);
-  if (npw <= 64) return launch_sp_t<64>(a, s);
+  const int ngw = ((a.N + 3) / 4 + kSpW - 1) / kSpW;
+  if (ngw <= 4) return launch_sp_t<4>(a, s);
+  if (ngw <= 8) return launch_sp_t<8>(a, s);
+  if (ngw <= 12) return launch_sp_t<12>(a, s);
+  if (ngw <= 16) return launch_sp_t<16>(a, s);
   return hipErrorInvalidValue;
 }
 
