@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_train.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tt.log 2>&1; rc=$?; tail -4 gpurun_out/tt.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python tools/bench_train.py > gpurun_out/bt.log 2>&1 || exit 1; echo "fused: $(tail -1 gpurun_out/bt.log | cut -c1-260)"
+DFWFM_NO_FUSED_RED=1 timeout -k 10 200 python tools/bench_train.py > gpurun_out/bt0.log 2>&1 || exit 1; echo "unfused: $(tail -1 gpurun_out/bt0.log | cut -c1-260)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/proftrain -o run --output-format csv -- python3 tools/bench_train.py > gpurun_out/pt.log 2>&1 || exit 1
+cut -c1-150 gpurun_out/proftrain/run_kernel_stats.csv | head -14

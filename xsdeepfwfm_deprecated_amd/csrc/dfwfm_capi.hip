@@ -716,6 +716,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   const int F = m->F, D = m->D, num = m->num, H = m->H;
   const bool drop = H > 0 && m->t_drop > 0.f;
   hipError_t e;
+  bool fused_red = false;
 
   // 1. per-tile backward: dE and the G chain (no atomics)
   if ((phases & DFWFM_BWD_TABLES) && (m->flags & kNeedE)) {
@@ -753,6 +754,19 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     a.drop_scale = 1.f / (1.f - m->t_drop);
     a.seed = m->t_seed;
     a.seed_src = m->step_src;
+    // the dense shallow reductions ride along (reduce_kernel's re-read of E / fo / X_H / dE is skipped;
+    // DFWFM_NO_FUSED_RED=1 keeps the separate kernel, for A/B)
+    if (!getenv("DFWFM_NO_FUSED_RED")) {
+      a.part = m->red_part;
+      a.sv_fo = m->sv_fo;
+      a.xv = m->t_xv;
+      a.xv_stride = m->t_vs;
+      a.num = num;
+      a.red = kRedOn | ((m->flags & kFoLw) && g->fm_1st ? kRedLw : 0) |
+              ((m->flags & kFoFwlw) && g->fwfm_lin ? kRedFwlw : 0) | (m->cfg.use_fwfm && g->field_cov ? kRedR : 0) |
+              (H > 0 && g->fc_w ? kRedFc : 0) | kRedNum2 | kRedNum1;
+      fused_red = true;
+    }
     // diagnostics only: DFWFM_DIAG_STAMPS=2 records the backward's phase clocks instead of the forward's
     int src = diag_stamps_buffer(m, batch, 2, &a.stamps);
     if (src != DFWFM_OK) return src;
@@ -796,7 +810,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     r.N = m->N;
     r.MT = m->MT;
     r.flags = m->flags;
-    e = launch_reduce(r, s);
+    e = fused_red ? launch_reduce_final(r, s) : launch_reduce(r, s);
     if (e != hipSuccess) return hip_fail(e, "reduce launch");
   }
 

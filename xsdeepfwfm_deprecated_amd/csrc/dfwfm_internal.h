@@ -144,7 +144,17 @@ struct BwdArgs {
   uint32_t seed;
   const int64_t* seed_src;       // as FwdArgs::seed_src
   uint64_t* stamps;              // diagnostics only (DFWFM_DIAG_STAMPS=2): phase clocks per workgroup
+  // the dense shallow reductions fused in (red != 0): the tile's partial sums to part[blockIdx.x] in
+  // reduce_kernel's layout (red_outputs), from the E / X_H / dE tiles already in LDS; reduce_final_kernel
+  // adds them.  red: kRed* bits of the gradients wanted
+  float* part;
+  const float* sv_fo;            // [B][F]
+  const float* xv;               // numerical values
+  int64_t xv_stride;
+  int32_t num;
+  int32_t red;
 };
+constexpr int kRedOn = 1, kRedLw = 2, kRedFwlw = 4, kRedR = 8, kRedFc = 16, kRedNum2 = 32, kRedNum1 = 64;
 
 // Batch reductions of the dense shallow parameters, per 16-row tile then summed over tiles:
 // bias, fm_1st (lw), fwfm_linear, field_cov (Gram on MFMA), net_1_fc, numerical-field tables.
@@ -379,6 +389,7 @@ hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds,
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
 hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages
+hipError_t launch_reduce_final(const RedArgs& a, hipStream_t s);  // the second stage only (bwd_kernel red)
 hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,

@@ -23,7 +23,7 @@
 namespace dfwfm {
 
 struct BwdLds {
-  int lw, fwlw, rsk, bufE, bufD, bufA, dl, fc, tailr, total;
+  int lw, fwlw, rsk, bufE, bufD, bufA, dl, fc, tailr, fo, xv, total;
 };
 
 __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX, int SY) {
@@ -38,6 +38,8 @@ __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX
   L.dl = o;    o += kBM;
   L.fc = o;    o += SY;                       // net_1_fc (G_H = dlogit * fc * mask)
   L.tailr = o; o += 8 * 64 * 4;               // split-tail partial products (eight waves)
+  L.fo = o;    o += kBM * r4(F);              // fused reductions: first order per field
+  L.xv = o;    o += kBM * r4(F);              //                   numerical values (num <= F)
   L.total = r4(o);
   return L;
 }
@@ -93,6 +95,21 @@ bwd_kernel(BwdArgs p) {
     for (int i = tid; i < p.MT * p.S * 16; i += NTH)
       reinterpret_cast<float4*>(rsk)[i] = reinterpret_cast<const float4*>(p.rsk)[i];
   if (tid < kBM) dl[tid] = (b0 + tid < p.batch) ? p.dlogit[b0 + tid] : 0.f;
+  const int red = p.red;
+  float* fo_s = smem + L.fo;
+  float* xv_s = smem + L.xv;
+  const int num = p.num, Fp = r4(F);
+  if (red & kRedLw)
+    for (int i = tid; i < kBM * F; i += NTH) {
+      const int b = i / F;
+      fo_s[b * Fp + (i - b * F)] = b < nrows ? p.sv_fo[(b0 + b) * F + (i - b * F)] : 0.f;
+    }
+  if (red)
+    for (int i = tid; i < kBM * num; i += NTH) {
+      const int b = i / num;
+      xv_s[b * Fp + (i - b * num)] = b < nrows ? p.xv[(b0 + b) * p.xv_stride + (i - b * num)] : 0.f;
+    }
+  float* rout = p.part + (size_t)blockIdx.x * red_outputs(F, D, p.N, num);  // fused reductions' partials
   if (deep)
     for (int i = tid; i < p.NT * 16; i += NTH) fc_s[i] = p.fc[i];
   // the E tile: rows of r4(F*D) floats (zero past F*D), zero-padded to W0 columns
@@ -136,6 +153,81 @@ bwd_kernel(BwdArgs p) {
       }
     }
   }
+  // ---- R: the dense shallow reductions over this tile (reduce_kernel's arithmetic, same order), from the
+  // E tile still in LDS: bias, fm_1st, fwfm_linear, the numerical fields' first order, field_cov's Gram
+  if (red) {
+    float* o_lw = rout + 1;
+    float* o_fw = o_lw + F;
+    float* o_R = o_fw + FD;
+    if (tid < kBM) {
+      const float v = sum16(dl[tid]);
+      if (tid == 0) rout[0] = v;
+    }
+    if (tid < F) {
+      float sl = 0.f;
+      if (red & kRedLw)
+#pragma unroll
+        for (int b = 0; b < kBM; ++b) sl = fmaf(dl[b], fo_s[b * Fp + tid], sl);
+      o_lw[tid] = sl;
+    }
+    for (int i = tid; i < FD; i += NTH) {
+      float sf = 0.f;
+      if (red & kRedFwlw)
+#pragma unroll
+        for (int b = 0; b < kBM; ++b) sf = fmaf(dl[b], bufE[b * SX + i], sf);
+      o_fw[i] = sf;
+    }
+    if (tid < num) {
+      float sn = 0.f;
+#pragma unroll
+      for (int b = 0; b < kBM; ++b) sn = fmaf(dl[b], xv_s[b * Fp + tid], sn);
+      float* o_n1 = o_fw + FD + F * F + p.N + num * D;
+      o_n1[tid] = sn;
+    }
+    if (red & kRedR) {
+      // d W[k,l] = 0.5 * sum_b dlogit_b <E_bk, E_bl>, k != l (:363-367): Gram on MFMA over (b, d)
+      const int MT = p.MT, ntile = MT * MT;
+      constexpr int steps = (kBM * D) / 4;
+      for (int t = wave; t < ntile; t += NW) {
+        const int mk = t / MT, ml = t - mk * MT;
+        const int kA = 16 * mk + (lane & 15);
+        const int lB = 16 * ml + (lane & 15);
+        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+        int st = 0;
+        for (; st + 4 <= steps; st += 4) {
+          float av[4], bv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int n = 4 * (st + u) + (lane >> 4);
+            const int b = n / D;
+            const int d = n - b * D;
+            av[u] = kA < F ? dl[b] * bufE[b * SX + kA * D + d] : 0.f;
+            bv[u] = lB < F ? bufE[b * SX + lB * D + d] : 0.f;
+          }
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc1, 0, 0, 0);
+        }
+        for (; st < steps; ++st) {
+          const int n = 4 * st + (lane >> 4);
+          const int b = n / D;
+          const int d = n - b * D;
+          const float av = kA < F ? dl[b] * bufE[b * SX + kA * D + d] : 0.f;
+          const float bv = lB < F ? bufE[b * SX + lB * D + d] : 0.f;
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
+        }
+        const f32x4 acc = acc0 + acc1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * mk + (lane >> 4) * 4 + r;
+          if (k < F && lB < F) o_R[k * F + lB] = k != lB ? 0.5f * acc[r] : 0.f;
+        }
+      }
+    } else {
+      for (int i = tid; i < F * F; i += NTH) o_R[i] = 0.f;
+    }
+  }
   __syncthreads();
   stamp(p.stamps, 2, tid);
 
@@ -148,11 +240,18 @@ bwd_kernel(BwdArgs p) {
     // at the top of layer H, behind its weight preload)
     load_tile<7>(bufA, SY, p.sv_x[H] + b0 * N, N, nrows, N / 4, NP / 4, tid, NTH);
     __syncthreads();
-    for (int i = tid; i < kBM * NP; i += NTH) {
-      const int b = i / NP;
-      const int n = i - b * NP;
-      const float x = bufA[b * SY + n];
-      bufA[b * SY + n] = (n < N && x > 0.f) ? dl[b] * fc_s[n] * scale : 0.f;
+    // column n per thread: the fused net_1_fc reduction (sum_b dlogit_b X_H[b, n], reduce_kernel's order)
+    // reads the column before it is overwritten with G_H
+    float* o_fc = rout + 1 + F + FD + F * F;
+    for (int n = tid; n < NP; n += NTH) {
+      float sc = 0.f;
+#pragma unroll
+      for (int b = 0; b < kBM; ++b) {
+        const float x = bufA[b * SY + n];
+        sc = fmaf(dl[b], x, sc);
+        bufA[b * SY + n] = (n < N && x > 0.f) ? dl[b] * fc_s[n] * scale : 0.f;
+      }
+      if (red && n < N) o_fc[n] = (red & kRedFc) ? sc : 0.f;
     }
     __syncthreads();
     stamp(p.stamps, 3, tid);
@@ -257,6 +356,18 @@ bwd_kernel(BwdArgs p) {
     const int b = i / FD;
     const int c = i - b * FD;
     if (b0 + b < p.batch) p.sv_de[(b0 + b) * FD + c] = bufD[b * SX + c];
+  }
+  if (red) {
+    // numerical fields' second-order tables: E_f = v_f * Xv_f (:297-299) -> sum_b dE[b, f, :] * Xv[b, f]
+    float* o_n2 = rout + 1 + F + FD + F * F + p.N;
+    for (int i = tid; i < num * D; i += NTH) {
+      const int f = i / D;
+      float s2 = 0.f;
+      if (red & kRedNum2)
+#pragma unroll
+        for (int b = 0; b < kBM; ++b) s2 = fmaf(bufD[b * SX + i], xv_s[b * Fp + f], s2);
+      o_n2[i] = s2;
+    }
   }
   stamp(p.stamps, 9, tid);
   stamp_rt(p.stamps, 11, tid);
@@ -963,6 +1074,13 @@ hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds,
     case 32: return launch_backward_d32(a, tpw, ng, lds, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_reduce_final(const RedArgs& a, hipStream_t s) {
+  const int nblk = (int)((a.batch + kBM - 1) / kBM);
+  const int P = red_outputs(a.F, a.D, a.N, a.num);
+  hipLaunchKernelGGL(reduce_final_kernel, dim3((P + 63) / 64), dim3(256), 0, s, a, nblk);
+  return hipGetLastError();
 }
 
 hipError_t launch_reduce(const RedArgs& a, hipStream_t s) {
