@@ -102,12 +102,13 @@ def kernel_name(config="deepfwfm"):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT select the A/B variants."""
     if config == "fwfm":
-        return "dfwfm::fwd_kernel<10,1,1,false,0,4>"
+        return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
     ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
     tpw = 6 if ng == 4 else 3
     if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):
         return f"dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::fwd_kernel<10,{tpw},1,false,2,{ng}>"
-    return f"dfwfm::fwd_kernel<10,{tpw},1,false,0,{ng}>"
+    ns = 25 if ng == 8 and tpw == 3 and not os.environ.get("DFWFM_NO_STATIC_K") else 0  # static 25-chunk K loop
+    return f"dfwfm::fwd_kernel<10,{tpw},1,false,0,{ng},{ns}>"
 
 
 def algorithmic_counts(cfg, sizes=None):

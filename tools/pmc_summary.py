@@ -24,6 +24,8 @@ for path in glob.glob(os.path.join(root, f"pmc_{tag}_*", "run_counter_collection
         k = r["Kernel_Name"]
         if "fwd_kernel" not in k:
             continue
+        # bench.py's kernel_name form: "dfwfm::fwd_kernel<10,3,1,false,0,8,25>"
+        k = k.replace("void ", "").replace(" ", "").split("(")[0]
         vals.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
         durs.setdefault(k, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 out = {}
@@ -36,7 +38,8 @@ for k, v in vals.items():
     if "SQ_VALU_MFMA_BUSY_CYCLES" in med and "GRBM_GUI_ACTIVE" in med:
         e["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (med["GRBM_GUI_ACTIVE"] / 8 * 1024)
     out[k] = e
-s = json.dumps(out, indent=1)
+s = json.dumps({"source": f"tools/pmc.sh (tag {tag}): eager, one stream, rocprofv3 --pmc, one counter group per pass",
+                "kernels": out}, indent=1)
 print(s)
 if dst:
     open(dst, "w").write(s + "\n")
