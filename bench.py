@@ -102,7 +102,8 @@ def kernel_name(config="deepfwfm"):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT select the A/B variants."""
     if config == "fwfm":
-        return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
+        return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>" if os.environ.get("DFWFM_NO_PART3") else \
+            "dfwfm::fwd_kernel<10,1,1,false,3,8,0>"
     ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
     tpw = 6 if ng == 4 else 3
     if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):

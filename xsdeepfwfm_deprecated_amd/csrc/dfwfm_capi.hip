@@ -244,6 +244,8 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   m->TPWI = m->TPWF;
   m->tailI = m->tail;
   m->lds_inf = m->lds_bytes;
+  if (!c.use_deep)  // the MLP-free forward runs on eight waves (fwd_kernel PART 3): its layout's per-wave slots
+    m->lds_inf = sizeof(float) * (size_t)lds_layout(F, D, m->MT, m->S, m->SX, m->SY, 1, 1, false, false, 8).total;
   if (c.use_deep && m->KS == 1 && NT <= 32 && m->NC0 <= 32) {
     const char* ng = getenv("DFWFM_NG");
     if (!ng || atoi(ng) == 8) {

@@ -27,6 +27,7 @@
 //   combine  total = ((first + second) + deep) + bias   (:458 order).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -46,7 +47,8 @@ namespace dfwfm {
 #endif
 // PART: 0 = the whole forward in one launch; 1 = stage, gather and shallow part only, E tile and
 // first + second to p.part_e / p.part_fs; 2 = MLP and combine from p.part_e / p.part_fs (the split
-// forward: two launches per batch, see launch_forward_split)
+// forward: two launches per batch, see launch_forward_split); 3 = a model without deep tower (no MLP
+// code: 105 registers on eight waves instead of the generic kernel's 165 on four)
 // NG: MLP output-tile groups = waves (4: one wave per SIMD, <= 256 registers; 8: two per SIMD, <= 128
 // registers, so one workgroup issues MFMAs from two waves per SIMD while a second batch's workgroup
 // on the same CU runs its gather; the training variant, one batch in flight, keeps 256 registers)
@@ -54,7 +56,7 @@ namespace dfwfm {
 // split tail tile rides on its register sets (mlp_k_loop_s)
 template <int D, int TPW, int KS, bool TRAIN, int PART, int NG, int NS>
 __global__ void __launch_bounds__(64 * NG * KS)
-__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE))))
+__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (PART == 3 ? 4 : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE)))))
 fwd_kernel(FwdArgs p) {
   static_assert(NG == 4 || (NG == 8 && KS == 1), "8 tile groups: no K split");
   constexpr int NTH = 64 * NG * KS;
@@ -69,7 +71,7 @@ fwd_kernel(FwdArgs p) {
   const int SX = p.SX;
   const int SY = p.SY;
   const int flags = p.flags;
-  const bool deep = PART != 1 && (flags & kHasDeep) != 0;  // the MLP runs in this launch
+  const bool deep = PART != 1 && PART != 3 && (flags & kHasDeep) != 0;  // the MLP runs in this launch
   const int Fp = r4(F);
   const bool tail = KS == 1 && p.tail != 0;
   const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep, tail, NG);  // PART 1: no MLP buffers
@@ -767,6 +769,10 @@ static hipError_t launch_fwd_8(const FwdArgs& a, int tpw, size_t lds, hipStream_
 
 template <int D>
 static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
+  // no deep tower: the MLP-free instantiation on eight waves (105 registers, no scratch): 4.92 us per batch
+  // at three batches in flight against 5.19 for the generic four-wave one (DFWFM_NO_PART3=1) and 6.0 for a
+  // four-wave MLP-free one (128 registers + spills)
+  if (!(a.flags & (kHasDeep | kTrain)) && !getenv("DFWFM_NO_PART3")) return launch_fwd_t<D, 1, 1, false, 3, 8>(a, lds, s);
   if (a.flags & kTrain) return ng == 8 ? launch_fwd_8<D, 0, true>(a, tpw, lds, s) : launch_fwd_k<D, 1, true>(a, tpw, lds, s);
   if (ng == 8) return launch_fwd_8<D, 0>(a, tpw, lds, s);
   return ks == 2 ? launch_fwd_k<D, 2, false>(a, tpw, lds, s) : launch_fwd_k<D, 1, false>(a, tpw, lds, s);
