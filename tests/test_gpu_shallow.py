@@ -1,6 +1,7 @@
-"""GPU: the forward without a deep tower (shallow_kernel, csrc/dfwfm_shallow.hip) -- the FwFM-only config
-of BASELINE configs[0] -- against the oracle, and bit-identical to the fused kernel's shallow path
-(DFWFM_SHALLOW=0, read at model creation)."""
+"""GPU: the forward without a deep tower -- the FwFM-only config of BASELINE configs[0]: the default
+MLP-free fwd_kernel (PART 3, per-sample Gram FwFM) and the opt-in shallow_kernel (csrc/dfwfm_shallow.hip,
+DFWFM_SHALLOW=1 at model creation) against the oracle; shallow_kernel bit-identical to the generic fused
+kernel (DFWFM_NO_PART3=1)."""
 import numpy as np
 import pytest
 import torch
@@ -71,8 +72,14 @@ def test_shallow_kernel_matches_oracle_and_fused(gpu, monkeypatch, case):
     got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
     assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    # bit-identical to the generic fused kernel (DFWFM_NO_PART3: the piece-wise FwFM, same arithmetic) ...
+    monkeypatch.setenv("DFWFM_NO_PART3", "1")
     fused = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
+    monkeypatch.delenv("DFWFM_NO_PART3")
     assert np.array_equal(got, fused)
+    # ... and the default MLP-free kernel (per-sample Gram FwFM, another summation order) within the bar
+    part3 = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
+    assert logit_close_scaled(part3, ref, cfg, params, xi, xv) < 1e-5
 
 
 @pytest.mark.parametrize("B", [1, 15, 16, 17, 255, 4096 + 3])
@@ -102,3 +109,16 @@ def test_shallow_kernel_index_out_of_range_raises(gpu, monkeypatch, bad):
     m = _model(cfg, params, gpu, monkeypatch, True)
     with pytest.raises(IndexError):
         _run(m, xi, xv, gpu)
+
+
+@pytest.mark.parametrize("B", [1, 17, 4096 + 3])
+def test_default_mlp_free_kernel_ragged_and_full_size(gpu, monkeypatch, B):
+    """The default FwFM-only forward (fwd_kernel PART 3) at ragged batches and the Criteo-39 tables;
+    a row's logit does not depend on its tile or slot."""
+    cfg, params, xi, xv = _case(39, 13, 10, B=B, big=B > 4096, seed=B + 1)
+    m = _model(cfg, params, gpu, monkeypatch, False)
+    got = _run(m, xi, xv, gpu)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    one = _run(m, xi[B - 1:], xv[B - 1:], gpu)
+    assert one[0] == got[B - 1]

@@ -342,7 +342,51 @@ fwd_kernel(FwdArgs p) {
     }
   }
   stamp(p.stamps, 9, tid);
-  if (flags & kHasSecond) {
+  if constexpr (PART == 3) {
+    if (flags & kHasSecond) {
+      // MLP-free forward: second[b] = sum_{k<l} U'[k,l] <E_bk, E_bl> from the per-sample Gram G_b = E_b E_b^T
+      // on MFMA (rows k, columns l, contraction over d: ceil(D/4) steps).  A sample's MT*ceil(D/4) operand
+      // fragments serve as both A and B of its upper tiles (m <= n), so every chain is ceil(D/4) MFMAs deep
+      // and a wave has 6 x 3 independent ones per sample at Criteo-39 -- the (row tile, column tile)
+      // pieces' 10-deep chains of fwd_kernel's other forms left this phase latency-bound.  U' is the
+      // strictly upper (R + R^T)/2 (FM: ones) read from the A-fragment pack in LDS.
+      constexpr int SD = (D + 3) / 4;
+      const int MT = p.MT, S = p.S;
+      for (int b = wave; b < kBM; b += NW) {
+        float ev[kMaxMT][SD];
+#pragma unroll
+        for (int m = 0; m < kMaxMT; ++m)
+#pragma unroll
+          for (int s = 0; s < SD; ++s) {
+            const int k = 16 * m + (lane & 15);
+            const int d = 4 * s + (lane >> 4);
+            ev[m][s] = (m < MT && k < F && d < D) ? bufX[b * SX + k * D + d] : 0.f;
+          }
+        float part = 0.f;
+#pragma unroll
+        for (int m = 0; m < kMaxMT; ++m)
+#pragma unroll
+          for (int n = m; n < kMaxMT; ++n) {
+            if (n >= MT) continue;  // wave-uniform
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < SD; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ev[m][s], ev[n][s], acc, 0, 0, 0);
+            // lane holds G[16m + 4(lane>>4) + r][16n + (lane&15)]; U'[k][l] sits in the pack at
+            // [(k/16) * S + l/4][(k%16) + 16 (l%4)]
+            const int l = 16 * n + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 16 * m + 4 * (lane >> 4) + r;
+              const float u = (l < 4 * S) ? upk[((k >> 4) * S + (l >> 2)) * 64 + (k & 15) + 16 * (l & 3)] : 0.f;
+              part = fmaf(u, acc[r], part);
+            }
+          }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+        if (lane == 0) part2[b] = part;
+      }
+    }
+  } else if (flags & kHasSecond) {
     // Y = U * E_b on MFMA: rows k (fields, MT tiles of 16), columns n = b*D + d (D tiles of 16), contraction
     // over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].  The work is cut into
     // pieces pc = (row tile m, column tile nt) of S - 4m steps each (U's rows 16m.. vanish for l <= 16m); the
@@ -429,9 +473,13 @@ fwd_kernel(FwdArgs p) {
       first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
     }
     if (flags & kHasSecond) {
-      for (int d = q; d < D; d += 16) {  // D = 32: two terms per lane
-        const int n = b * D + d;
-        for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
+      if constexpr (PART == 3) {
+        second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
+      } else {
+        for (int d = q; d < D; d += 16) {  // D = 32: two terms per lane
+          const int n = b * D + d;
+          for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
+        }
       }
     }
 #pragma unroll
