@@ -71,9 +71,9 @@ def parse():
 
 
 class _HostGate:
-    """hipStreamWaitValue32 on a coherent pinned host word: the stream waits until release() writes 1."""
+    """hipStreamWaitValue32 on a coherent pinned host word: the streams wait until release() writes 1."""
 
-    def __init__(self, stream):
+    def __init__(self, streams):
         import ctypes
         self._hip = ctypes.CDLL("libamdhip64.so.7")
         self._p = ctypes.c_void_p()
@@ -82,11 +82,11 @@ class _HostGate:
             raise RuntimeError(f"hipHostMalloc: {rc}")
         self._word = ctypes.cast(self._p, ctypes.POINTER(ctypes.c_uint32))
         self._word[0] = 0
-        # flags 0 = hipStreamWaitValueGte
-        rc = self._hip.hipStreamWaitValue32(ctypes.c_void_p(stream.cuda_stream), self._p, ctypes.c_uint32(1),
-                                            ctypes.c_uint(0), ctypes.c_uint32(0xFFFFFFFF))
-        if rc != 0:
-            raise RuntimeError(f"hipStreamWaitValue32: {rc}")
+        for stream in streams:  # flags 0 = hipStreamWaitValueGte
+            rc = self._hip.hipStreamWaitValue32(ctypes.c_void_p(stream.cuda_stream), self._p, ctypes.c_uint32(1),
+                                                ctypes.c_uint(0), ctypes.c_uint32(0xFFFFFFFF))
+            if rc != 0:
+                raise RuntimeError(f"hipStreamWaitValue32: {rc}")
 
     def release(self):
         self._word[0] = 1
@@ -261,36 +261,39 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
-        t0 = torch.cuda.Event(enable_timing=True)
-        t1 = torch.cuda.Event(enable_timing=True)
         # per-stream events: a launch's duration while S run side by side (what rocprofv3 reports)
         s0 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
         s1 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
         wall0 = time.perf_counter()
-        # the K steps are enqueued behind a device-side wait on a host flag, released once everything is
-        # queued: the timed region measures the GPU running K forwards back to back, not the host
-        # submitting the graphs (at K = 20 that submission added ~3 us per step)
-        gate = _HostGate(streams[0]) if not a.no_gate else None
-        t0.record(streams[0])
+        # the K steps are enqueued behind a device-side wait on a host flag (one wait per stream, one
+        # flag), released once everything is queued: the timed region measures the GPU running K forwards,
+        # not the host submitting graphs.  The region runs from the earliest stream's start event to the
+        # latest stream's end event (each recorded on its own stream): cross-stream event waits inside the
+        # region cost ~20 us each on this stack (a late second stream, a late final event)
+        gate = _HostGate(streams) if not a.no_gate else None
         for k, st in enumerate(streams):
-            if k:
+            if k and gate is None:
                 st.wait_stream(streams[0])
             s0[k].record(st)
         run_n(a.steps)
         for k, st in enumerate(streams):
             s1[k].record(st)
-            if k:
-                streams[0].wait_stream(st)
-        t1.record(streams[0])
         if gate is not None:
             gate.release()
-        streams[0].synchronize()
+        for st in streams:
+            st.synchronize()
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - wall0
         if world > 1:
             torch.distributed.barrier()
-    ms = t0.elapsed_time(t1)
+    # the timed region: the earliest stream start to the latest stream end
+    first = min(range(S), key=lambda k: s0[0].elapsed_time(s0[k]))
+    last = max(range(S), key=lambda k: s0[0].elapsed_time(s1[k]))
+    ms = s0[first].elapsed_time(s1[last])
     launch_ms = sum(s0[k].elapsed_time(s1[k]) for k in range(S)) / a.steps  # per launch, S side by side
+    # where the streams start and end inside the timed region (fill / drain of a short run)
+    skew = {"start_us": [round(s0[first].elapsed_time(s0[k]) * 1e3, 2) for k in range(S)],
+            "end_us": [round(s1[k].elapsed_time(s1[last]) * 1e3, 2) for k in range(S)]}
     if world > 1:
         t = torch.tensor([ms], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -335,6 +338,7 @@ def main():
         "settle": {"forwards": settle_n, "ms": round(settle_ms, 1),
                    "what": "untimed back-to-back forwards before the warmup steps (clock ramp)"},
         "wall_s": round(wall, 4),
+        "streams_in_region": skew,
     }
     mfma = {"bound": mfma_bound, "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "flops_per_sample": flops}
