@@ -53,6 +53,9 @@ def main(argv=None):
                       logger=logger)
     model = load_model_dic(model, save_model_name, sparse=pars.prune).cuda()
     model.print_size_of_model()
+    if not pars.time_on_cuda:
+        logger.info("-time_on_cuda 0: this engine has no CPU forward (no fallback by design); the benchmark "
+                    "times the HIP forward, and bench.py's cpu_baseline times the reference op sequence on the host")
     logger.info("TEST DATASET")
     return model.run_benchmark(test_dict["index"], test_dict["value"], test_dict["label"], batch_size=8192,
                                cuda=True)

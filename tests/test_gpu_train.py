@@ -282,9 +282,11 @@ def test_device_threshold_equals_reference_value(gpu):
     assert pr.threshold([(W.to(gpu), 39)], 0.7).item() == ref
 
 
-def test_main_all_tiny_criteo_end_to_end(gpu, tmp_path):
+@pytest.mark.parametrize("extra,name", [([], "DeepFwFM"), (["-use_deep", "0", "-c", "FwFM"], "FwFM")])
+def test_main_all_tiny_criteo_end_to_end(gpu, tmp_path, extra, name):
     """main_all.py (the reference entry point) on the tiny-criteo fixture rows: native ingest, fit with the
-    fused HIP step (one epoch), save, reload, print_size_of_model, run_benchmark (device metrics)."""
+    fused HIP step (one epoch), save, reload, print_size_of_model, run_benchmark (device metrics) -- for
+    DeepFwFM and for BASELINE configs[0] (FwFM only, use_deep 0)."""
     import shutil
     import subprocess
     import sys
@@ -295,11 +297,11 @@ def test_main_all_tiny_criteo_end_to_end(gpu, tmp_path):
     shutil.copy(src, data / "tiny_train_input.csv")
     shutil.copy(src, data / "tiny_test_input.csv")
     r = subprocess.run([sys.executable, os.path.join(REPO, "main_all.py"), "-dataset", "tiny-criteo", "-n_epochs",
-                        "1", "-batch_size", "256", "-data_root", str(tmp_path)], cwd=str(tmp_path),
+                        "1", "-batch_size", "256", "-data_root", str(tmp_path)] + extra, cwd=str(tmp_path),
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "Training [1] loss" in r.stdout and "Acc:" in r.stdout and "Avg forward pass time" in r.stdout
-    assert any(f.startswith("DeepFwFM_l2_") for f in os.listdir(tmp_path / "saved_models"))
+    assert any(f.startswith(name + "_l2_") for f in os.listdir(tmp_path / "saved_models"))
 
 
 def _dp_fit_worker(rank, world, port, q):
