@@ -925,8 +925,24 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
 // g += wd * p; m = lerp(m, g, 1 - b1);
 // v = v * b2 + (1 - b2) * g * g; p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) adam_kernel(const AdamList list, float step_size, float omb1, float b2,
-                                                   float omb2, float eps, float wd, float bc2_sqrt) {
+// one element of torch.optim.Adam: torch's CPU kernels' evaluation order -- fmadd where ATen's vector path
+// uses one, every other product / sum rounded on its own
+struct AdamCoef {
+  float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt;
+};
+__device__ __forceinline__ void adam_elem(const AdamCoef& c, float& p, float g, float& m, float& v) {
+  if (c.wd != 0.f) g = fmaf(c.wd, p, g);                          // grad.add(param, alpha=wd): ATen's fmadd
+  m = fmaf(c.omb1, __fsub_rn(g, m), m);                            // exp_avg.lerp_(grad, 1-b1): fmadd, w < 0.5
+  v = __fmul_rn(v, c.b2);                                          // exp_avg_sq.mul_(b2)
+  v = __fadd_rn(v, __fmul_rn(__fmul_rn(c.omb2, g), g));           //   .addcmul_(g, g, 1-b2)
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), c.bc2_sqrt), c.eps);  // sqrt(v)/sqrt(bc2) + eps
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(-c.step_size, m), denom));  // addcdiv_(m, denom, -lr/bc1)
+}
+
+// a block's 1024 elements: when the tensor's four arrays are 16-byte aligned thread t owns [4t, 4t+4) -- one
+// 16-byte load of each of p, g, m, v and three 16-byte stores, every load in flight at once -- else the
+// lanes take consecutive elements
+__device__ __forceinline__ void adam_block(const AdamList& list, const AdamCoef& c) {
   int lo = 0, hi = list.n - 1;
   const int bid = blockIdx.x;
   while (lo < hi) {  // last tensor whose block0 <= bid
@@ -936,21 +952,44 @@ __global__ void __launch_bounds__(256) adam_kernel(const AdamList list, float st
   }
   const AdamTensor T = list.t[lo];
   const int64_t i0 = (int64_t)(bid - T.block0) * 1024;
-  // torch's CPU kernels' evaluation order: fmadd where ATen's vector path uses one, every other
-  // product / sum rounded on its own
-  for (int64_t i = i0 + threadIdx.x; i < i0 + 1024 && i < T.n; i += 256) {
-    const float pv = T.p[i];
-    float g = T.g[i];
-    if (wd != 0.f) g = fmaf(wd, pv, g);                        // grad.add(param, alpha=wd): ATen's fmadd
-    float m = T.m[i];
-    m = fmaf(omb1, __fsub_rn(g, m), m);                         // exp_avg.lerp_(grad, 1-b1): fmadd, w < 0.5
-    float v = __fmul_rn(T.v[i], b2);                                             // exp_avg_sq.mul_(b2)
-    v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));                         //   .addcmul_(g, g, 1-b2)
-    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), eps);     // sqrt(v)/sqrt(bc2) + eps
-    T.m[i] = m;
-    T.v[i] = v;
-    T.p[i] = __fadd_rn(pv, __fdiv_rn(__fmul_rn(-step_size, m), denom));          // addcdiv_(m, denom, -lr/bc1)
+  const int64_t i = i0 + 4 * threadIdx.x;
+  const bool vec = (((uintptr_t)T.p | (uintptr_t)T.g | (uintptr_t)T.m | (uintptr_t)T.v) & 15) == 0;
+  if (!vec) {
+    // unaligned arrays (a gradient view at an odd offset of the flat buffer): lane-consecutive elements
+    for (int64_t j = i0 + threadIdx.x; j < i0 + 1024 && j < T.n; j += 256) {
+      float p = T.p[j], m = T.m[j], v = T.v[j];
+      adam_elem(c, p, T.g[j], m, v);
+      T.m[j] = m;
+      T.v[j] = v;
+      T.p[j] = p;
+    }
+  } else if (i + 3 < T.n) {
+    float4 p = *reinterpret_cast<const float4*>(T.p + i);
+    const float4 g = *reinterpret_cast<const float4*>(T.g + i);
+    float4 m = *reinterpret_cast<const float4*>(T.m + i);
+    float4 v = *reinterpret_cast<const float4*>(T.v + i);
+    adam_elem(c, p.x, g.x, m.x, v.x);
+    adam_elem(c, p.y, g.y, m.y, v.y);
+    adam_elem(c, p.z, g.z, m.z, v.z);
+    adam_elem(c, p.w, g.w, m.w, v.w);
+    *reinterpret_cast<float4*>(T.m + i) = m;
+    *reinterpret_cast<float4*>(T.v + i) = v;
+    *reinterpret_cast<float4*>(T.p + i) = p;
+  } else {
+    for (int k = 0; k < 4; ++k) {
+      if (i + k >= T.n) break;
+      float p = T.p[i + k], m = T.m[i + k], v = T.v[i + k];
+      adam_elem(c, p, T.g[i + k], m, v);
+      T.m[i + k] = m;
+      T.v[i + k] = v;
+      T.p[i + k] = p;
+    }
   }
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(const AdamList list, float step_size, float omb1, float b2,
+                                                   float omb2, float eps, float wd, float bc2_sqrt) {
+  adam_block(list, AdamCoef{step_size, omb1, b2, omb2, eps, wd, bc2_sqrt});
 }
 
 // Graph-replayable Adam: one thread bumps the device step and derives the step's scalars in double
@@ -970,30 +1009,7 @@ __global__ void adam_prep_kernel(AdamDevState* st, double lr, double b1, double 
 }
 
 __global__ void __launch_bounds__(256) adam_dev_kernel(const AdamList list, const AdamDevState* __restrict__ st) {
-  int lo = 0, hi = list.n - 1;
-  const int bid = blockIdx.x;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (list.t[mid].block0 <= bid) lo = mid;
-    else hi = mid - 1;
-  }
-  const AdamTensor T = list.t[lo];
-  const int64_t i0 = (int64_t)(bid - T.block0) * 1024;
-  const float step_size = st->step_size, omb1 = st->omb1, b2 = st->b2, omb2 = st->omb2, eps = st->eps,
-              wd = st->wd, bc2_sqrt = st->bc2_sqrt;
-  for (int64_t i = i0 + threadIdx.x; i < i0 + 1024 && i < T.n; i += 256) {
-    const float pv = T.p[i];
-    float g = T.g[i];
-    if (wd != 0.f) g = fmaf(wd, pv, g);
-    float m = T.m[i];
-    m = fmaf(omb1, __fsub_rn(g, m), m);
-    float v = __fmul_rn(T.v[i], b2);
-    v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));
-    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), eps);
-    T.m[i] = m;
-    T.v[i] = v;
-    T.p[i] = __fadd_rn(pv, __fdiv_rn(__fmul_rn(-step_size, m), denom));
-  }
+  adam_block(list, AdamCoef{st->step_size, st->omb1, st->b2, st->omb2, st->eps, st->wd, st->bc2_sqrt});
 }
 
 // dL/dz of BCE-with-logits with the loss normalised by `denom` (torch: (sigmoid(z) - y) * 1, then

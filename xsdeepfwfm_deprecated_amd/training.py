@@ -158,23 +158,27 @@ class FusedTrainStep:
         params = [p for p in params if id(p) in cat_ids] + \
             [p for p in params if id(p) not in mlp_ids and id(p) not in cat_ids] + \
             [p for p in params if id(p) in mlp_ids]
-        total = sum(p.numel() for p in params)
-        self.n_tables = sum(p.numel() for p in params if id(p) in cat_ids)
-        self.n_bucket_a = sum(p.numel() for p in params if id(p) not in mlp_ids)
+        # every tensor's slice starts 16-byte aligned (offsets padded to 4 floats; the pads stay zero), so
+        # the Adam kernel takes its 16-byte path on every tensor
+        offs, total = [], 0
+        for p in params:
+            offs.append(total)
+            total += (p.numel() + 3) & ~3
+        self.n_tables = next((offs[i] for i, p in enumerate(params) if id(p) not in cat_ids), total)
+        self.n_bucket_a = next((offs[i] for i, p in enumerate(params) if id(p) in mlp_ids), total)
         self.sparse = dist is not None and bool(sparse_exchange) and self.n_tables > 0
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
         self.state = torch.zeros(_lib.ADAM_STATE_BYTES // 8, dtype=torch.int64, device=dev)
-        views, off = {}, 0
+        views = {}
         adam = (_lib.dfwfm_adam_tensor * len(params))()
         for i, p in enumerate(params):
-            n = p.numel()
+            n, off = p.numel(), offs[i]
             g, m, v = (t[off:off + n].view_as(p) for t in (self.grad, self.exp_avg, self.exp_avg_sq))
             p.grad = g
             views[id(p)] = g
             adam[i] = _lib.dfwfm_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n)
-            off += n
         self.params, self.adam, self.n_adam = params, adam, len(params)
         ptr = lambda t: None if t is None else views[id(t)].data_ptr()  # noqa: E731
         # sparse exchange: the backward leaves the categorical tables alone (no dense scatter); their rows
