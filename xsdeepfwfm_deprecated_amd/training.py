@@ -171,6 +171,10 @@ class FusedTrainStep:
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
         self.state = torch.zeros(_lib.ADAM_STATE_BYTES // 8, dtype=torch.int64, device=dev)
+        # Adam runs as two launches -- everything but the MLP (state), the MLP weights and biases
+        # (state_b) -- so that the first can overlap the weight-gradient GEMM; each state's step counter is
+        # bumped once per step, so both hold the same step and bias corrections
+        self.state_b = torch.zeros_like(self.state)
         views = {}
         adam = (_lib.dfwfm_adam_tensor * len(params))()
         for i, p in enumerate(params):
@@ -180,6 +184,9 @@ class FusedTrainStep:
             views[id(p)] = g
             adam[i] = _lib.dfwfm_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n)
         self.params, self.adam, self.n_adam = params, adam, len(params)
+        self.n_main = sum(1 for p in params if id(p) not in mlp_ids)  # params are ordered with the MLP last
+        self.adam_mlp = ctypes.cast(ctypes.addressof(adam) + self.n_main * ctypes.sizeof(_lib.dfwfm_adam_tensor),
+                                    ctypes.POINTER(_lib.dfwfm_adam_tensor))
         ptr = lambda t: None if t is None else views[id(t)].data_ptr()  # noqa: E731
         # sparse exchange: the backward leaves the categorical tables alone (no dense scatter); their rows
         # come from every rank's touched-row lists (_apply_sparse)
@@ -306,7 +313,7 @@ class FusedTrainStep:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
 
-    def _part1(self, n, denom):
+    def _part1(self, n, denom, phases=None):
         L, st, h = self.L, self._stream(), self.eng.handle
         self.grad.zero_()
         _lib.check(L.dfwfm_model_set_dense(h, *self.dense_args, st), "dfwfm_model_set_dense")
@@ -317,7 +324,8 @@ class FusedTrainStep:
         _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(self.out.data_ptr()), ctypes.c_void_p(self.y.data_ptr()), n,
                                     float(denom), ctypes.c_void_p(self.dlogit.data_ptr()),
                                     ctypes.c_void_p(self.loss_sum.data_ptr()), st), "dfwfm_bce_grad")
-        phases = _lib.BWD_TABLES if self._bucketed() else (_lib.BWD_TABLES | _lib.BWD_MLP_WEIGHTS)
+        if phases is None:
+            phases = _lib.BWD_TABLES if self._bucketed() else (_lib.BWD_TABLES | _lib.BWD_MLP_WEIGHTS)
         _lib.check(L.dfwfm_backward_phases(h, ctypes.c_void_p(self.dlogit.data_ptr()), ctypes.byref(self.grads),
                                            phases, st), "dfwfm_backward_phases")
         if self.sparse:
@@ -332,11 +340,23 @@ class FusedTrainStep:
     def _bucketed(self):
         return self.dist is not None and self.n_bucket_a < self.grad.numel()
 
-    def _part2(self):
+    def _adam_main(self):
         b1, b2 = self.betas
-        _lib.check(self.L.dfwfm_adam_step_dev(self.adam, self.n_adam, self.lr, b1, b2, self.eps, self.wd,
-                                              ctypes.c_void_p(self.state.data_ptr()), self._stream()),
-                   "dfwfm_adam_step_dev")
+        if self.n_main:
+            _lib.check(self.L.dfwfm_adam_step_dev(self.adam, self.n_main, self.lr, b1, b2, self.eps, self.wd,
+                                                  ctypes.c_void_p(self.state.data_ptr()), self._stream()),
+                       "dfwfm_adam_step_dev")
+
+    def _adam_mlp(self):
+        b1, b2 = self.betas
+        if self.n_adam > self.n_main:
+            _lib.check(self.L.dfwfm_adam_step_dev(self.adam_mlp, self.n_adam - self.n_main, self.lr, b1, b2, self.eps,
+                                                  self.wd, ctypes.c_void_p(self.state_b.data_ptr()), self._stream()),
+                       "dfwfm_adam_step_dev")
+
+    def _part2(self):
+        self._adam_main()
+        self._adam_mlp()
 
     def _exchange(self, run_part1b, run_apply=None):
         """Data parallelism: all-reduce the gradient buffer (RCCL).  Bucketed: the first bucket (every
@@ -376,6 +396,21 @@ class FusedTrainStep:
         s.wait_stream(torch.cuda.current_stream(self.dev))
         g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         ga = None
+        if self.dist is None and self.n_adam > self.n_main:
+            # one process: a single graph that forks after the backward's first part -- the weight-gradient
+            # GEMM and the MLP's Adam on a side stream, the other tensors' Adam (the 58 MB of tables) beside it
+            s1 = torch.cuda.Stream(self.dev)
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g1, stream=s):
+                    self._part1(self.B, denom, phases=_lib.BWD_TABLES)
+                    s1.wait_stream(s)
+                    with torch.cuda.stream(s1):
+                        self._part1b()
+                        self._adam_mlp()
+                    self._adam_main()
+                    s.wait_stream(s1)
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            return g1, None, None, None
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s):
                 self._part1(self.B, denom)
@@ -419,9 +454,10 @@ class FusedTrainStep:
                 self._graph_key = (denom, self.drop, self._ws_generation())
             g1, g1b, ga, g2 = self.graphs
             g1.replay()
-            self._exchange(lambda: g1b.replay() if g1b is not None else None,
-                           lambda: ga.replay() if ga is not None else None)
-            g2.replay()
+            if g2 is not None:  # else the whole step (backward parts and Adam) is in g1
+                self._exchange(lambda: g1b.replay() if g1b is not None else None,
+                               lambda: ga.replay() if ga is not None else None)
+                g2.replay()
         else:
             self._part1(n, denom)
             self._exchange(self._part1b if self._bucketed() else (lambda: None), self._apply_sparse)
