@@ -351,7 +351,22 @@ fwd_kernel(FwdArgs p) {
       // pieces' 10-deep chains of fwd_kernel's other forms left this phase latency-bound.  U' is the
       // strictly upper (R + R^T)/2 (FM: ones) read from the A-fragment pack in LDS.
       constexpr int SD = (D + 3) / 4;
+      constexpr int NTL = kMaxMT * (kMaxMT + 1) / 2;  // upper tiles (m <= n) at most
       const int MT = p.MT, S = p.S;
+      // this lane's U' entries of every upper tile, read once (the same for every sample): lane holds
+      // G[16m + 4(lane>>4) + r][16n + (lane&15)], and U'[k][l] sits in the pack at [(k/16) S + l/4][(k%16) + 16 (l%4)]
+      float uu[NTL][4];
+#pragma unroll
+      for (int m = 0, t = 0; m < kMaxMT; ++m)
+#pragma unroll
+        for (int n = m; n < kMaxMT; ++n, ++t) {
+          const int l = 16 * n + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 16 * m + 4 * (lane >> 4) + r;
+            uu[t][r] = (n < MT && l < 4 * S) ? upk[((k >> 4) * S + (l >> 2)) * 64 + (k & 15) + 16 * (l & 3)] : 0.f;
+          }
+        }
       for (int b = wave; b < kBM; b += NW) {
         float ev[kMaxMT][SD];
 #pragma unroll
@@ -362,25 +377,23 @@ fwd_kernel(FwdArgs p) {
             const int d = 4 * s + (lane >> 4);
             ev[m][s] = (m < MT && k < F && d < D) ? bufX[b * SX + k * D + d] : 0.f;
           }
+        // every upper tile's chain issued step by step across the tiles (independent accumulators), then the
+        // U'-weighted sum
+        f32x4 acc[NTL];
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < SD; ++s)
+#pragma unroll
+          for (int m = 0, t = 0; m < kMaxMT; ++m)
+#pragma unroll
+            for (int n = m; n < kMaxMT; ++n, ++t)
+              if (n < MT) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ev[m][s], ev[n][s], acc[t], 0, 0, 0);
         float part = 0.f;
 #pragma unroll
-        for (int m = 0; m < kMaxMT; ++m)
+        for (int t = 0; t < NTL; ++t)
 #pragma unroll
-          for (int n = m; n < kMaxMT; ++n) {
-            if (n >= MT) continue;  // wave-uniform
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < SD; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ev[m][s], ev[n][s], acc, 0, 0, 0);
-            // lane holds G[16m + 4(lane>>4) + r][16n + (lane&15)]; U'[k][l] sits in the pack at
-            // [(k/16) * S + l/4][(k%16) + 16 (l%4)]
-            const int l = 16 * n + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int k = 16 * m + 4 * (lane >> 4) + r;
-              const float u = (l < 4 * S) ? upk[((k >> 4) * S + (l >> 2)) * 64 + (k & 15) + 16 * (l & 3)] : 0.f;
-              part = fmaf(u, acc[r], part);
-            }
-          }
+          for (int r = 0; r < 4; ++r) part = fmaf(uu[t][r], acc[t][r], part);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
         if (lane == 0) part2[b] = part;
