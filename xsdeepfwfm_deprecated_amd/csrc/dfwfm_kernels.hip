@@ -45,6 +45,9 @@ namespace dfwfm {
 #define DFWFM_FWD_WPE 2  // register budget of two waves per SIMD (<= 256 per lane): a second batch's
                          // workgroup fits beside this one (stream-level overlap)
 #endif
+#ifndef DFWFM_P3_WPE
+#define DFWFM_P3_WPE 6  // MLP-free forward: six waves per SIMD (<= 80 registers): three workgroups per CU
+#endif
 // PART: 0 = the whole forward in one launch; 1 = stage, gather and shallow part only, E tile and
 // first + second to p.part_e / p.part_fs; 2 = MLP and combine from p.part_e / p.part_fs (the split
 // forward: two launches per batch, see launch_forward_split); 3 = a model without deep tower (no MLP
@@ -56,7 +59,7 @@ namespace dfwfm {
 // split tail tile rides on its register sets (mlp_k_loop_s)
 template <int D, int TPW, int KS, bool TRAIN, int PART, int NG, int NS>
 __global__ void __launch_bounds__(64 * NG * KS)
-__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (PART == 3 ? 4 : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE)))))
+__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (PART == 3 ? DFWFM_P3_WPE : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE)))))
 fwd_kernel(FwdArgs p) {
   static_assert(NG == 4 || (NG == 8 && KS == 1), "8 tile groups: no K split");
   constexpr int NTH = 64 * NG * KS;
@@ -111,7 +114,9 @@ fwd_kernel(FwdArgs p) {
   const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.fc), (short)0, p.NT * 16 * 4, 0x00020000);
   TailStream<NG> ts;
-  f32x4 tw[NS ? 1 : TailStream<NG>::C];  // preloaded tail fragments (NS == 0)
+  // NS is the MLP's static K-chunk count, except in the MLP-free PART 3, where it is the FwFM row-tile count
+  constexpr int NSK = PART == 3 ? 0 : NS;
+  f32x4 tw[NSK ? 1 : TailStream<NG>::C];  // preloaded tail fragments (NSK == 0)
   constexpr int TT = NG * TPW;  // the tail tile (when p.tail)
 
   constexpr bool train = TRAIN;
@@ -135,7 +140,7 @@ fwd_kernel(FwdArgs p) {
     const float fsv = tid < nrows ? p.part_fs[b0 + tid] : 0.f;
     ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
     DFWFM_PRELOAD(ls);
-    if constexpr (NS == 0) {
+    if constexpr (NSK == 0) {
       if (tail) {
         ts.init(0, p.NC0, TT, g);
         ts.load(wrsrc, tw, lane * 16);
@@ -351,15 +356,16 @@ fwd_kernel(FwdArgs p) {
       // pieces' 10-deep chains of fwd_kernel's other forms left this phase latency-bound.  U' is the
       // strictly upper (R + R^T)/2 (FM: ones) read from the A-fragment pack in LDS.
       constexpr int SD = (D + 3) / 4;
-      constexpr int NTL = kMaxMT * (kMaxMT + 1) / 2;  // upper tiles (m <= n) at most
+      constexpr int MTC = NS > 0 ? NS : kMaxMT;  // row tiles (PART 3 instantiates NS = MT: no idle registers)
+      constexpr int NTL = MTC * (MTC + 1) / 2;  // upper tiles (m <= n)
       const int MT = p.MT, S = p.S;
       // this lane's U' entries of every upper tile, read once (the same for every sample): lane holds
       // G[16m + 4(lane>>4) + r][16n + (lane&15)], and U'[k][l] sits in the pack at [(k/16) S + l/4][(k%16) + 16 (l%4)]
       float uu[NTL][4];
 #pragma unroll
-      for (int m = 0, t = 0; m < kMaxMT; ++m)
+      for (int m = 0, t = 0; m < MTC; ++m)
 #pragma unroll
-        for (int n = m; n < kMaxMT; ++n, ++t) {
+        for (int n = m; n < MTC; ++n, ++t) {
           const int l = 16 * n + (lane & 15);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -368,9 +374,9 @@ fwd_kernel(FwdArgs p) {
           }
         }
       for (int b = wave; b < kBM; b += NW) {
-        float ev[kMaxMT][SD];
+        float ev[MTC][SD];
 #pragma unroll
-        for (int m = 0; m < kMaxMT; ++m)
+        for (int m = 0; m < MTC; ++m)
 #pragma unroll
           for (int s = 0; s < SD; ++s) {
             const int k = 16 * m + (lane & 15);
@@ -385,9 +391,9 @@ fwd_kernel(FwdArgs p) {
 #pragma unroll
         for (int s = 0; s < SD; ++s)
 #pragma unroll
-          for (int m = 0, t = 0; m < kMaxMT; ++m)
+          for (int m = 0, t = 0; m < MTC; ++m)
 #pragma unroll
-            for (int n = m; n < kMaxMT; ++n, ++t)
+            for (int n = m; n < MTC; ++n, ++t)
               if (n < MT) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ev[m][s], ev[n][s], acc[t], 0, 0, 0);
         float part = 0.f;
 #pragma unroll
@@ -450,7 +456,7 @@ fwd_kernel(FwdArgs p) {
     }
   }
   // layer 0's tail fragments once the gather rows are dead (live across the gather, they spilled)
-  if constexpr (NS == 0) {
+  if constexpr (NSK == 0) {
     if (deep && tail) {
       ts.init(0, p.NC0, TT, g);
       ts.load(wrsrc, tw, lane * 16);
@@ -564,12 +570,12 @@ fwd_kernel(FwdArgs p) {
     f32x4 acc[TPW];
 #pragma unroll
     for (int j = 0; j < TPW; ++j) acc[j] = bq[j];  // the K loop accumulates onto the bias
-    if constexpr (NS > 0) {
+    if constexpr (NSK > 0) {
       // the tail tile's share rides on the K loop's register sets
       if (tail) ts.init(layer_off, NC, TT, g);
       else ts.cnt = 0;
       f32x4 tp;
-      mlp_k_loop_s<TPW, NG, NS, true>(acc, in, SA, ls, wb0, wb1, wb2, lane, ts, tp);
+      mlp_k_loop_s<TPW, NG, NSK, true>(acc, in, SA, ls, wb0, wb1, wb2, lane, ts, tp);
       if (tail) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = tp;
     } else {
       // the tail tile's share first: its fragments (loaded with the preload) are then dead during the K loop
@@ -637,7 +643,7 @@ fwd_kernel(FwdArgs p) {
     if (!last) {
       ls.init(wrsrc, layer_off, p.NT, p.NT, g, kh);
       DFWFM_PRELOAD(ls);
-      if constexpr (NS == 0) {
+      if constexpr (NSK == 0) {
         if (tail) {
           ts.init(layer_off, p.NT, TT, g);
           ts.load(wrsrc, tw, lane * 16);
@@ -833,7 +839,16 @@ static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t
   // no deep tower: the MLP-free instantiation on eight waves (105 registers, no scratch): 4.92 us per batch
   // at three batches in flight against 5.19 for the generic four-wave one (DFWFM_NO_PART3=1) and 6.0 for a
   // four-wave MLP-free one (128 registers + spills)
-  if (!(a.flags & (kHasDeep | kTrain)) && !getenv("DFWFM_NO_PART3")) return launch_fwd_t<D, 1, 1, false, 3, 8>(a, lds, s);
+  if (!(a.flags & (kHasDeep | kTrain)) && !getenv("DFWFM_NO_PART3")) {
+    // one instantiation per FwFM row-tile count (NS = MT): the Gram tiles' registers sized to the model
+    auto k = a.MT == 1 ? fwd_kernel<D, 1, 1, false, 3, 8, 1>
+           : a.MT == 2 ? fwd_kernel<D, 1, 1, false, 3, 8, 2>
+           : a.MT == 3 ? fwd_kernel<D, 1, 1, false, 3, 8, 3> : fwd_kernel<D, 1, 1, false, 3, 8, 4>;
+    hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((unsigned)((a.batch + kBM - 1) / kBM)), dim3(64 * 8), lds, s, a);
+    return hipGetLastError();
+  }
   if (a.flags & kTrain) return ng == 8 ? launch_fwd_8<D, 0, true>(a, tpw, lds, s) : launch_fwd_k<D, 1, true>(a, tpw, lds, s);
   if (ng == 8) return launch_fwd_8<D, 0>(a, tpw, lds, s);
   return ks == 2 ? launch_fwd_k<D, 2, false>(a, tpw, lds, s) : launch_fwd_k<D, 1, false>(a, tpw, lds, s);
