@@ -1,0 +1,174 @@
+// ubench_gather.hip -- what does the FwFM-only forward's gather cost by itself?
+// Criteo-39's categorical part: B = 4096 samples x 26 int64 indices into 26 tables of 10-float rows
+// (53 MB in all, the real field sizes), uniform random indices.  Each 16-sample tile: load the tile's
+// indices, gather its 416 rows into an LDS tile, barrier, one float per sample out (so nothing is dead).
+// Variants of the row loads (per wave instruction):
+//   0  one lane per row, 5 dwordx2 per row (fwd_kernel PART 3 today: 64 rows per instruction)
+//   1  five lanes per row, one dwordx2 each (12 rows per instruction, 60 lanes busy)
+//   2  ten lanes per row, one dword each (6 rows per instruction)
+// TILES: 16-sample tiles per workgroup (walked with the next tile's loads issued before this tile's
+// LDS stores: TILES > 1 is the persistent form).  Reports microseconds per 4096-sample batch with
+// NB batches in flight (one launch over NB batches, as NB streams would).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+constexpr int F = 26, D = 10, BM = 16, NTH = 512;
+
+struct Args {
+  const float* const* tabs;  // [F] table bases
+  const int64_t* xi;         // [NB*B][F]
+  float* out;                // [NB*B]
+  int64_t total;             // samples
+};
+
+template <int V>
+__device__ __forceinline__ void tile_loads(const Args& a, int64_t b0, int tid, float2 (&v2)[8], float (&v1)[16]) {
+  if constexpr (V == 0) {
+    const int r = tid;  // row r: field r / 16, sample r % 16
+    if (r < F * BM) {
+      const int f = r >> 4;
+      const int64_t idx = a.xi[(b0 + (r & 15)) * F + f];
+      const float2* src = reinterpret_cast<const float2*>(a.tabs[f] + idx * D);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) v2[j] = src[j];
+    }
+  } else if constexpr (V == 1) {
+    const int w = tid >> 6, lane = tid & 63;
+    const int rw = lane / 5, part = lane - rw * 5;  // 12 rows per wave per round
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {  // 8 waves x 12 rows x 5 rounds = 480 >= 416
+      const int r = (k * 8 + w) * 12 + rw;
+      if (rw < 12 && r < F * BM) {
+        const int f = r >> 4;
+        const int64_t idx = a.xi[(b0 + (r & 15)) * F + f];
+        v2[k] = reinterpret_cast<const float2*>(a.tabs[f] + idx * D)[part];
+      }
+    }
+  } else {
+    const int w = tid >> 6, lane = tid & 63;
+    const int rw = lane / 10, part = lane - rw * 10;  // 6 rows per wave per round
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {  // 8 x 6 x 9 = 432 >= 416
+      const int r = (k * 8 + w) * 6 + rw;
+      if (rw < 6 && r < F * BM) {
+        const int f = r >> 4;
+        const int64_t idx = a.xi[(b0 + (r & 15)) * F + f];
+        v1[k] = (a.tabs[f] + idx * D)[part];
+      }
+    }
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void tile_stores(float* E, int tid, const float2 (&v2)[8], const float (&v1)[16]) {
+  if constexpr (V == 0) {
+    const int r = tid;
+    if (r < F * BM) {
+      float2* dst = reinterpret_cast<float2*>(E + (r & 15) * (F * D + 2) + (r >> 4) * D);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) dst[j] = v2[j];
+    }
+  } else if constexpr (V == 1) {
+    const int w = tid >> 6, lane = tid & 63;
+    const int rw = lane / 5, part = lane - rw * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int r = (k * 8 + w) * 12 + rw;
+      if (rw < 12 && r < F * BM) reinterpret_cast<float2*>(E + (r & 15) * (F * D + 2) + (r >> 4) * D)[part] = v2[k];
+    }
+  } else {
+    const int w = tid >> 6, lane = tid & 63;
+    const int rw = lane / 10, part = lane - rw * 10;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int r = (k * 8 + w) * 6 + rw;
+      if (rw < 6 && r < F * BM) (E + (r & 15) * (F * D + 2) + (r >> 4) * D)[part] = v1[k];
+    }
+  }
+}
+
+template <int V, int TILES>
+__global__ void __launch_bounds__(NTH) gather_kernel(Args a) {
+  __shared__ float E[BM * (F * D + 2)];
+  const int tid = threadIdx.x;
+  float2 v2[8];
+  float v1[16];
+  for (int t = 0; t < TILES; ++t) {
+    const int64_t b0 = ((int64_t)blockIdx.x * TILES + t) * BM;
+    if (b0 >= a.total) break;
+    tile_loads<V>(a, b0, tid, v2, v1);
+    __syncthreads();  // the previous tile's sums are done with E
+    tile_stores<V>(E, tid, v2, v1);
+    __syncthreads();
+    if (tid < 64 * 4) {  // 16 lanes per sample
+      const int b = tid >> 4, q = tid & 15;
+      float s = 0.f;
+      for (int c = q; c < F * D; c += 16) s += E[b * (F * D + 2) + c];
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+      if (q == 0) a.out[b0 + b] = s;
+    }
+  }
+}
+
+// synth.CRITEO_FEATURE_SIZES (the 26 categorical fields bench.py's model uses: 1.33 M rows, 53 MB)
+static const int64_t kSizes[F] = {1458, 556, 245197, 166166, 306, 20, 12055, 634, 4, 46330, 5229, 243454, 3177,
+                                  27, 11745, 225322, 11, 4727, 2058, 5, 238640, 18, 16, 67856, 89, 50942};
+
+int main(int argc, char** argv) {
+  const int B = 4096;
+  const int NB = argc > 1 ? atoi(argv[1]) : 3;
+  const int reps = 200;
+  std::vector<int64_t> n(kSizes, kSizes + F);
+  int64_t rows = 0;
+  for (int f = 0; f < F; ++f) rows += n[f];
+  float* tab;
+  CHECK(hipMalloc(&tab, rows * D * 4));
+  CHECK(hipMemset(tab, 0, rows * D * 4));
+  std::vector<const float*> hb(F);
+  int64_t off = 0;
+  for (int f = 0; f < F; ++f) { hb[f] = tab + off * D; off += n[f]; }
+  const float** dtabs;
+  CHECK(hipMalloc(&dtabs, F * sizeof(float*)));
+  CHECK(hipMemcpy(dtabs, hb.data(), F * sizeof(float*), hipMemcpyHostToDevice));
+  const int64_t total = (int64_t)NB * B;
+  std::vector<int64_t> hx(total * F);
+  uint64_t s = 88172645463325252ull;
+  for (int64_t i = 0; i < total; ++i)
+    for (int f = 0; f < F; ++f) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; hx[i * F + f] = (int64_t)(s % (uint64_t)n[f]); }
+  int64_t* dx;
+  float* dout;
+  CHECK(hipMalloc(&dx, hx.size() * 8));
+  CHECK(hipMemcpy(dx, hx.data(), hx.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMalloc(&dout, total * 4));
+  Args a{dtabs, dx, dout, total};
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  auto run = [&](auto kern, int tiles, const char* name) {
+    const int grid = (int)((total / BM + tiles - 1) / tiles);
+    for (int i = 0; i < 50; ++i) kern<<<grid, NTH>>>(a);
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) kern<<<grid, NTH>>>(a);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    const double us_batch = ms * 1e3 / reps / NB;
+    const double alg = (double)B * (F * 8 + F * D * 4);  // indices + rows
+    printf("%-28s NB=%d tiles/wg=%d grid=%6d: %.3f us per 4096-sample batch, %.2f TB/s of index+row bytes\n", name, NB,
+           tiles, grid, us_batch, alg / (us_batch * 1e-6) / 1e12);
+  };
+  run(gather_kernel<0, 1>, 1, "lane per row (5 x dwordx2)");
+  run(gather_kernel<1, 1>, 1, "5 lanes per row (dwordx2)");
+  run(gather_kernel<2, 1>, 1, "10 lanes per row (dword)");
+  run(gather_kernel<0, 4>, 4, "lane per row, 4 tiles/wg");
+  run(gather_kernel<1, 4>, 4, "5 lanes per row, 4 tiles/wg");
+  return 0;
+}
