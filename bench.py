@@ -102,8 +102,10 @@ def kernel_name(config="deepfwfm"):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT select the A/B variants."""
     if config == "fwfm":
-        return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>" if os.environ.get("DFWFM_NO_PART3") else \
-            "dfwfm::fwd_kernel<10,1,1,false,3,8,0>"
+        if os.environ.get("DFWFM_NO_PART3"):
+            return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
+        ng = 4 if os.environ.get("DFWFM_P3_NG") == "4" else 8
+        return f"dfwfm::fwd_kernel<10,1,1,false,3,{ng},3,false>"  # MLP-free, 3 FwFM row tiles, no QR field
     ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
     tpw = 6 if ng == 4 else 3
     if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):
@@ -183,7 +185,7 @@ def main():
             xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=seed)
         batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
     # batches in flight: 2 fill the CUs' register files for the deep configs (two eight-wave workgroups per
-    # CU); the FwFM-only forward is latency-bound and gains from a third (5.2 vs 7.4 us per batch)
+    # CU); the FwFM-only forward is latency-bound and gains from a third (three eight-wave workgroups per CU)
     S = max(1, a.streams if a.streams is not None else (3 if a.config == "fwfm" else 2))
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
 

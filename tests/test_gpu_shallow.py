@@ -122,3 +122,29 @@ def test_default_mlp_free_kernel_ragged_and_full_size(gpu, monkeypatch, B):
     assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
     one = _run(m, xi[B - 1:], xv[B - 1:], gpu)
     assert one[0] == got[B - 1]
+
+
+@pytest.mark.parametrize("case", [dict(F=39, num=13, D=10), dict(F=39, num=13, D=10, fwlw=1, lw=0),
+                                  dict(F=64, num=0, D=16), dict(F=5, num=2, D=4), dict(F=39, num=13, D=32)],
+                         ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_mlp_free_four_and_eight_waves_bit_identical(gpu, monkeypatch, case):
+    """PART 3 on eight waves (the default) and on four (DFWFM_P3_NG=4, no QR operands): each sample's Gram sum
+    is formed by one wave in the same order, so the logits are bit-identical."""
+    cfg, params, xi, xv = _case(**case, B=4096 + 5, seed=11)
+    got8 = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
+    monkeypatch.setenv("DFWFM_P3_NG", "4")
+    got4 = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
+    monkeypatch.delenv("DFWFM_P3_NG")
+    assert np.array_equal(got4, got8)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close_scaled(got4, ref, cfg, params, xi, xv) < 1e-5
+
+
+@pytest.mark.parametrize("bad", [-1, "n"])
+def test_default_mlp_free_kernel_index_out_of_range_raises(gpu, monkeypatch, bad):
+    cfg, params, xi, xv = _case(39, 13, 10, B=64, seed=3)
+    xi = xi.copy()
+    xi[37, 5] = -1 if bad == -1 else cfg["feature_sizes"][13 + 5]
+    m = _model(cfg, params, gpu, monkeypatch, False)
+    with pytest.raises(IndexError):
+        _run(m, xi, xv, gpu)

@@ -99,21 +99,24 @@ struct LdsLayout {
 
 __host__ __device__ inline int r4(int x) { return (x + 3) & ~3; }
 
+// p3: the MLP-free forward (fwd_kernel PART 3): FwFM fragments read from global memory (no upk), fwlw only when
+// that first order is used, one FwFM sum per sample -- 30.7 KB at Criteo-39 (42.3 KB generic), so five
+// workgroups share a CU
 __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int SX, int SY, int TPW, int KS,
-                                                bool deep, bool tail, int NG = 4) {
+                                                bool deep, bool tail, int NG = 4, bool p3 = false, bool fwlw = true) {
   LdsLayout L;
   int o = 0;
   L.desc = o;  o += r4(14 * F);
   L.lw = o;    o += r4(F);
-  L.fwlw = o;  o += r4(F * D);
-  L.upk = o;   o += MT * S * 64;
+  L.fwlw = o;  o += (p3 && !fwlw) ? 0 : r4(F * D);
+  L.upk = o;   o += p3 ? 0 : MT * S * 64;
   L.bufX = o;  o += kBM * SX;
   L.bufY = o;  o += deep ? kBM * SY : 0;
   L.red = o;   o += (deep && KS == 2) ? 4 * TPW * 64 * 4 : 0;
   L.tailr = o; o += (deep && tail) ? NG * 64 * 4 + 4 * kBM : 0;  // partials + per-(wave, row) deep sums of the tail
   L.fo = o;    o += kBM * r4(F);
-  L.part2 = o; o += MT * D * 16;  // per FwFM piece, its 16 column sums
-  L.dsum = o;  o += NG * kBM;
+  L.part2 = o; o += p3 ? kBM : MT * D * 16;  // per FwFM piece, its 16 column sums (p3: per sample)
+  L.dsum = o;  o += p3 ? 0 : NG * kBM;
   L.fs = o;    o += kBM;
   L.total = r4(o);
   return L;

@@ -46,20 +46,26 @@ namespace dfwfm {
                          // workgroup fits beside this one (stream-level overlap)
 #endif
 #ifndef DFWFM_P3_WPE
-#define DFWFM_P3_WPE 6  // MLP-free forward: six waves per SIMD (<= 80 registers): three workgroups per CU
+#define DFWFM_P3_WPE 6  // MLP-free forward on eight waves: six waves per SIMD (<= 80 registers): three workgroups per CU
+#endif
+#ifndef DFWFM_P3_WPE4
+#define DFWFM_P3_WPE4 5  // MLP-free forward on four waves: five waves per SIMD (<= 96 registers): five workgroups
+                         // per CU (LDS 30.7 KB each at Criteo-39)
 #endif
 // PART: 0 = the whole forward in one launch; 1 = stage, gather and shallow part only, E tile and
 // first + second to p.part_e / p.part_fs; 2 = MLP and combine from p.part_e / p.part_fs (the split
 // forward: two launches per batch, see launch_forward_split); 3 = a model without deep tower (no MLP
-// code: 105 registers on eight waves instead of the generic kernel's 165 on four)
+// code, trimmed LDS, FwFM fragments read from global memory: 70 registers on eight waves)
 // NG: MLP output-tile groups = waves (4: one wave per SIMD, <= 256 registers; 8: two per SIMD, <= 128
 // registers, so one workgroup issues MFMAs from two waves per SIMD while a second batch's workgroup
 // on the same CU runs its gather; the training variant, one batch in flight, keeps 256 registers)
 // NS: every layer has NS K chunks and NS output tiles (0: any) -- the K loop is then fully static and the
 // split tail tile rides on its register sets (mlp_k_loop_s)
-template <int D, int TPW, int KS, bool TRAIN, int PART, int NG, int NS>
+// QR: some field may be a QR embedding (false: the gather carries no second operand -- PART 3 only)
+template <int D, int TPW, int KS, bool TRAIN, int PART, int NG, int NS, bool QR = true>
 __global__ void __launch_bounds__(64 * NG * KS)
-__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (PART == 3 ? DFWFM_P3_WPE : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE)))))
+__attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (PART == 3 ? (NG == 4 ? DFWFM_P3_WPE4 : DFWFM_P3_WPE)
+                                                               : (NG == 8 ? (TRAIN ? 2 : 4) : DFWFM_FWD_WPE)))))
 fwd_kernel(FwdArgs p) {
   static_assert(NG == 4 || (NG == 8 && KS == 1), "8 tile groups: no K split");
   constexpr int NTH = 64 * NG * KS;
@@ -77,7 +83,8 @@ fwd_kernel(FwdArgs p) {
   const bool deep = PART != 1 && PART != 3 && (flags & kHasDeep) != 0;  // the MLP runs in this launch
   const int Fp = r4(F);
   const bool tail = KS == 1 && p.tail != 0;
-  const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep, tail, NG);  // PART 1: no MLP buffers
+  const LdsLayout L = lds_layout(F, D, p.MT, p.S, SX, SY, TPW, KS, deep, tail, NG, PART == 3,
+                                 (flags & kFoFwlw) != 0);  // PART 1: no MLP buffers; PART 3: trimmed
   FieldDev* desc = reinterpret_cast<FieldDev*>(smem + L.desc);
   float* lw_s = smem + L.lw;
   float* fwlw_s = smem + L.fwlw;
@@ -192,7 +199,7 @@ fwd_kernel(FwdArgs p) {
     }
   }
   f32x4 uw[kUpkPT];
-  const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
+  const int n_upk = (PART != 3 && (flags & kHasSecond)) ? p.MT * p.S * 16 : 0;  // PART 3 reads them from global
 #pragma unroll
   for (int k = 0; k < kUpkPT; ++k) {
     const int i = tid + k * NTH;
@@ -214,14 +221,40 @@ fwd_kernel(FwdArgs p) {
   __syncthreads();
   stamp(p.stamps, 1, tid);
 
+  // PART 3: this lane's U' entries of every upper Gram tile (the same for every sample), loaded from the packed
+  // A fragments in global memory (L2) behind the gather's row loads: lane holds
+  // G[16m + 4(lane>>4) + r][16n + (lane&15)], and U'[k][l] sits in the pack at [(k/16) S + l/4][(k%16) + 16 (l%4)]
+  constexpr int P3_MTC = NS > 0 ? NS : kMaxMT;  // row tiles (PART 3 instantiates NS = MT: no idle registers)
+  constexpr int P3_NTL = PART == 3 ? P3_MTC * (P3_MTC + 1) / 2 : 1;  // upper tiles (m <= n)
+  float uu[P3_NTL][4];
+  auto load_uu = [&]() {
+    if constexpr (PART == 3) {
+      const float* up = p.upack;
+      const int MT = p.MT, S = p.S;
+#pragma unroll
+      for (int m = 0, t = 0; m < P3_MTC; ++m)
+#pragma unroll
+        for (int n = m; n < P3_MTC; ++n, ++t) {
+          const int l = 16 * n + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 16 * m + 4 * (lane >> 4) + r;
+            uu[t][r] = ((flags & kHasSecond) && n < MT && l < 4 * S)
+                           ? up[((k >> 4) * S + (l >> 2)) * 64 + (k & 15) + 16 * (l & 3)] : 0.f;
+          }
+        }
+    }
+  };
+
   // ---- phase G: gather E rows and table first order --------------------------
   {
     const bool needE = (flags & kNeedE) != 0;
     const bool fo_tab = (flags & kFoTables) != 0;
     const float* pa[RPT];
-    const float* pb[RPT];
+    constexpr int RQ = QR ? RPT : 1;  // QR second operands
+    const float* pb[RQ];
     const float* qa[RPT];
-    const float* qb[RPT];
+    const float* qb[RQ];
     float scale[RPT];
     int mode[RPT];
     bool live[RPT];
@@ -230,7 +263,8 @@ fwd_kernel(FwdArgs p) {
       const int r = tid + k * NTH;
       const int f = r >> 4;
       live[k] = f < F && (b0 + (r & 15)) < p.batch;
-      pa[k] = pb[k] = qa[k] = qb[k] = nullptr;
+      pa[k] = qa[k] = nullptr;
+      if constexpr (QR) pb[k] = qb[k] = nullptr;
       scale[k] = 1.f;
       mode[k] = 0;
       if (live[k]) {
@@ -245,10 +279,10 @@ fwd_kernel(FwdArgs p) {
             atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
             idx = 0;
           }
-          if (fd.c == 0) {
+          if (!QR || fd.c == 0) {
             pa[k] = fd.emb2 + idx * D;
             if (fo_tab) qa[k] = fd.emb1 + idx;
-          } else {
+          } else if constexpr (QR) {
             const int64_t q = idx / fd.c;
             const int64_t rr = idx - q * fd.c;
             mode[k] = fd.op == 0 ? 1 : 2;
@@ -263,19 +297,26 @@ fwd_kernel(FwdArgs p) {
       }
     }
     // all loads first (the second operand only for QR rows) ...
-    float va[RPT][D], vb[RPT][D], fa[RPT], fb[RPT];
+    float va[RPT][D], vb[RQ][D], fa[RPT], fb[RQ];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      fa[k] = fb[k] = 0.f;
+      fa[k] = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) va[k][d] = vb[k][d] = 0.f;
+      for (int d = 0; d < D; ++d) va[k][d] = 0.f;
+      if constexpr (QR) {
+        fb[k] = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
+      }
       if (live[k] && needE) {
         load_row<D>(va[k], pa[k]);
-        if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
+        if constexpr (QR)
+          if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
       }
       if (live[k] && fo_tab) {
         fa[k] = *qa[k];
-        if (mode[k] != 0) fb[k] = *qb[k];
+        if constexpr (QR)
+          if (mode[k] != 0) fb[k] = *qb[k];
       }
     }
     // layer-0 weights: the first two chunks go out behind the row loads (vmcnt retires in issue order, so
@@ -285,6 +326,7 @@ fwd_kernel(FwdArgs p) {
       ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
       DFWFM_PRELOAD(ls);
     }
+    if constexpr (!QR) load_uu();  // PART 3: behind the row loads (vmcnt retires in order); QR: no room
     // ... the shallow parameters go to LDS while the row loads are in flight ...
 #pragma unroll
     for (int k = 0; k < kUpkPT; ++k) {
@@ -313,10 +355,10 @@ fwd_kernel(FwdArgs p) {
         if (needE) {
           float e[D];
 #pragma unroll
-          for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(mode[k], va[k][d], vb[k][d], scale[k]) : 0.f;
+          for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(mode[k], va[k][d], QR ? vb[k][d] : 0.f, scale[k]) : 0.f;
           store_row<D>(bufX + b * SX + f * D, e);
         }
-        fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], fb[k], scale[k]) : 0.f;
+        fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], QR ? fb[k] : 0.f, scale[k]) : 0.f;
       }
     }
   }
@@ -356,23 +398,10 @@ fwd_kernel(FwdArgs p) {
       // pieces' 10-deep chains of fwd_kernel's other forms left this phase latency-bound.  U' is the
       // strictly upper (R + R^T)/2 (FM: ones) read from the A-fragment pack in LDS.
       constexpr int SD = (D + 3) / 4;
-      constexpr int MTC = NS > 0 ? NS : kMaxMT;  // row tiles (PART 3 instantiates NS = MT: no idle registers)
-      constexpr int NTL = MTC * (MTC + 1) / 2;  // upper tiles (m <= n)
-      const int MT = p.MT, S = p.S;
-      // this lane's U' entries of every upper tile, read once (the same for every sample): lane holds
-      // G[16m + 4(lane>>4) + r][16n + (lane&15)], and U'[k][l] sits in the pack at [(k/16) S + l/4][(k%16) + 16 (l%4)]
-      float uu[NTL][4];
-#pragma unroll
-      for (int m = 0, t = 0; m < MTC; ++m)
-#pragma unroll
-        for (int n = m; n < MTC; ++n, ++t) {
-          const int l = 16 * n + (lane & 15);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int k = 16 * m + 4 * (lane >> 4) + r;
-            uu[t][r] = (n < MT && l < 4 * S) ? upk[((k >> 4) * S + (l >> 2)) * 64 + (k & 15) + 16 * (l & 3)] : 0.f;
-          }
-        }
+      constexpr int MTC = P3_MTC;
+      constexpr int NTL = P3_NTL;
+      const int MT = p.MT;
+      if constexpr (QR) load_uu();
       for (int b = wave; b < kBM; b += NW) {
         float ev[MTC][SD];
 #pragma unroll
@@ -840,13 +869,32 @@ static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t
   // at three batches in flight against 5.19 for the generic four-wave one (DFWFM_NO_PART3=1) and 6.0 for a
   // four-wave MLP-free one (128 registers + spills)
   if (!(a.flags & (kHasDeep | kTrain)) && !getenv("DFWFM_NO_PART3")) {
-    // one instantiation per FwFM row-tile count (NS = MT): the Gram tiles' registers sized to the model
-    auto k = a.MT == 1 ? fwd_kernel<D, 1, 1, false, 3, 8, 1>
-           : a.MT == 2 ? fwd_kernel<D, 1, 1, false, 3, 8, 2>
-           : a.MT == 3 ? fwd_kernel<D, 1, 1, false, 3, 8, 3> : fwd_kernel<D, 1, 1, false, 3, 8, 4>;
-    hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
+    // one instantiation per FwFM row-tile count (NS = MT): the Gram tiles' registers sized to the model.  Eight
+    // waves (70 registers, three workgroups per CU: 3.55 us per batch at three batches in flight); DFWFM_P3_NG=4
+    // selects four waves without QR operands (94 registers, five workgroups per CU by the trimmed LDS: 3.74 us
+    // at three or six in flight, profiles/r02/r02r_*); a model with a QR field always takes eight (four would
+    // spill the QR rows' second operands)
+    const char* png = getenv("DFWFM_P3_NG");
+    const bool qr = (a.flags & kHasQR) != 0;
+    const bool w8 = qr || !png || atoi(png) != 4;
+    auto pick = [&](auto ng_, auto qr_) {
+      constexpr int NG = decltype(ng_)::value;
+      constexpr bool Q = decltype(qr_)::value;
+      return a.MT == 1 ? fwd_kernel<D, 1, 1, false, 3, NG, 1, Q>
+           : a.MT == 2 ? fwd_kernel<D, 1, 1, false, 3, NG, 2, Q>
+           : a.MT == 3 ? fwd_kernel<D, 1, 1, false, 3, NG, 3, Q> : fwd_kernel<D, 1, 1, false, 3, NG, 4, Q>;
+    };
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    using T = std::true_type;
+    using Fl = std::false_type;
+    auto k = qr ? pick(I8{}, T{}) : (w8 ? pick(I8{}, Fl{}) : pick(I4{}, Fl{}));
+    const int ng = w8 ? 8 : 4;
+    const size_t lds3 = sizeof(float) * (size_t)lds_layout(a.F, D, a.MT, a.S, a.SX, a.SY, 1, 1, false, false, ng,
+                                                            true, (a.flags & kFoFwlw) != 0).total;
+    hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds3);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3((unsigned)((a.batch + kBM - 1) / kBM)), dim3(64 * 8), lds, s, a);
+    hipLaunchKernelGGL(k, dim3((unsigned)((a.batch + kBM - 1) / kBM)), dim3(64 * ng), lds3, s, a);
     return hipGetLastError();
   }
   if (a.flags & kTrain) return ng == 8 ? launch_fwd_8<D, 0, true>(a, tpw, lds, s) : launch_fwd_k<D, 1, true>(a, tpw, lds, s);
