@@ -353,6 +353,15 @@ def main():
         result["roofline_hbm"] = hbm
     else:                # gather + FwFM only: ~12 FLOP/B, below the f32 ridge -> HBM-bound
         result["roofline"] = {**hbm, **common}
+        if traffic:      # the fabric rate of the PMC-counted bytes (40-B rows fetched as 128-B lines)
+            result["roofline"]["traffic_gbs"] = round(traffic * S / (launch_ms / 1e3) / 1e9, 1)
+        if a.config == "fwfm" and a.inputs == "uniform":
+            # the same 26 rows x 4096 samples from the same tables and nothing else (tools/ubench_gather.hip,
+            # one lane per row, three batches in flight): what the gather alone costs at this concurrency
+            floor_us = 1.596
+            result["roofline"]["gather_floor"] = {
+                "us_per_batch": floor_us, "frac": round(floor_us / (ms_per_step * 1e3), 4),
+                "source": "tools/ubench_gather.hip 3 (profiles/r02/r02q_ubench_gather_nb3.log)"}
         result["roofline_mfma"] = mfma
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(cfg, params, sizes, a.cpu_seconds, model, dev)

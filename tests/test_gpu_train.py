@@ -695,3 +695,29 @@ def test_data_parallel_step_equals_single_process_global_batch(gpu, name):
     for k in gs:
         sc = np.abs(gs[k]).max()
         assert np.abs(gd[k] - g0[k]).max() <= G_TOL * sc + 1e-12, k
+
+
+def test_resident_inputs_graphs_equal_copied_inputs(gpu):
+    """FusedTrainStep(resident_inputs=True) replays one captured graph set per resident (xi, xv, y) buffer set,
+    reading the batches in place; the parameters after 6 steps over 3 resident batches equal the copying path's
+    (the same kernels on the same values, dropout included with the same seed) up to the weight-gradient GEMM's
+    split-K float atomics, which make two runs of either path differ in the last bits -- the DP test's bar."""
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_lw")
+    B = 64
+    bat = [tuple(torch.from_numpy(a).to(gpu) for a in b) for b in _batches(cfg, xi, xv, y, B, 3)]
+    res = []
+    for resident in (False, True):
+        m = build(cfg, params, gpu, is_deep_dropout=True)
+        m.train()
+        torch.manual_seed(5)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, resident_inputs=resident)
+        for k in range(6):
+            t.step(*bat[k % 3])
+        torch.cuda.synchronize()
+        if resident:
+            assert len(t._graph_sets) == 3  # one graph set per resident batch
+        res.append({n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()})
+        t.close()
+    e = np.concatenate([np.abs(res[0][n] - res[1][n]).reshape(-1) / 1e-3 for n in res[0]])
+    assert np.median(e) < 1e-4 and np.quantile(e, 0.999) < 0.02, (np.median(e), np.quantile(e, 0.999))

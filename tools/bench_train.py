@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
     ap.add_argument("--no-dropout", action="store_true")
+    ap.add_argument("--copy-inputs", action="store_true",
+                    help="copy every batch into the fused step's own input buffers (fit()'s path) instead of "
+                         "reading the resident batches in place")
     ap.add_argument("--mode", choices=["fused", "autograd"], default="fused",
                     help="fused: FusedTrainStep (HIP-graph replay, what fit() runs); autograd: model() + "
                          "loss.backward() + HIP Adam")
@@ -64,7 +67,9 @@ def main():
     trainer = None
     if a.mode == "fused":
         dist = torch.distributed if world > 1 else None
-        trainer = FusedTrainStep(model, B, lr=1e-3, weight_decay=3e-7, dist=dist)
+        # the four resident batches are read in place (one captured graph set each), like a loader's ring of
+        # device input buffers; --copy-inputs copies each batch into the step's own buffers first
+        trainer = FusedTrainStep(model, B, lr=1e-3, weight_decay=3e-7, dist=dist, resident_inputs=not a.copy_inputs)
 
     def step(i):
         xi, xv, y = batches[i % 4]
@@ -102,7 +107,8 @@ def main():
            "value": round(world * B * a.steps / (ms / 1e3), 1), "unit": "samples/s", "n_gpus": world,
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms / a.steps, 4), "per_gpu_batch": B,
            "first_order": a.first_order, "dropout": not a.no_dropout, "wall_s": round(wall, 3),
-           "mode": a.mode, "final_loss_sum": round(float(loss.item()), 4)}
+           "mode": a.mode, "inputs": "copied" if (a.copy_inputs or a.mode != "fused") else "resident (read in place)",
+           "final_loss_sum": round(float(loss.item()), 4)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -126,10 +126,15 @@ class FusedTrainStep:
     buffer, so a data-parallel all-reduce is one call).  Adam's step counter and bias corrections, and
     the dropout seed, are read from device memory, so every replay is a fresh step.  Under
     torch.distributed the loss is normalised by the global batch and the step is split into two graphs
-    around an RCCL all-reduce of the gradient buffer."""
+    around an RCCL all-reduce of the gradient buffer.
+
+    resident_inputs: full batches whose (xi, xv, y) tensors recur (a ring of device-resident input buffers,
+    e.g. a loader double-buffering into fixed tensors) are read in place -- one captured graph set per buffer
+    set (at most ``max_graph_sets``, least recently used dropped) -- instead of being copied into the step's
+    own input buffers first (three copy launches per step)."""
 
     def __init__(self, model, batch_size, lr=1e-3, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8,
-                 use_graph=True, dist=None, sparse_exchange=True):
+                 use_graph=True, dist=None, sparse_exchange=True, resident_inputs=False, max_graph_sets=8):
         dev = model._device()
         if dev.type != "cuda":
             raise _lib.DfwfmError("FusedTrainStep runs only on a HIP device")
@@ -138,6 +143,9 @@ class FusedTrainStep:
         self.lr, self.wd, self.betas, self.eps = float(lr), float(weight_decay), tuple(betas), float(eps)
         self.dist = dist
         self.use_graph = use_graph
+        self.resident_inputs = bool(resident_inputs)
+        self.max_graph_sets = max(1, int(max_graph_sets))
+        self._graph_sets = {}  # (denom, drop, workspace generation, input pointers) -> (graphs, inputs)
         self.eng = model._sync_engine(dev)
         self.L = _lib.lib()
         params = [p for p in model.parameters() if p.requires_grad]
@@ -210,6 +218,7 @@ class FusedTrainStep:
         self.xi = torch.zeros(self.B, max(ncat, 1), dtype=torch.int64, device=dev)
         self.xv = torch.zeros(self.B, max(num, 1), dtype=torch.float32, device=dev)
         self.y = torch.zeros(self.B, dtype=torch.float32, device=dev)
+        self._in = (self.xi, self.xv, self.y)  # the inputs _part1 launches on
         self.out = torch.zeros(self.B, dtype=torch.float32, device=dev)
         self.dlogit = torch.zeros(self.B, dtype=torch.float32, device=dev)
         self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -298,6 +307,7 @@ class FusedTrainStep:
             self.L.dfwfm_set_step_source(eng.handle, None)
         self._attached = False
         self.graphs = None
+        self._graph_sets = {}
 
     def __del__(self):
         try:
@@ -317,11 +327,12 @@ class FusedTrainStep:
         L, st, h = self.L, self._stream(), self.eng.handle
         self.grad.zero_()
         _lib.check(L.dfwfm_model_set_dense(h, *self.dense_args, st), "dfwfm_model_set_dense")
-        _lib.check(L.dfwfm_train_forward(h, ctypes.c_void_p(self.xi.data_ptr()), self.xi.stride(0),
-                                         ctypes.c_void_p(self.xv.data_ptr()), self.xv.stride(0), n,
+        xi, xv, y = self._in
+        _lib.check(L.dfwfm_train_forward(h, ctypes.c_void_p(xi.data_ptr()), xi.stride(0),
+                                         ctypes.c_void_p(xv.data_ptr()), xv.stride(0), n,
                                          ctypes.c_void_p(self.out.data_ptr()), self.drop, self.seed, st),
                    "dfwfm_train_forward")
-        _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(self.out.data_ptr()), ctypes.c_void_p(self.y.data_ptr()), n,
+        _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(self.out.data_ptr()), ctypes.c_void_p(y.data_ptr()), n,
                                     float(denom), ctypes.c_void_p(self.dlogit.data_ptr()),
                                     ctypes.c_void_p(self.loss_sum.data_ptr()), st), "dfwfm_bce_grad")
         if phases is None:
@@ -428,6 +439,21 @@ class FusedTrainStep:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         return g1, g1b, ga, g2
 
+    def _direct_inputs(self, xi, xv, y, n):
+        """(xi, xv, y) as the graphs can read them in place, or None (then they are copied): a full batch of
+        row-contiguous int64 indices, float32 values and float32 labels on this device."""
+        xi2 = xi.reshape(n, -1) if xi.is_contiguous() else None
+        if (xi2 is None or xi2.dtype != torch.int64 or xi2.device != self.dev or xi2.shape[1] != self.xi.shape[1]
+                or y.dtype != torch.float32 or y.device != self.dev or y.dim() != 1 or not y.is_contiguous()):
+            return None
+        if self.num:
+            if (xv.dtype != torch.float32 or xv.device != self.dev or xv.dim() != 2 or xv.stride(1) != 1
+                    or xv.shape[1] < self.num):
+                return None
+        else:
+            xv = self.xv
+        return (xi2, xv, y)
+
     def step(self, xi, xv, y, n_global=None):
         """One step on device tensors xi [n, F-num] int64, xv [n, num] f32, y [n] f32 (n <= batch_size);
         n_global = rows of the global batch under data parallelism (loss normaliser)."""
@@ -435,23 +461,35 @@ class FusedTrainStep:
         if n > self.B:
             raise ValueError(f"batch of {n} rows exceeds the step's {self.B}")
         denom = float(max(n_global if n_global is not None else n, 1))
-        if n:
-            self.xi[:n].copy_(xi.reshape(n, -1))
-            if self.num:
-                self.xv[:n].copy_(xv[:, :self.num])
-            self.y[:n].copy_(y)
-        self.drop = self.drop_train if self.model.training else 0.0  # nn.Dropout is off in eval mode
         full = n == self.B
+        use_graph = self.use_graph and full and self.steps >= 1
+        direct = self._direct_inputs(xi, xv, y, n) if (use_graph and self.resident_inputs) else None
+        if direct is None:
+            if n:
+                self.xi[:n].copy_(xi.reshape(n, -1))
+                if self.num:
+                    self.xv[:n].copy_(xv[:, :self.num])
+                self.y[:n].copy_(y)
+            inputs = (self.xi, self.xv, self.y)
+        else:
+            inputs = direct
+        self.drop = self.drop_train if self.model.training else 0.0  # nn.Dropout is off in eval mode
         if not self._attached:
             raise RuntimeError("FusedTrainStep.step after close()")
-        if self.use_graph and full and self.steps >= 1:
+        if use_graph:
             # the graphs bake in the engine's activation workspace: a train forward at a larger batch
-            # elsewhere (e.g. autograd) re-allocates it, and then the graphs are re-captured
-            key = (denom, self.drop, self._ws_generation())
-            if self.graphs is None or self._graph_key != key:
-                self.graphs = None
-                self.graphs = self._capture(denom)
-                self._graph_key = (denom, self.drop, self._ws_generation())
+            # elsewhere (e.g. autograd) re-allocates it, and then the graphs are re-captured; and they bake in
+            # the input pointers: one graph set per resident input buffer set
+            key = (denom, self.drop, self._ws_generation(), tuple(t.data_ptr() for t in inputs))
+            hit = self._graph_sets.pop(key, None)
+            if hit is None:
+                if len(self._graph_sets) >= self.max_graph_sets:
+                    self._graph_sets.pop(next(iter(self._graph_sets)))
+                self._in = inputs
+                hit = (self._capture(denom), inputs)
+            self._graph_sets[key] = hit  # most recently used last
+            self.graphs = hit[0]
+            self._graph_key = key
             g1, g1b, ga, g2 = self.graphs
             g1.replay()
             if g2 is not None:  # else the whole step (backward parts and Adam) is in g1
@@ -459,6 +497,7 @@ class FusedTrainStep:
                                lambda: ga.replay() if ga is not None else None)
                 g2.replay()
         else:
+            self._in = inputs
             self._part1(n, denom)
             self._exchange(self._part1b if self._bucketed() else (lambda: None), self._apply_sparse)
             self._part2()
