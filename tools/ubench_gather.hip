@@ -6,6 +6,7 @@
 //   0  one lane per row, 5 dwordx2 per row (fwd_kernel PART 3 today: 64 rows per instruction)
 //   1  five lanes per row, one dwordx2 each (12 rows per instruction, 60 lanes busy)
 //   2  ten lanes per row, one dword each (6 rows per instruction)
+//   3  one lane per row, two 16-B aligned dwordx4 + one dwordx2 placed by the row's alignment (3 loads per row)
 // TILES: 16-sample tiles per workgroup (walked with the next tile's loads issued before this tile's
 // LDS stores: TILES > 1 is the persistent form).  Reports microseconds per 4096-sample batch with
 // NB batches in flight (one launch over NB batches, as NB streams would).
@@ -37,6 +38,21 @@ __device__ __forceinline__ void tile_loads(const Args& a, int64_t b0, int tid, f
       const float2* src = reinterpret_cast<const float2*>(a.tabs[f] + idx * D);
 #pragma unroll
       for (int j = 0; j < 5; ++j) v2[j] = src[j];
+    }
+  } else if constexpr (V == 3) {  // one lane per row: two aligned dwordx4 + one dwordx2 (fwd_kernel's load_row_x4)
+    const int r = tid;
+    if (r < F * BM) {
+      const int f = r >> 4;
+      const int64_t idx = a.xi[(b0 + (r & 15)) * F + f];
+      const float* src = a.tabs[f] + idx * D;
+      const bool al = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+      const float* q = al ? src : src + 2;
+      const float* t = al ? src + 8 : src;
+      const float4 x0 = reinterpret_cast<const float4*>(q)[0], x1 = reinterpret_cast<const float4*>(q)[1];
+      const float2 c = *reinterpret_cast<const float2*>(t);
+      v1[0] = al ? x0.x : c.x; v1[1] = al ? x0.y : c.y; v1[2] = al ? x0.z : x0.x; v1[3] = al ? x0.w : x0.y;
+      v1[4] = al ? x1.x : x0.z; v1[5] = al ? x1.y : x0.w; v1[6] = al ? x1.z : x1.x; v1[7] = al ? x1.w : x1.y;
+      v1[8] = al ? c.x : x1.z; v1[9] = al ? c.y : x1.w;
     }
   } else if constexpr (V == 1) {
     const int w = tid >> 6, lane = tid & 63;
@@ -73,6 +89,13 @@ __device__ __forceinline__ void tile_stores(float* E, int tid, const float2 (&v2
       float2* dst = reinterpret_cast<float2*>(E + (r & 15) * (F * D + 2) + (r >> 4) * D);
 #pragma unroll
       for (int j = 0; j < 5; ++j) dst[j] = v2[j];
+    }
+  } else if constexpr (V == 3) {
+    const int r = tid;
+    if (r < F * BM) {
+      float2* dst = reinterpret_cast<float2*>(E + (r & 15) * (F * D + 2) + (r >> 4) * D);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) dst[j] = make_float2(v1[2 * j], v1[2 * j + 1]);
     }
   } else if constexpr (V == 1) {
     const int w = tid >> 6, lane = tid & 63;
@@ -166,6 +189,7 @@ int main(int argc, char** argv) {
            tiles, grid, us_batch, alg / (us_batch * 1e-6) / 1e12);
   };
   run(gather_kernel<0, 1>, 1, "lane per row (5 x dwordx2)");
+  run(gather_kernel<3, 1>, 1, "lane per row (2 x4 + 1 x2)");
   run(gather_kernel<1, 1>, 1, "5 lanes per row (dwordx2)");
   run(gather_kernel<2, 1>, 1, "10 lanes per row (dword)");
   run(gather_kernel<0, 4>, 4, "lane per row, 4 tiles/wg");
