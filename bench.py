@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=600)
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
-    ap.add_argument("--config", choices=["deepfwfm", "fwfm", "qr", "pruned"], default="deepfwfm",
+    ap.add_argument("--config", choices=["deepfwfm", "fwfm", "qr", "pruned", "fwfm_pruned"], default="deepfwfm",
                     help="BASELINE.json configs[1] (default), fwfm = configs[0]'s model (use_fwfm=1 use_deep=0: the "
                          "HBM-bound gather path) at Criteo-39 batch 4096, [2] QR embeddings (embedding_bag=1 "
                          "qr_flag=1, c=4, threshold 200, mult), [3] pruned (sparse 0.90, emb_r 0.444, prune_r 1: "
@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--sparse-mlp", type=float, default=None,
                     help="DeepFMs.sparse_mlp_max_density for this run (pruned config: the sparse deep tower when "
                          "the hidden layers' nonzero fraction is at most this); default: the model's")
+    ap.add_argument("--pair-max", type=int, default=None,
+                    help="DeepFMs.fwfm_pair_max for this run (fwfm_pruned: 0 runs the dense Gram FwFM)")
     ap.add_argument("--streams", type=int, default=None,
                     help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
                          "batch's workgroup shares each CU, hiding the gather / FwFM phases)")
@@ -101,7 +103,7 @@ class _HostGate:
 def kernel_name(config="deepfwfm"):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT select the A/B variants."""
-    if config == "fwfm":
+    if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
             return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
         ng = 4 if os.environ.get("DFWFM_P3_NG") == "4" else 8
@@ -156,7 +158,7 @@ def main():
     sizes = synth.CRITEO_FEATURE_SIZES
     fwlw = a.first_order == "fwlw"
     qr = a.config == "qr"
-    deep = int(a.config != "fwfm")
+    deep = int(a.config not in ("fwfm", "fwfm_pruned"))
     cfg = dict(field_size=39, numerical=13, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0, use_deep=deep,
                use_lw=1, use_fwlw=int(fwlw), h_depth=3, deep_nodes=400, embedding_bag=int(qr), qr_flag=int(qr),
                qr_operation="mult", qr_collisions=4, qr_threshold=200)
@@ -168,8 +170,13 @@ def main():
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     model = model.to(dev).eval()
     model.strict_index_check = False
-    if a.config == "pruned":
-        # reference :647-673 with sparse=0.90, emb_r=0.444, prune_r=1 (main_all.py flags of config 4)
+    if a.config == "fwfm_pruned":
+        model.fwfm_pair_max = 192  # the pair path (measured level with the dense Gram: DESIGN.md section 3.3)
+    if a.pair_max is not None:
+        model.fwfm_pair_max = a.pair_max
+    if a.config in ("pruned", "fwfm_pruned"):
+        # reference :647-673 with sparse=0.90, emb_r=0.444, prune_r=1 (main_all.py flags of config 4); FwFM-only:
+        # R keeps 73 of 741 pairs and the forward sums those (dfwfm_model_build_fwfm_pairs)
         from xsdeepfwfm_deprecated_amd.training import prune_step
         prune_step(model, 0.90, 1, 1, 1, 0.444, 1.0)
         torch.cuda.synchronize(dev)
@@ -186,7 +193,7 @@ def main():
         batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
     # batches in flight: 2 fill the CUs' register files for the deep configs (two eight-wave workgroups per
     # CU); the FwFM-only forward is latency-bound and gains from a third (three eight-wave workgroups per CU)
-    S = max(1, a.streams if a.streams is not None else (3 if a.config == "fwfm" else 2))
+    S = max(1, a.streams if a.streams is not None else (3 if not deep else 2))
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
 
     with torch.no_grad():
@@ -331,7 +338,9 @@ def main():
         "config": {"workload": (f"DeepFwFM forward, Criteo-39, emb 10, MLP 3x400, FwFM + {a.first_order}"
                                 if deep else f"FwFM-only forward (use_deep=0), Criteo-39, emb 10, FwFM + {a.first_order}")
                                + {"deepfwfm": "", "fwfm": "", "qr": ", QR embeddings (c=4, mult, threshold 200)",
-                                  "pruned": ", pruned (sparse 0.90, emb_r 0.444, prune_r 1)"}[a.config]
+                                  "pruned": ", pruned (sparse 0.90, emb_r 0.444, prune_r 1)",
+                                  "fwfm_pruned": ", pruned (sparse 0.90, emb_r 0.444, prune_r 1; FwFM over R's "
+                                                 "nonzero pairs)"}[a.config]
                                + f"; batch {BATCH} per GPU",
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
@@ -355,7 +364,7 @@ def main():
         result["roofline"] = {**hbm, **common}
         if traffic:      # the fabric rate of the PMC-counted bytes (40-B rows fetched as 128-B lines)
             result["roofline"]["traffic_gbs"] = round(traffic * S / (launch_ms / 1e3) / 1e9, 1)
-        if a.config == "fwfm" and a.inputs == "uniform":
+        if a.config in ("fwfm", "fwfm_pruned") and a.inputs == "uniform":
             # the same 26 rows x 4096 samples from the same tables and nothing else (tools/ubench_gather.hip,
             # one lane per row, three batches in flight): what the gather alone costs at this concurrency
             floor_us = 1.596

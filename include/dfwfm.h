@@ -136,6 +136,15 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
  * order (1e-5 bar). */
 int dfwfm_model_build_sparse_mlp(dfwfm_model* m, double max_density, int32_t* enabled, void* stream);
 
+/* Pruned FwFM (R masked by |(R + R^T)/2|, reference model/DeepFMs.py:661-666; SURVEY a12: 73 of 741 pairs at
+ * Criteo-39): lists the nonzero strictly-upper entries of (R + R^T)/2 from the last dfwfm_model_set_dense and,
+ * when there are at most max_pairs, makes the forward without a deep tower (fwd_kernel PART 3) sum
+ * second[b] = sum over the list of w_kl <E_bk, E_bl> instead of the dense per-sample Gram on MFMA.
+ * *enabled = 1 when the pair path is on.  Synchronises `stream` (reads the packed R); call it after a weight
+ * update, not per forward; dfwfm_model_set_dense turns the path off until the next call; max_pairs <= 0 turns
+ * it off.  Logits agree with the dense forward to fp32 summation order (1e-5 bar). */
+int dfwfm_model_build_fwfm_pairs(dfwfm_model* m, int32_t max_pairs, int32_t* enabled, void* stream);
+
 /* ---- training step (reference model/DeepFMs.py:553-637) ---------------------------------- */
 
 /* Forward of a training step: as dfwfm_forward, and additionally keeps (in model-owned device

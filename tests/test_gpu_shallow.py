@@ -148,3 +148,64 @@ def test_default_mlp_free_kernel_index_out_of_range_raises(gpu, monkeypatch, bad
     m = _model(cfg, params, gpu, monkeypatch, False)
     with pytest.raises(IndexError):
         _run(m, xi, xv, gpu)
+
+
+def _prune_r(params, keep=0.1, seed=0):
+    """The reference's R mask (model/DeepFMs.py:661-666): entries whose |(R + R^T)/2| is below the threshold are
+    zeroed, so the mask is symmetric; `keep` of the off-diagonal pairs survive."""
+    p = dict(params)
+    W = p["field_cov.weight"].copy()
+    sym = np.abs(0.5 * (W + W.T))
+    F = W.shape[0]
+    iu = np.triu_indices(F, 1)
+    thr = np.quantile(sym[iu], 1.0 - keep)
+    W[sym < thr] = 0.0
+    p["field_cov.weight"] = W
+    return p, int((sym[iu] >= thr).sum())
+
+
+@pytest.mark.parametrize("case", [dict(F=39, num=13, D=10), dict(F=39, num=13, D=10, fwlw=1, lw=0),
+                                  dict(F=64, num=0, D=16), dict(F=5, num=2, D=4), dict(F=39, num=13, D=32)],
+                         ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+@pytest.mark.parametrize("B", [17, 4096 + 3])
+def test_pruned_fwfm_pair_path_matches_oracle_and_gram(gpu, monkeypatch, case, B):
+    """A pruned R (8 % of the pairs) takes the pair path (dfwfm_model_build_fwfm_pairs) in the MLP-free forward;
+    its logits equal the oracle's and the dense Gram path's (fwfm_pair_max = 0) within the 1e-5 bar."""
+    cfg, params, xi, xv = _case(**case, B=B, seed=B + 3)
+    params, npairs = _prune_r(params, 0.08)
+    m = _model(cfg, params, gpu, monkeypatch, False)
+    m.fwfm_pair_max = 192  # opt-in (default 0: measured no faster, DESIGN.md section 3.3)
+    got = _run(m, xi, xv, gpu)
+    assert m._engine._pairs_on and npairs <= m.fwfm_pair_max
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    m.fwfm_pair_max = 0
+    dense = _run(m, xi, xv, gpu)
+    assert not m._engine._pairs_on
+    assert logit_close_scaled(dense, ref, cfg, params, xi, xv) < 1e-5
+    one = _run(m, xi[B - 1:], xv[B - 1:], gpu)  # a row's logit does not depend on its tile or slot
+    assert one[0] == dense[B - 1]
+
+
+def test_pair_list_follows_weight_updates(gpu, monkeypatch):
+    """set_dense (a weight change) turns the pair path off until the list is rebuilt from the new R; a dense R
+    (more than fwfm_pair_max pairs) keeps the Gram path."""
+    cfg, params, xi, xv = _case(39, 13, 10, B=300, seed=21)
+    pruned, _ = _prune_r(params, 0.1)
+    m = _model(cfg, pruned, gpu, monkeypatch, False)
+    m.fwfm_pair_max = 192
+    _run(m, xi, xv, gpu)
+    assert m._engine._pairs_on
+    pruned2, _ = _prune_r(params, 0.05)
+    with torch.no_grad():
+        m.field_cov.weight.copy_(torch.from_numpy(pruned2["field_cov.weight"]))
+    got = _run(m, xi, xv, gpu)
+    assert m._engine._pairs_on
+    ref = dfwfm_oracle.forward(cfg, pruned2, xi, xv)
+    assert logit_close_scaled(got, ref, cfg, pruned2, xi, xv) < 1e-5
+    with torch.no_grad():
+        m.field_cov.weight.copy_(torch.from_numpy(params["field_cov.weight"]))  # dense R: 741 pairs
+    got = _run(m, xi, xv, gpu)
+    assert not m._engine._pairs_on
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5

@@ -98,6 +98,10 @@ class DeepFMs(nn.Module):
         # of their weights is nonzero; 0 (default) keeps the dense MFMA kernel, which is faster at the
         # reference's 90 % masks (34.7 vs 100 us per batch)
         self.sparse_mlp_max_density = 0.0
+        # the forward without a deep tower sums the FwFM over R's nonzero pairs when a pruned R
+        # (reference :661-666) leaves at most this many (of F (F - 1) / 2); 0 (default) keeps the dense Gram
+        # on MFMA, which is as fast at the reference's 73 of 741 pairs
+        self.fwfm_pair_max = 0
         self._defer_index_check = 0     # >0 inside a batched caller: one flag read at its end, not per batch
         self._engine = None
 
@@ -297,6 +301,8 @@ class DeepFMs(nn.Module):
             # magnitude-pruned hidden layers (fit(prune=1), reference :647-673) run as a sparse MLP when
             # at most sparse_mlp_max_density of their weights are nonzero (checked once per weight update)
             eng.sync_sparse(self.sparse_mlp_max_density)
+        elif self.use_fwfm:
+            eng.sync_pairs(self.fwfm_pair_max)
         params = [q for q in self.parameters() if q.requires_grad]
         out, _ = torch.ops.dfwfm.forward(torch_ops.register(self), xi, xv, params, False, 0.0, 0)
         if self.strict_index_check and not self._defer_index_check:

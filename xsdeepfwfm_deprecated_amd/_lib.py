@@ -109,6 +109,7 @@ SIGNATURES = {
     "dfwfm_forward_ws": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P,
                                         ctypes.c_size_t, _P]),
     "dfwfm_model_build_sparse_mlp": (ctypes.c_int, [_P, ctypes.c_double, ctypes.POINTER(ctypes.c_int32), _P]),
+    "dfwfm_model_build_fwfm_pairs": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), _P]),
     "dfwfm_train_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P,
                                            ctypes.c_float, ctypes.c_uint32, _P]),
     "dfwfm_backward": (ctypes.c_int, [_P, _P, ctypes.POINTER(dfwfm_grads), _P]),

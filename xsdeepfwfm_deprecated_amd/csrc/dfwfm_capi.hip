@@ -42,6 +42,8 @@ struct dfwfm_model {
   // device state (owned)
   FieldDev* d_fields;
   float* d_upack;  // FwFM A-operand fragments [MT][S][64]
+  int2* d_pairs;   // build_fwfm_pairs: nonzero pairs of a pruned R (F (F - 1) / 2 capacity)
+  int32_t npairs;
   int32_t* d_err;
   float4* d_wpack;
   size_t wpack_elems;
@@ -122,7 +124,7 @@ void free_model(dfwfm_model* m) {
   if (!m) return;
   void* ptrs[] = {m->d_fields, m->d_upack, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
                   m->d_lw,     m->d_bias,  m->d_stamps,  m->d_wtpack, m->d_rsk,   m->d_ws,
-                  m->d_ell,    m->d_cnt,   m->d_spstat};
+                  m->d_ell,    m->d_cnt,   m->d_spstat, m->d_pairs};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -407,6 +409,7 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
   if (e != hipSuccess) return hip_fail(e, "pack launch");
   m->dense_set = true;
   m->sp = 0;  // new weights: the sparse tower's ELL is stale until rebuilt
+  m->flags &= ~kPairs;  // and so is the FwFM pair list
   for (int h = 0; h < m->H; ++h) m->lin_w[h] = lin_w ? lin_w[h] : nullptr;
   return DFWFM_OK;
 }
@@ -442,6 +445,8 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.out = out;
   a.err = m->d_err;
   a.upack = m->d_upack;
+  a.pairs = m->d_pairs;
+  a.npairs = m->npairs;
   a.fwlw = m->d_fwlw;
   a.lw = m->d_lw;
   a.bias = m->d_bias;
@@ -616,6 +621,46 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
   hipError_t e = launch_forward_split(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->NG, m->lds_gather, m->lds_inf,
                                       (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
+  return DFWFM_OK;
+}
+
+int dfwfm_model_build_fwfm_pairs(dfwfm_model* m, int32_t max_pairs, int32_t* enabled, void* stream) {
+  if (!m || !enabled) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  *enabled = 0;
+  m->flags &= ~kPairs;
+  if (!m->dense_set) return fail(DFWFM_ERR_STATE, "set_dense must precede build_fwfm_pairs");
+  if (!(m->flags & kHasSecond) || max_pairs <= 0) return DFWFM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  // the packed strictly-upper (R + R^T)/2 (FM: ones), as the forward reads it
+  std::vector<float> pk((size_t)m->MT * m->S * 64);
+  hipError_t e = hipMemcpyAsync(pk.data(), m->d_upack, pk.size() * sizeof(float), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "read FwFM pack");
+  std::vector<int2> list;
+  for (int k = 0; k < m->F; ++k)
+    for (int l = k + 1; l < m->F; ++l) {
+      const float w = pk[((size_t)(k >> 4) * m->S + (l >> 2)) * 64 + (k & 15) + 16 * (l & 3)];
+      if (w != 0.f) {
+        if ((int)list.size() >= max_pairs) return DFWFM_OK;  // denser than the pair path pays for
+        int2 q;
+        q.x = k | (l << 16);
+        memcpy(&q.y, &w, sizeof w);
+        list.push_back(q);
+      }
+    }
+  if (!m->d_pairs) {
+    const size_t cap = (size_t)m->F * (m->F - 1) / 2 + 1;
+    e = hipMalloc(&m->d_pairs, cap * sizeof(int2));
+    if (e != hipSuccess) return hip_fail(e, "pair list alloc");
+  }
+  if (!list.empty()) {
+    e = hipMemcpyAsync(m->d_pairs, list.data(), list.size() * sizeof(int2), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "pair list upload");
+  }
+  m->npairs = (int32_t)list.size();
+  m->flags |= kPairs;
+  *enabled = 1;
   return DFWFM_OK;
 }
 

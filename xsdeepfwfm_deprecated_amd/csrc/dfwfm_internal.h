@@ -28,6 +28,7 @@ constexpr int kTrain = 64;     // save the activations the backward needs (FwdAr
 constexpr int kDrop = 128;     // dropout on the deep tower (train only)
 constexpr int kPrio = 256;     // raise the wave priority for the phases before the MLP (A/B: DFWFM_PRIO)
 constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables; shallow_kernel's QR loads)
+constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kMaxH = 16;      // hidden layers
 
 // Device copy of dfwfm_field_tables (same field order and sizes); for QR fields
@@ -55,6 +56,8 @@ struct FwdArgs {
   float* out;
   int32_t* err;
   const float* upack;  // FwFM A-operand fragments [MT][S][64]: strictly-upper (R + R^T)/2
+  const int2* pairs;   // kPairs: the nonzero strictly-upper entries of (R + R^T)/2, (k | l << 16, w bits), k-major
+  int32_t npairs;
   const float* fwlw;   // [F*D]
   const float* lw;     // [F]
   const float* bias;   // [1]

@@ -326,7 +326,8 @@ fwd_kernel(FwdArgs p) {
       ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
       DFWFM_PRELOAD(ls);
     }
-    if constexpr (!QR) load_uu();  // PART 3: behind the row loads (vmcnt retires in order); QR: no room
+    if constexpr (!QR)  // PART 3: behind the row loads (vmcnt retires in order); QR: no room
+      if (!(flags & kPairs)) load_uu();
     // ... the shallow parameters go to LDS while the row loads are in flight ...
 #pragma unroll
     for (int k = 0; k < kUpkPT; ++k) {
@@ -390,7 +391,26 @@ fwd_kernel(FwdArgs p) {
   }
   stamp(p.stamps, 9, tid);
   if constexpr (PART == 3) {
-    if (flags & kHasSecond) {
+    if ((flags & kHasSecond) && (flags & kPairs)) {
+      // pruned R (dfwfm_model_build_fwfm_pairs): second[b] = sum over the nonzero pairs of w_kl <E_bk, E_bl>,
+      // LPS lanes per sample taking every LPS-th pair (k-major list), then an LPS-lane butterfly
+      constexpr int LPS = NTH / kBM;
+      const int b = tid / LPS, j = tid % LPS;
+      const float* eb = bufX + b * SX;
+      float part = 0.f;
+      for (int q = j; q < p.npairs; q += LPS) {
+        const int2 pr = p.pairs[q];
+        const float* ek = eb + (pr.x & 0xffff) * D;
+        const float* el = eb + (pr.x >> 16) * D;
+        float dot = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) dot = fmaf(ek[d], el[d], dot);
+        part = fmaf(__int_as_float(pr.y), dot, part);
+      }
+#pragma unroll
+      for (int o = LPS / 2; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+      if (j == 0) part2[b] = part;
+    } else if (flags & kHasSecond) {
       // MLP-free forward: second[b] = sum_{k<l} U'[k,l] <E_bk, E_bl> from the per-sample Gram G_b = E_b E_b^T
       // on MFMA (rows k, columns l, contraction over d: ceil(D/4) steps).  A sample's MT*ceil(D/4) operand
       // fragments serve as both A and B of its upper tiles (m <= n), so every chain is ceil(D/4) MFMAs deep

@@ -101,6 +101,21 @@ class ForwardEngine:
             "dfwfm_model_set_dense")
         self._dense_key = key
 
+    def sync_pairs(self, max_pairs: int) -> bool:
+        """(Re)build the pruned FwFM's nonzero pair list after a weight update (syncs the stream once per
+        update): the forward without a deep tower then sums the listed pairs when there are at most
+        max_pairs.  Returns whether the pair path is on."""
+        key = (self._dense_key, int(max_pairs))
+        if key == getattr(self, "_pairs_key", None):
+            return self._pairs_on
+        en = ctypes.c_int32(0)
+        _lib.check(_lib.lib().dfwfm_model_build_fwfm_pairs(self.handle, int(max_pairs), ctypes.byref(en),
+                                                           _stream_handle(self.device)),
+                   "dfwfm_model_build_fwfm_pairs")
+        self._pairs_on = bool(en.value)
+        self._pairs_key = key
+        return self._pairs_on
+
     def sync_sparse(self, max_density: float) -> bool:
         """(Re)build the pruned deep tower's nonzero lists after a weight update (inference only; syncs
         the stream once per update): dfwfm_forward_ws then runs the sparse MLP when the hidden layers'
