@@ -48,6 +48,9 @@ namespace dfwfm {
 #ifndef DFWFM_P3_WPE
 #define DFWFM_P3_WPE 6  // MLP-free forward on eight waves: six waves per SIMD (<= 80 registers): three workgroups per CU
 #endif
+#ifndef DFWFM_P3_DIRECT_DESC
+#define DFWFM_P3_DIRECT_DESC 1  // MLP-free forward without QR: row descriptors from global, no staging barrier
+#endif
 #ifndef DFWFM_P3_WPE4
 #define DFWFM_P3_WPE4 5  // MLP-free forward on four waves: five waves per SIMD (<= 96 registers): five workgroups
                          // per CU (LDS 30.7 KB each at Criteo-39)
@@ -178,11 +181,31 @@ fwd_kernel(FwdArgs p) {
   // ext-vector element types throughout: HIP's uint2 / float4 are unions, which keeps these arrays out
   // of registers (scratch, and a vmcnt(0) at every spill point)
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  u32x2 dw[kDescPT];
+  // PART 3 without QR fields: each thread loads its rows' descriptor fields (table bases, row count) from
+  // global memory with its keys -- no LDS staging and no barrier before the gather
+  constexpr bool kDirectDesc = DFWFM_P3_DIRECT_DESC && PART == 3 && !QR;
+  u32x2 dw[kDirectDesc ? 1 : kDescPT];
+  const float* rd_emb2[kDirectDesc ? RPT : 1];
+  const float* rd_emb1[kDirectDesc ? RPT : 1];
+  int64_t rd_n[kDirectDesc ? RPT : 1];
+  if constexpr (kDirectDesc) {
 #pragma unroll
-  for (int k = 0; k < kDescPT; ++k) {
-    const int i = tid + k * NTH;
-    if (i < 7 * F) dw[k] = reinterpret_cast<const u32x2*>(p.fields)[i];
+    for (int k = 0; k < RPT; ++k) {
+      const int f = (tid + k * NTH) >> 4;
+      rd_emb2[k] = rd_emb1[k] = nullptr;
+      rd_n[k] = 0;
+      if (f < F) {
+        rd_emb2[k] = p.fields[f].emb2;
+        rd_emb1[k] = p.fields[f].emb1;
+        rd_n[k] = p.fields[f].n;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kDescPT; ++k) {
+      const int i = tid + k * NTH;
+      if (i < 7 * F) dw[k] = reinterpret_cast<const u32x2*>(p.fields)[i];
+    }
   }
   int64_t key[RPT];  // gather row r -> field f = r / 16, sample b = r % 16: index or Xv bits
 #pragma unroll
@@ -213,12 +236,14 @@ fwd_kernel(FwdArgs p) {
     if (i < n_fwlw) fw[k] = p.fwlw[i];
   }
   const float lwv = ((flags & kFoLw) && tid < F) ? p.lw[tid] : 0.f;
+  if constexpr (!kDirectDesc) {
 #pragma unroll
-  for (int k = 0; k < kDescPT; ++k) {
-    const int i = tid + k * NTH;
-    if (i < 7 * F) reinterpret_cast<u32x2*>(desc)[i] = dw[k];
+    for (int k = 0; k < kDescPT; ++k) {
+      const int i = tid + k * NTH;
+      if (i < 7 * F) reinterpret_cast<u32x2*>(desc)[i] = dw[k];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   stamp(p.stamps, 1, tid);
 
   // PART 3: this lane's U' entries of every upper Gram tile (the same for every sample), loaded from the packed
@@ -267,7 +292,21 @@ fwd_kernel(FwdArgs p) {
       if constexpr (QR) pb[k] = qb[k] = nullptr;
       scale[k] = 1.f;
       mode[k] = 0;
-      if (live[k]) {
+      if (kDirectDesc && live[k]) {
+        if (f < num) {
+          scale[k] = __int_as_float((int)key[k]);
+          pa[k] = rd_emb2[kDirectDesc ? k : 0];
+          qa[k] = rd_emb1[kDirectDesc ? k : 0];
+        } else {
+          int64_t idx = key[k];
+          if (idx < 0 || idx >= rd_n[kDirectDesc ? k : 0]) {
+            atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
+            idx = 0;
+          }
+          pa[k] = rd_emb2[kDirectDesc ? k : 0] + idx * D;
+          if (fo_tab) qa[k] = rd_emb1[kDirectDesc ? k : 0] + idx;
+        }
+      } else if (live[k]) {
         const FieldDev fd = desc[f];
         if (f < num) {
           scale[k] = __int_as_float((int)key[k]);
