@@ -51,6 +51,9 @@ namespace dfwfm {
 #ifndef DFWFM_P3_DIRECT_DESC
 #define DFWFM_P3_DIRECT_DESC 1  // MLP-free forward without QR: row descriptors from global, no staging barrier
 #endif
+#ifndef DFWFM_DIRECT_DESC_DEEP
+#define DFWFM_DIRECT_DESC_DEEP 1  // the fused forward (static 3x400 form) without QR: the same direct descriptors
+#endif
 #ifndef DFWFM_P3_WPE4
 #define DFWFM_P3_WPE4 5  // MLP-free forward on four waves: five waves per SIMD (<= 96 registers): five workgroups
                          // per CU (LDS 30.7 KB each at Criteo-39)
@@ -64,7 +67,8 @@ namespace dfwfm {
 // on the same CU runs its gather; the training variant, one batch in flight, keeps 256 registers)
 // NS: every layer has NS K chunks and NS output tiles (0: any) -- the K loop is then fully static and the
 // split tail tile rides on its register sets (mlp_k_loop_s)
-// QR: some field may be a QR embedding (false: the gather carries no second operand -- PART 3 only)
+// QR: some field may be a QR embedding (false: the gather carries no second operand and loads its row descriptors
+// directly -- PART 3, and PART 0's static form)
 template <int D, int TPW, int KS, bool TRAIN, int PART, int NG, int NS, bool QR = true>
 __global__ void __launch_bounds__(64 * NG * KS)
 __attribute__((amdgpu_waves_per_eu(PART == 1 ? 3 : (PART == 3 ? (NG == 4 ? DFWFM_P3_WPE4 : DFWFM_P3_WPE)
@@ -183,7 +187,7 @@ fwd_kernel(FwdArgs p) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   // PART 3 without QR fields: each thread loads its rows' descriptor fields (table bases, row count) from
   // global memory with its keys -- no LDS staging and no barrier before the gather
-  constexpr bool kDirectDesc = DFWFM_P3_DIRECT_DESC && PART == 3 && !QR;
+  constexpr bool kDirectDesc = !QR && ((DFWFM_P3_DIRECT_DESC && PART == 3) || (DFWFM_DIRECT_DESC_DEEP && PART == 0));
   u32x2 dw[kDirectDesc ? 1 : kDescPT];
   const float* rd_emb2[kDirectDesc ? RPT : 1];
   const float* rd_emb1[kDirectDesc ? RPT : 1];
@@ -884,7 +888,10 @@ template <int D, int TPW, int KS, bool TRAIN, int PART = 0, int NG = 4>
 static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, hipStream_t s) {
   // the static 25-chunk form (3x400 MLP over 39x10 embeddings: 25 tiles = 8 waves x 3 + the split 25th)
   constexpr bool S25 = NG == 8 && TPW == 3 && KS == 1 && PART != 1;
-  auto k = (S25 && a.ns == 25) ? fwd_kernel<D, TPW, KS, TRAIN, PART, NG, S25 ? 25 : 0>
+  // the static form without QR fields also loads its row descriptors directly (no staging barrier)
+  constexpr bool S25D = S25 && PART == 0 && DFWFM_DIRECT_DESC_DEEP;
+  auto k = (S25 && a.ns == 25) ? ((S25D && !(a.flags & kHasQR)) ? fwd_kernel<D, TPW, KS, TRAIN, PART, NG, S25 ? 25 : 0, false>
+                                                               : fwd_kernel<D, TPW, KS, TRAIN, PART, NG, S25 ? 25 : 0>)
                                : fwd_kernel<D, TPW, KS, TRAIN, PART, NG, 0>;
   {
     hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
