@@ -113,7 +113,8 @@ def kernel_name(config="deepfwfm"):
     if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):
         return f"dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::fwd_kernel<10,{tpw},1,false,2,{ng}>"
     ns = 25 if ng == 8 and tpw == 3 and not os.environ.get("DFWFM_NO_STATIC_K") else 0  # static 25-chunk K loop
-    return f"dfwfm::fwd_kernel<10,{tpw},1,false,0,{ng},{ns},true>"  # as rocprofv3 names it (QR argument last)
+    qr = "true" if (config == "qr" or ns != 25) else "false"  # the static form without QR fields: QR=false
+    return f"dfwfm::fwd_kernel<10,{tpw},1,false,0,{ng},{ns},{qr}>"  # as rocprofv3 names it (QR argument last)
 
 
 def algorithmic_counts(cfg, sizes=None):
