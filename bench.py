@@ -1,6 +1,6 @@
 """Benchmark of the hot path: DeepFwFM Criteo-39 forward, batch 4096 per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: starts N ranks itself, one per GPU)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -72,12 +72,35 @@ def parse():
     return ap.parse_args()
 
 
+def _hip_runtime():
+    """The HIP runtime torch already loaded (by its soname; any ROCm major), or None."""
+    import ctypes
+    import ctypes.util
+    names = ["libamdhip64.so.7", "libamdhip64.so.6", "libamdhip64.so", ctypes.util.find_library("amdhip64")]
+    for nm in names:
+        if not nm:
+            continue
+        try:
+            h = ctypes.CDLL(nm)
+        except OSError:
+            continue
+        if all(hasattr(h, f) for f in ("hipHostMalloc", "hipHostFree", "hipStreamWaitValue32")):
+            return h
+    return None
+
+
 class _HostGate:
-    """hipStreamWaitValue32 on a coherent pinned host word: the streams wait until release() writes 1."""
+    """hipStreamWaitValue32 on a coherent pinned host word: the streams wait until release() writes 1.
+
+    The host releases the gate after at most GATE_STEPS steps are queued behind it (then keeps enqueueing while
+    the GPU runs): a gate held until an unbounded number of commands is queued could fill the hardware queue,
+    and the host would then block inside a launch without ever reaching release()."""
 
     def __init__(self, streams):
         import ctypes
-        self._hip = ctypes.CDLL("libamdhip64.so.7")
+        self._hip = _hip_runtime()
+        if self._hip is None:
+            raise OSError("HIP runtime without hipStreamWaitValue32")
         self._p = ctypes.c_void_p()
         rc = self._hip.hipHostMalloc(ctypes.byref(self._p), ctypes.c_size_t(64), ctypes.c_uint(0x40000000))
         if rc != 0:
@@ -92,6 +115,9 @@ class _HostGate:
 
     def release(self):
         self._word[0] = 1
+        self.released = True
+
+    released = False
 
     def __del__(self):
         try:
@@ -135,13 +161,22 @@ def algorithmic_counts(cfg, sizes=None):
     return flops, bytes_
 
 
+GATE_STEPS = 640  # steps queued behind the host gate before it is released (see _HostGate)
+
+
 def main():
     a = parse()
+    # --gpus N without torchrun: start N ranks (one process per GPU) before anything touches the GPU, and exit
+    # with their status; rank 0 prints the JSON line
+    from xsdeepfwfm_deprecated_amd.launch import spawn_ranks
+    rc = spawn_ranks(a.gpus)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world} (torchrun); using WORLD_SIZE", file=sys.stderr)
     # one process per GPU; the modulo only matters for rehearsing N > 1 on fewer GPUs (with
     # DFWFM_BENCH_BACKEND=gloo: RCCL refuses two ranks on one device)
     local = local % max(1, torch.cuda.device_count())
@@ -236,16 +271,21 @@ def main():
                         gk[n % G] = capture(n % G, k)
                 graphs.append(gk)
 
-        def run_n(n_total):
+        def run_n(n_total, progress=None):
             # enqueue round-robin over the streams (stream k's replays must not wait behind the host
-            # enqueueing all of stream 0's first: the streams would start one after the other)
+            # enqueueing all of stream 0's first: the streams would start one after the other);
+            # progress(steps enqueued so far) after every round
             ns = per_stream(n_total)
+            done = 0
             if graphs is None:
                 for i in range(max(ns)):
                     for k in range(S):
                         if i < ns[k]:
                             with torch.cuda.stream(streams[k]):
                                 step(i, k)
+                            done += 1
+                    if progress:
+                        progress(done)
                 return
             for r in range(max(ns) // G + 1):
                 for k in range(S):
@@ -254,6 +294,9 @@ def main():
                         continue
                     with torch.cuda.stream(streams[k]):
                         graphs[k][G if left >= G else left].replay()
+                    done += min(G, left)
+                if progress:
+                    progress(done)
 
         # settle: untimed back-to-back forwards until the chip has run them for --settle-ms (its clock ramps
         # over the first few hundred forwards); then the W warmup steps, then the K timed steps
@@ -280,15 +323,24 @@ def main():
         # not the host submitting graphs.  The region runs from the earliest stream's start event to the
         # latest stream's end event (each recorded on its own stream): cross-stream event waits inside the
         # region cost ~20 us each on this stack (a late second stream, a late final event)
-        gate = _HostGate(streams) if not a.no_gate else None
+        gate = None
+        if not a.no_gate:
+            try:
+                gate = _HostGate(streams)
+            except (OSError, RuntimeError) as e:  # no gate on this runtime: time as --no-gate does
+                print(f"bench: host gate unavailable ({e}); timing without it", file=sys.stderr)
         for k, st in enumerate(streams):
             if k and gate is None:
                 st.wait_stream(streams[0])
             s0[k].record(st)
-        run_n(a.steps)
+
+        def progress(done):
+            if gate is not None and not gate.released and done >= GATE_STEPS:
+                gate.release()
+        run_n(a.steps, progress)
         for k, st in enumerate(streams):
             s1[k].record(st)
-        if gate is not None:
+        if gate is not None and not gate.released:
             gate.release()
         for st in streams:
             st.synchronize()

@@ -260,8 +260,9 @@ typedef struct {
   int64_t r;
 } dfwfm_sparse_dest;
 
-/* Entries a batch of `batch` rows can produce (capacity = tables x batch), their row width and the device
- * workspace dfwfm_sparse_grads needs. */
+/* Entries a batch of `batch` rows can produce (capacity = sum over the family's tables of min(batch, the
+ * table's rows): one entry per distinct touched row), their row width and the device workspace
+ * dfwfm_sparse_grads needs. */
 int dfwfm_sparse_grads_size(dfwfm_model* m, int32_t family, int64_t batch, int64_t* capacity, int32_t* width,
                             int64_t* ws_bytes);
 /* The list of the last training step: out_dest[e] (device int64) = float offset of entry e's row in the flat

@@ -319,6 +319,37 @@ def test_full_size_criteo_batch_matches_oracle(gpu, inputs):
     assert np.array_equal(alone, full[rows])
 
 
+@pytest.mark.parametrize("op", ["mult", "add"])
+@pytest.mark.parametrize("inputs", ["uniform", "zipf"])
+def test_full_size_qr_batch_matches_oracle(gpu, inputs, op):
+    """BASELINE configs[2] at full size: Criteo-39 tables as QR embedding bags (c = 4, threshold 200:
+    18 of the 26 categorical fields, e.g. 245,197 rows -> 61,300 quotient rows), B = 4096; every logit against
+    the float64 oracle at the north-star bar (reference model/DeepFMs.py:1071-1073, model/QREmbeddingBag.py:
+    156-174), and rows run alone bit-identical."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = synth.CRITEO_FEATURE_SIZES
+    cfg = dict(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0,
+               use_deep=1, use_lw=1, use_fwlw=0, h_depth=3, deep_nodes=400, numerical=13, embedding_bag=1,
+               qr_flag=1, qr_operation=op, qr_collisions=4, qr_threshold=200)
+    m = DeepFMs(**model_kwargs(cfg))
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert sum(k.endswith("weight_q") for k in shapes) == 2 * 18  # first- and second-order QR bags
+    assert shapes["fm_2nd_embeddings.15.weight_q"] == (61300, 10)
+    params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=4321)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    m = m.to(gpu).eval()
+    gen = synth.zipf_inputs if inputs == "zipf" else synth.synth_inputs
+    xi, xv = gen(sizes, 13, 4096, seed=12)
+    xi[0] = np.asarray(sizes[13:]) - 1  # the last row of every table
+    xi[1] = 0
+    full = run(m, xi, xv, gpu)
+    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+    assert logit_close(full, ref) < 1e-5
+    rows = np.random.default_rng(1).choice(4096, 64, replace=False)
+    alone = run(m, xi[rows], xv[rows], gpu)
+    assert np.array_equal(alone, full[rows])
+
+
 def test_custom_op_opcheck_and_matches_engine(gpu):
     """torch.ops.dfwfm.forward passes torch.library.opcheck (schema, fake tensor, autograd
     registration) and returns the engine's logits bit for bit."""

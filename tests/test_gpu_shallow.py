@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import logit_close_scaled, model_kwargs
+from conftest import logit_close, logit_close_scaled, model_kwargs
 from oracle import dfwfm_oracle
 
 pytestmark = pytest.mark.gpu
@@ -28,6 +28,16 @@ def _case(F, num, D, *, fwlw=0, lw=1, qr=0, qr_op="mult", fm=0, logit=0, bag=0, 
     params = synth.synth_state(shapes, F, D, 400, second, False, seed=seed)
     xi, xv = synth.synth_inputs(sizes, num, B, seed=seed + 1)
     return cfg, params, xi, xv
+
+
+def _err(got, ref, cfg, params, xi, xv):
+    """The north-star bar |d| <= 1e-5 * max(1, |ref|) where the first-order terms are projected by lw (BASELINE
+    configs[0]'s model: terms ~1e1 at the init_weights scales, no cancellation to tiny logits); the bar scaled by
+    the row's absolute term sum (conftest.logit_close_scaled) where they are not: without lw the ~N(0, 1) table
+    weights times Xv up to 63 cancel from ~1e2 to logits ~1e-1, below one fp32 ulp of the partial sums."""
+    if cfg.get("use_lw") and not cfg.get("use_logit"):
+        return logit_close(got, ref)
+    return logit_close_scaled(got, ref, cfg, params, xi, xv)
 
 
 def _model(cfg, params, dev, monkeypatch, shallow):
@@ -71,7 +81,7 @@ def test_shallow_kernel_matches_oracle_and_fused(gpu, monkeypatch, case):
     cfg, params, xi, xv = _case(**case, seed=len(str(case)))
     got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
     # bit-identical to the generic fused kernel (DFWFM_NO_PART3: the piece-wise FwFM, same arithmetic) ...
     monkeypatch.setenv("DFWFM_NO_PART3", "1")
     fused = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
@@ -79,7 +89,7 @@ def test_shallow_kernel_matches_oracle_and_fused(gpu, monkeypatch, case):
     assert np.array_equal(got, fused)
     # ... and the default MLP-free kernel (per-sample Gram FwFM, another summation order) within the bar
     part3 = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
-    assert logit_close_scaled(part3, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(part3, ref, cfg, params, xi, xv) < 1e-5
 
 
 @pytest.mark.parametrize("B", [1, 15, 16, 17, 255, 4096 + 3])
@@ -87,7 +97,7 @@ def test_shallow_kernel_ragged_batches(gpu, monkeypatch, B):
     cfg, params, xi, xv = _case(39, 13, 10, B=B, seed=B)
     got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
     # a row's logit does not depend on its tile or slot
     one = _run(_model(cfg, params, gpu, monkeypatch, True), xi[B - 1:], xv[B - 1:], gpu)
     assert one[0] == got[B - 1]
@@ -98,7 +108,7 @@ def test_shallow_kernel_full_size_tables(gpu, monkeypatch):
     cfg, params, xi, xv = _case(39, 13, 10, B=4096, big=True, seed=7)
     got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
 
 
 @pytest.mark.parametrize("bad", [-1, "n"])
@@ -119,7 +129,7 @@ def test_default_mlp_free_kernel_ragged_and_full_size(gpu, monkeypatch, B):
     m = _model(cfg, params, gpu, monkeypatch, False)
     got = _run(m, xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
     one = _run(m, xi[B - 1:], xv[B - 1:], gpu)
     assert one[0] == got[B - 1]
 
@@ -137,7 +147,7 @@ def test_mlp_free_four_and_eight_waves_bit_identical(gpu, monkeypatch, case):
     monkeypatch.delenv("DFWFM_P3_NG")
     assert np.array_equal(got4, got8)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert logit_close_scaled(got4, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(got4, ref, cfg, params, xi, xv) < 1e-5
 
 
 @pytest.mark.parametrize("bad", [-1, "n"])
@@ -178,11 +188,11 @@ def test_pruned_fwfm_pair_path_matches_oracle_and_gram(gpu, monkeypatch, case, B
     got = _run(m, xi, xv, gpu)
     assert m._engine._pairs_on and npairs <= m.fwfm_pair_max
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
     m.fwfm_pair_max = 0
     dense = _run(m, xi, xv, gpu)
     assert not m._engine._pairs_on
-    assert logit_close_scaled(dense, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(dense, ref, cfg, params, xi, xv) < 1e-5
     one = _run(m, xi[B - 1:], xv[B - 1:], gpu)  # a row's logit does not depend on its tile or slot
     assert one[0] == dense[B - 1]
 
@@ -202,10 +212,10 @@ def test_pair_list_follows_weight_updates(gpu, monkeypatch):
     got = _run(m, xi, xv, gpu)
     assert m._engine._pairs_on
     ref = dfwfm_oracle.forward(cfg, pruned2, xi, xv)
-    assert logit_close_scaled(got, ref, cfg, pruned2, xi, xv) < 1e-5
+    assert _err(got, ref, cfg, pruned2, xi, xv) < 1e-5
     with torch.no_grad():
         m.field_cov.weight.copy_(torch.from_numpy(params["field_cov.weight"]))  # dense R: 741 pairs
     got = _run(m, xi, xv, gpu)
     assert not m._engine._pairs_on
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert logit_close_scaled(got, ref, cfg, params, xi, xv) < 1e-5
+    assert _err(got, ref, cfg, params, xi, xv) < 1e-5

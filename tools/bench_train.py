@@ -1,6 +1,6 @@
 """Training-step benchmark (BASELINE.json configs[4]: DeepFwFM training, DP over RCCL).
 
-    python tools/bench_train.py [--steps K] [--warmup W] [--batch 4096] [--first-order lw|fwlw]
+    python tools/bench_train.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--first-order lw|fwlw]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_train.py
 
 One step = the reference's fit() inner loop body (model/DeepFMs.py:619-637) on a resident synthetic
@@ -36,15 +36,25 @@ def main():
     ap.add_argument("--mode", choices=["fused", "autograd"], default="fused",
                     help="fused: FusedTrainStep (HIP-graph replay, what fit() runs); autograd: model() + "
                          "loss.backward() + HIP Adam")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; started here unless "
+                                                           "torchrun already set WORLD_SIZE)")
     a = ap.parse_args()
+    from xsdeepfwfm_deprecated_amd.launch import spawn_ranks
+    rc = spawn_ranks(a.gpus)  # before any HIP call
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("DFWFM_BENCH_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
     from xsdeepfwfm_deprecated_amd.training import Adam, FusedTrainStep, allreduce_grads
     sizes = synth.CRITEO_FEATURE_SIZES
@@ -109,6 +119,11 @@ def main():
            "first_order": a.first_order, "dropout": not a.no_dropout, "wall_s": round(wall, 3),
            "mode": a.mode, "inputs": "copied" if (a.copy_inputs or a.mode != "fused") else "resident (read in place)",
            "final_loss_sum": round(float(loss.item()), 4)}
+    if trainer is not None and getattr(trainer, "sparse", False):
+        # touched-row lists all-gathered per step (fixed capacity: sum over tables of min(batch, rows))
+        res["exchange"] = {"backend": torch.distributed.get_backend(), "packed_bytes_per_rank": trainer.sp_bytes,
+                           "dense_bucket_bytes": 4 * (trainer.n_bucket_a - trainer.n_tables),
+                           "mlp_bucket_bytes": 4 * (trainer.grad.numel() - trainer.n_bucket_a)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

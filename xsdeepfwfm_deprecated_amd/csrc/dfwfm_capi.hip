@@ -1069,6 +1069,25 @@ int sparse_tasks(const dfwfm_model* m, int family, const dfwfm_sparse_dest* dest
   return n;
 }
 
+// largest entry count of one family's touched-row list: a table contributes at most one entry per distinct row,
+// so min(batch, its rows) -- plain tables n_f rows, QR quotient tables n_f / c (n_f rounded up to a multiple of
+// c at set_tables), remainder tables c -- instead of batch per table (Criteo-39, B = 4096: 14 of 26 tables have
+// fewer rows than the batch)
+int64_t sparse_capacity(const dfwfm_model* m, int family, const dfwfm_sparse_dest* dest, int64_t batch) {
+  const bool has = family == DFWFM_FAMILY_SECOND ? (m->flags & kNeedE) != 0 : (m->flags & kFoTables) != 0;
+  if (!has) return 0;
+  int64_t cap = 0;
+  for (int f = m->num; f < m->F; ++f) {
+    const FieldDev& fd = m->h_fields[f];
+    for (int part = 0; part < (fd.c > 0 ? 2 : 1); ++part) {
+      if (dest && (part == 0 ? dest[f].q : dest[f].r) < 0) continue;
+      const int64_t rows = fd.c == 0 ? fd.n : (part == 0 ? fd.n / fd.c : (int64_t)fd.c);
+      cap += rows < batch ? rows : batch;
+    }
+  }
+  return cap;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1080,9 +1099,10 @@ int dfwfm_sparse_grads_size(dfwfm_model* m, int32_t family, int64_t batch, int64
   if (!m->tables_set) return fail(DFWFM_ERR_STATE, "set_tables must precede dfwfm_sparse_grads_size");
   const int nt = sparse_tasks(m, family, nullptr, nullptr);
   *width = family == DFWFM_FAMILY_SECOND ? m->D : 1;
-  *capacity = (int64_t)nt * batch;
-  if (*capacity > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "more than 2^31 (table, sample) pairs");
-  *ws_bytes = nt ? (int64_t)sparse_workspace_bytes(*capacity, *width, nt) : 0;
+  if ((int64_t)nt * batch > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "more than 2^31 (table, sample) pairs");
+  *capacity = sparse_capacity(m, family, nullptr, batch);
+  // the sort runs over every (table, sample) position; only the exchanged list is capped per table
+  *ws_bytes = nt ? (int64_t)sparse_workspace_bytes((int64_t)nt * batch, *width, nt) : 0;
   return DFWFM_OK;
 }
 
@@ -1110,7 +1130,9 @@ int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, cons
   a.dlogit = dlogit;
   a.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
   const int64_t n = (int64_t)a.ntasks * a.batch;
-  if (n > capacity) return fail(DFWFM_ERR_INVALID_ARG, "capacity %lld < %lld entries", (long long)capacity, (long long)n);
+  const int64_t bound = sparse_capacity(m, family, dest, a.batch);
+  if (bound > capacity)
+    return fail(DFWFM_ERR_INVALID_ARG, "capacity %lld < %lld entries", (long long)capacity, (long long)bound);
   if (n > 0 && (!dlogit || !out_dest || !out_rows || !ws)) return fail(DFWFM_ERR_INVALID_ARG, "null buffer");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {

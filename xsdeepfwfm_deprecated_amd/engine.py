@@ -95,11 +95,19 @@ class ForwardEngine:
         W = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_w])
         B = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_b])
         self.__dict__.pop("_ws_cache", None)  # set_dense turns the sparse tower off until sync_sparse
+        self.invalidate_derived()
         _lib.check(_lib.lib().dfwfm_model_set_dense(
             self.handle, _ptr(field_cov), _ptr(fwfm_lin), _ptr(fm_1st), _ptr(bias),
             W if H else None, B if H else None, _ptr(fc_w), _stream_handle(self.device)),
             "dfwfm_model_set_dense")
         self._dense_key = key
+
+    def invalidate_derived(self):
+        """Forget the pruned FwFM pair list and the sparse deep tower: dfwfm_model_set_dense turns both off in
+        the library (and a captured training step re-packs the weights they were built from), so the next
+        sync_pairs / sync_sparse must rebuild them rather than report the cached state."""
+        self._pairs_key = None
+        self._sparse_key = None
 
     def sync_pairs(self, max_pairs: int) -> bool:
         """(Re)build the pruned FwFM's nonzero pair list after a weight update (syncs the stream once per

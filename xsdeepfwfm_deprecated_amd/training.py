@@ -256,15 +256,18 @@ class FusedTrainStep:
                        "dfwfm_sparse_grads_size")
             if cap.value > 0:
                 fams.append(dict(fam=fam, dest=dest, cap=int(cap.value), w=int(w.value), ws_bytes=int(ws.value)))
+        # every section starts 16-byte aligned and the buffer is a multiple of 16 bytes, so each rank's slice of
+        # the all-gathered [world, nbytes] buffer keeps the int64 destination lists aligned
+        a16 = lambda x: (x + 15) & ~15  # noqa: E731
         nbytes = 0
         for f in fams:
             f["o_dest"] = nbytes
-            nbytes += 8 * f["cap"]
+            nbytes = a16(nbytes + 8 * f["cap"])
         for f in fams:
             f["o_rows"] = nbytes
-            nbytes += 4 * f["cap"] * f["w"]
+            nbytes = a16(nbytes + 4 * f["cap"] * f["w"])
         o_cnt = nbytes
-        nbytes += 8 * ((4 * len(fams) + 7) // 8)
+        nbytes = a16(nbytes + 4 * len(fams))
         world = self.dist.get_world_size()
         self.sp_send = torch.zeros(nbytes, dtype=torch.uint8, device=self.dev)
         self.sp_recv = torch.zeros(world, nbytes, dtype=torch.uint8, device=self.dev)
@@ -444,11 +447,12 @@ class FusedTrainStep:
         row-contiguous int64 indices, float32 values and float32 labels on this device."""
         xi2 = xi.reshape(n, -1) if xi.is_contiguous() else None
         if (xi2 is None or xi2.dtype != torch.int64 or xi2.device != self.dev or xi2.shape[1] != self.xi.shape[1]
-                or y.dtype != torch.float32 or y.device != self.dev or y.dim() != 1 or not y.is_contiguous()):
+                or y.dtype != torch.float32 or y.device != self.dev or y.dim() != 1 or not y.is_contiguous()
+                or y.shape[0] != n):
             return None
         if self.num:
             if (xv.dtype != torch.float32 or xv.device != self.dev or xv.dim() != 2 or xv.stride(1) != 1
-                    or xv.shape[1] < self.num):
+                    or xv.shape[1] < self.num or xv.shape[0] < n):
                 return None
         else:
             xv = self.xv
@@ -480,7 +484,10 @@ class FusedTrainStep:
             # the graphs bake in the engine's activation workspace: a train forward at a larger batch
             # elsewhere (e.g. autograd) re-allocates it, and then the graphs are re-captured; and they bake in
             # the input pointers: one graph set per resident input buffer set
-            key = (denom, self.drop, self._ws_generation(), tuple(t.data_ptr() for t in inputs))
+            # (slices of one large resident array get a new key per step: each is a capture, so fit() copies
+            # its batches -- resident_inputs is for a fixed ring of input buffers)
+            key = (denom, self.drop, self._ws_generation(),
+                   tuple((t.data_ptr(), tuple(t.stride())) for t in inputs))
             hit = self._graph_sets.pop(key, None)
             if hit is None:
                 if len(self._graph_sets) >= self.max_graph_sets:
@@ -503,6 +510,7 @@ class FusedTrainStep:
             self._part2()
         self.steps += 1
         self.eng._dense_key = None  # weights changed behind torch's version counters: re-pack on next use
+        self.eng.invalidate_derived()  # and the pair list / sparse tower built from the old weights are stale
         return self.loss_sum
 
     _graph_key = None
@@ -784,6 +792,7 @@ def _fit_loop(model, trainer, dist, rank, world, Xi_train, Xv_train, y_train, x_
                     # 100 batch means); the device sum restarts every window, so it never grows large in f32
                     total_loss = float(trainer.loss_sum.item()) * 100.0 / max(win_rows, 1)
                     trainer.loss_sum.zero_()
+                    model.check_index_errors()  # the stream is synchronised here anyway: surface a bad Xi early
                 win_rows = 0
                 # (the reference's evaluate() leaves the model in eval mode -- dropout off -- for the
                 # rest of training, :627-630, :880-893; kept as is)
