@@ -23,6 +23,7 @@
 #ifndef DFWFM_H
 #define DFWFM_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus

@@ -1,6 +1,7 @@
 """Entry point of the reference (main_all.py), on the MI355X engine: parse the same flags, read the
-dataset (native ingest), build DeepFMs, fit (HIP training step), reload the saved weights, report the
-model size and run the benchmark on the test split.
+dataset (native ingest), build DeepFMs, fit (HIP training step; with -use_cuda 0 the host kernels), reload the
+saved weights, report the model size and run the benchmark on the test split (on the device with
+-time_on_cuda 1, else the host kernels' thread sweep).
 
     python main_all.py -dataset tiny-criteo -n_epochs 2 [-data_root DIR]
 """
@@ -47,18 +48,19 @@ def main(argv=None):
               prune_r=pars.prune_r, prune_deep=pars.prune_deep, save_path=save_model_name, emb_r=pars.emb_r,
               emb_corr=pars.emb_corr, early_stopping=False)
 
-    # measurements (the reference reloads the saved weights; its CPU timing path needs -time_on_cuda 0,
-    # which this engine does not have: the benchmark runs on the device)
-    model = get_model(field_size=field_size, cuda=True, feature_sizes=train_dict["feature_sizes"], pars=pars,
+    # measurements: the reference rebuilds the model (on the device with -time_on_cuda 1, else on the CPU),
+    # reloads the saved weights, reports the size and benchmarks the test split (main_all.py:56-63); on the CPU
+    # the host kernels run the reference's 1- / 4-thread sweep (model/DeepFMs.py:982-1009)
+    on_dev = bool(pars.time_on_cuda) and torch.cuda.is_available()
+    model = get_model(field_size=field_size, cuda=on_dev, feature_sizes=train_dict["feature_sizes"], pars=pars,
                       logger=logger)
-    model = load_model_dic(model, save_model_name, sparse=pars.prune).cuda()
+    model = load_model_dic(model, save_model_name, sparse=pars.prune)
+    if on_dev:
+        model = model.cuda()
     model.print_size_of_model()
-    if not pars.time_on_cuda:
-        logger.info("-time_on_cuda 0: this engine has no CPU forward (no fallback by design); the benchmark "
-                    "times the HIP forward, and bench.py's cpu_baseline times the reference op sequence on the host")
     logger.info("TEST DATASET")
     return model.run_benchmark(test_dict["index"], test_dict["value"], test_dict["label"], batch_size=8192,
-                               cuda=True)
+                               cuda=on_dev)
 
 
 if __name__ == "__main__":

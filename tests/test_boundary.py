@@ -87,13 +87,41 @@ def test_state_dict_contract_matches_reference(name):
         assert np.array_equal(v.numpy(), params[k])
 
 
-def test_no_cpu_fallback():
-    from xsdeepfwfm_deprecated_amd import DeepFMs, DfwfmError
+def test_cpu_module_runs_the_host_library_never_torch_ops(monkeypatch):
+    """A module on the CPU runs libdfwfm_cpu.so (include/dfwfm_cpu.h) -- not the HIP library and not PyTorch's
+    generic ops: with the host library made unloadable the forward raises (no fallback either way)."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, DfwfmError, _lib
     cfg, params, xi, xv, *_ = load_golden("deepfwfm_lw")
     m = DeepFMs(**model_kwargs(cfg))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    monkeypatch.setattr(_lib, "_cpu", None)
+    monkeypatch.setattr(_lib, "CPU_PATH", "/nonexistent/libdfwfm_cpu.so")
     with pytest.raises(DfwfmError):
         with torch.no_grad():
             m(torch.from_numpy(xi), torch.from_numpy(xv))
+    with pytest.raises(DfwfmError):
+        m._sync_engine(torch.device("meta"))
+
+
+def cpu_header_functions():
+    src = open(os.path.join(REPO, "include", "dfwfm_cpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dfwfm_cpu_[a-z_]+)\s*\(", src)))
+
+
+def test_cpu_library_exports_every_header_symbol(built):
+    assert cpu_header_functions() == sorted(["dfwfm_cpu_abi_version", "dfwfm_cpu_backward", "dfwfm_cpu_forward",
+                                             "dfwfm_cpu_last_error", "dfwfm_cpu_saved_floats"])
+    L = ctypes.CDLL(built.CPU_PATH)
+    for name in cpu_header_functions():
+        assert hasattr(L, name), name
+    assert set(built.CPU_SIGNATURES) == set(cpu_header_functions())
+    C = built.cpu_lib()
+    assert C.dfwfm_cpu_abi_version() == 1
+    assert C.dfwfm_cpu_forward(None, None, 0, None, 0, 4, None, None, 0.0, 0, None, 1) == -1
+    assert b"null" in C.dfwfm_cpu_last_error()
+    assert C.dfwfm_cpu_backward(None, None, 0, None, 0, 4, None, None, 0.0, 0, None, 1) == -1
+    assert ctypes.sizeof(built.dfwfm_cpu_model) == 11 * 4 + 4 + 8 * 8
 
 
 def test_init_weights_distributions():

@@ -302,7 +302,8 @@ def test_main_all_tiny_criteo_end_to_end(gpu, tmp_path, extra, name):
     shutil.copy(src, data / "tiny_train_input.csv")
     shutil.copy(src, data / "tiny_test_input.csv")
     r = subprocess.run([sys.executable, os.path.join(REPO, "main_all.py"), "-dataset", "tiny-criteo", "-n_epochs",
-                        "1", "-batch_size", "256", "-data_root", str(tmp_path)] + extra, cwd=str(tmp_path),
+                        "1", "-batch_size", "256", "-data_root", str(tmp_path), "-time_on_cuda", "1"] + extra,
+                       cwd=str(tmp_path),
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "Training [1] loss" in r.stdout and "Acc:" in r.stdout and "Avg forward pass time" in r.stdout

@@ -12,12 +12,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int TPW, int MT, int NW = 4, bool LD = true, bool AL = true, int NS = 3, bool REAL = false, int IL = 0>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 16 ? 8 : NW / 2)))
-kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out) {
-  __shared__ f32x4 actl[MT][32 * 64];
+kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out, unsigned* cu_ids) {
+  __shared__ f32x4 actl[MT][REAL ? 1 : 32 * 64];
+  extern __shared__ float lds_pad[];
+  if (cu_ids && threadIdx.x == 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+    cu_ids[blockIdx.x] = ((xcc & 0xF) << 8) | ((hw >> 8) & 0xFF);
+    lds_pad[0] = 0.f;
+  }
   __shared__ float tile[2][16 * 404];
   for (int i = threadIdx.x; i < 2 * 16 * 404; i += 64 * NW) (&tile[0][0])[i] = 1e-3f * (i & 255);
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < MT * 32 * 64; i += 64 * NW) (&actl[0][0])[i] = f32x4{1e-3f * i, 0.5f, 1.f, -2.f};
+  if constexpr (!REAL)
+    for (int i = threadIdx.x; i < MT * 32 * 64; i += 64 * NW) (&actl[0][0])[i] = f32x4{1e-3f * i, 0.5f, 1.f, -2.f};
   __syncthreads();
   f32x4 acc[MT][TPW];
 #pragma unroll
@@ -51,8 +59,8 @@ kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out) {
     LOAD(b1, chunk(1));
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      a0[m] = actl[m][(chunk(0) & 31) * 64 + lane];
-      a1[m] = actl[m][(chunk(1) & 31) * 64 + lane];
+      a0[m] = REAL ? *reinterpret_cast<const f32x4*>(&tile[0][(lane & 15) * 404 + 4 * (lane >> 4)]) : actl[m][(chunk(0) & 31) * 64 + lane];
+      a1[m] = REAL ? *reinterpret_cast<const f32x4*>(&tile[0][(lane & 15) * 404 + 4 * (lane >> 4) + 16]) : actl[m][(chunk(1) & 31) * 64 + lane];
     }
 #define STEP(X, AX, Z, AZ, i)                                                        \
   {                                                                                  \
@@ -121,8 +129,11 @@ kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out) {
       for (int j = 0; j < TPW; ++j) {
         const int n = (g + NW * j) * 16 + (lane & 15);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) tile[(L + 1) & 1][((lane >> 4) * 4 + r) * 404 + n] = fmaxf(acc[0][j][r] + 0.01f, 0.f);
-        acc[0][j] = f32x4{0, 0, 0, 0};
+        for (int m = 0; m < MT; ++m) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tile[(L + 1) & 1][((lane >> 4) * 4 + r) * 404 + n] = fmaxf(acc[m][j][r] + 0.01f, 0.f);
+          acc[m][j] = f32x4{0, 0, 0, 0};
+        }
       }
     }
     __syncthreads();
@@ -136,17 +147,34 @@ kern(const f32x4* __restrict__ w, int NT_, int NC, int layers, float* out) {
 }
 
 template <int TPW, int MT, int NW = 4, bool LD = true, bool AL = true, int NS = 3, bool REAL = false, int IL = 0>
-void run(const char* name, const f32x4* w, int grid, float* out, hipStream_t* st, int nst) {
+void run(const char* name, const f32x4* w, int grid, float* out, hipStream_t* st, int nst, size_t pad = 0,
+         unsigned* cu = nullptr) {
   const int NT_ = NW * TPW, NC = 25, layers = 3;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL, IL>), dim3(grid), dim3(64 * NW), 0, st[0], w, NT_, NC, layers, out);
+  if (pad) CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern<TPW, MT, NW, LD, AL, NS, REAL, IL>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad));
+  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL, IL>), dim3(grid), dim3(64 * NW), pad, st[0], w, NT_, NC, layers, out, nullptr);
+  if (cu) {  // placement of one launch on an idle GPU: distinct CUs used
+    CHECK(hipDeviceSynchronize());
+    hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL, IL>), dim3(grid), dim3(64 * NW), pad, st[0], w, NT_, NC, layers, out, cu);
+    CHECK(hipDeviceSynchronize());
+    unsigned h[4096];
+    CHECK(hipMemcpy(h, cu, grid * sizeof(unsigned), hipMemcpyDeviceToHost));
+    int distinct = 0, maxper = 0;
+    for (int i = 0; i < grid; ++i) {
+      int c = 0, first = 1;
+      for (int j = 0; j < grid; ++j) { if (h[j] == h[i]) { ++c; if (j < i) first = 0; } }
+      distinct += first; maxper = c > maxper ? c : maxper;
+    }
+    printf("  placement of one launch (grid %d, pad %zu): %d distinct CUs, at most %d WGs on one CU\n", grid, pad, distinct, maxper);
+  }
   CHECK(hipDeviceSynchronize());
   const int reps = 100;
   CHECK(hipEventRecord(e0, 0));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL, IL>), dim3(grid), dim3(64 * NW), 0, st[r % nst], w, NT_, NC, layers, out);
+    hipLaunchKernelGGL((kern<TPW, MT, NW, LD, AL, NS, REAL, IL>), dim3(grid), dim3(64 * NW), pad, st[r % nst], w, NT_, NC, layers, out, nullptr);
   for (int k = 0; k < nst; ++k) {
     hipEvent_t ev;
     CHECK(hipEventCreate(&ev));
@@ -176,10 +204,18 @@ int main() {
   CHECK(hipMemcpy(w, h, n * sizeof(f32x4), hipMemcpyHostToDevice));
   hipStream_t st[4];
   for (int k = 0; k < 4; ++k) CHECK(hipStreamCreate(&st[k]));
-  run<3, 1, 8, true, true, 3, true, 0>("TPW=3 8w real, IL0 (forward today)", w, 256, out, st, 1);
-  run<3, 1, 8, true, true, 3, true, 1>("TPW=3 8w real, IL1 4 mfma : 1 load", w, 256, out, st, 1);
-  run<3, 1, 8, true, true, 3, true, 2>("TPW=3 8w real, IL2 loads first", w, 256, out, st, 1);
-  run<3, 1, 8, true, true, 3, true, 3>("TPW=3 8w real, IL3 1 mfma : 1 load", w, 256, out, st, 1);
-  run<3, 1, 8, true, true, 3, true, 0>("TPW=3 8w real, IL0 (forward today)", w, 256, out, st, 1);
+  unsigned* cu;
+  CHECK(hipMalloc(&cu, 4096 * sizeof(unsigned)));
+  run<3, 1, 8, true, true, 3, true, 0>("warm-up", w, 256, out, st, 2);
+  for (int rep = 0; rep < 2; ++rep) {
+    run<3, 1, 8, true, true, 3, true, 0>("MT1 TPW3 8w real (forward today)", w, 256, out, st, 2, 0, cu);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 1 stream", w, 128, out, st, 1, 0, cu);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 2 streams", w, 128, out, st, 2);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 4 streams", w, 128, out, st, 4);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 2 streams, 1 WG/CU (pad)", w, 128, out, st, 2, 40000, cu);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 4 streams, 1 WG/CU (pad)", w, 128, out, st, 4, 40000);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 256, 2 streams", w, 256, out, st, 2, 0, cu);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 256, 1 WG/CU (pad)", w, 256, out, st, 1, 40000);
+  }
   return 0;
 }

@@ -12,8 +12,9 @@ Deliberate deviations (documented in DESIGN.md):
 * ``predict`` / ``predict_proba`` accept ``Xi`` in the layout ``fit`` uses,
   ``[-1, field_size - numerical, 1]``; the reference reshapes to
   ``[-1, field_size, 1]`` (model/DeepFMs.py:854,865) and then fails.
-* No CPU execution: the module must live on a HIP device; there is no
-  fallback path.
+* A module on the CPU runs the host kernels of libdfwfm_cpu.so (include/dfwfm_cpu.h: the custom op's CPU
+  kernel, for the reference's -use_cuda 0 / -time_on_cuda 0 paths); a module on a HIP device runs
+  libdfwfm.so.  Neither falls back to the other or to PyTorch ops: a missing library raises.
 * FFM, quantization and multiple deep towers (``num_deeps > 1``) are not part
   of this engine (out of scope) and raise.
 """
@@ -33,7 +34,7 @@ import torch.nn.functional as F
 
 from . import metrics
 from .QREmbeddingBag import QREmbeddingBag
-from .engine import ForwardEngine
+from .engine import CpuEngine, ForwardEngine
 from ._lib import DfwfmError, FLAG_INDEX_OUT_OF_RANGE
 
 _log = logging.getLogger("xsDeepFwFM")
@@ -217,9 +218,10 @@ class DeepFMs(nn.Module):
         return dict(emb2=e2, emb2_r=e2r, emb1=e1, emb1_r=e1r, n=n, c=c, op=op)
 
     def _sync_engine(self, device):
+        if device.type == "cpu":
+            return self._sync_cpu_engine()
         if device.type != "cuda":
-            raise DfwfmError("DeepFMs forward runs only on a HIP device (no CPU fallback): move the module "
-                             "with .cuda() first")
+            raise DfwfmError(f"DeepFMs forward runs on a HIP device or the CPU, not on {device}")
         if self._engine is None or self._engine.device != device:
             if self._engine is not None:
                 self._engine.close()
@@ -240,6 +242,26 @@ class DeepFMs(nn.Module):
         eng.sync_dense(w("field_cov"), w("fwfm_linear"), w("fm_1st") if self.use_lw else None,
                        self.bias.detach(), lin_w, lin_b, w("net_1_fc") if self.use_deep else None)
         return eng
+
+    def _sync_cpu_engine(self):
+        """The host kernels' engine (libdfwfm_cpu.so), re-described on every call (pointers, no copies)."""
+        if not isinstance(self._engine, CpuEngine):
+            if self._engine is not None:
+                self._engine.close()
+            self._engine = CpuEngine(self.engine_config())
+        first = getattr(self, "fm_1st_embeddings", None)
+        second = getattr(self, "fm_2nd_embeddings", None)
+        fields = [self._field_desc(None if second is None else second[f], None if first is None else first[f])
+                  for f in range(self.field_size)]
+
+        def w(name, attr="weight"):
+            m = getattr(self, name, None)
+            return None if m is None else getattr(m, attr).detach()
+        lin_w = [w(f"net_1_linear_{i}") for i in range(1, self.h_depth + 1)] if self.use_deep else []
+        lin_b = [w(f"net_1_linear_{i}", "bias") for i in range(1, self.h_depth + 1)] if self.use_deep else []
+        self._engine.sync(fields, w("field_cov"), w("fwfm_linear"), w("fm_1st") if self.use_lw else None,
+                          self.bias.detach(), lin_w, lin_b, w("net_1_fc") if self.use_deep else None)
+        return self._engine
 
     def _param_layout(self):
         """The trainable parameters in the C ABI's gradient layout (include/dfwfm.h dfwfm_grads):
@@ -297,7 +319,9 @@ class DeepFMs(nn.Module):
             from .training import train_forward
             return train_forward(self, eng, xi, xv)
         from . import torch_ops  # torch.ops.dfwfm.forward (the registered custom op)
-        if self.use_deep:
+        if device.type == "cpu":
+            pass  # the host kernel has no pruned-layout variants
+        elif self.use_deep:
             # magnitude-pruned hidden layers (fit(prune=1), reference :647-673) run as a sparse MLP when
             # at most sparse_mlp_max_density of their weights are nonzero (checked once per weight update)
             eng.sync_sparse(self.sparse_mlp_max_density)
@@ -397,6 +421,11 @@ class DeepFMs(nn.Module):
             y_pred = torch.sigmoid(logits).cpu().numpy().astype("float64")
             return (total_loss.item() / x_size, self.eval_metric(np.asarray(y)[:x_size], y_pred),
                     self.compute_prauc(y_pred, np.asarray(y)[:x_size]), self.compute_rce(y_pred, np.asarray(y)[:x_size]))
+        if dev.type == "cpu":  # the reference's sklearn metrics on host arrays (:781-783)
+            y_pred = torch.sigmoid(logits).numpy().astype("float64")
+            yt = np.asarray(y)[:x_size]
+            return (total_loss.item() / x_size, metrics.roc_auc_score(yt, y_pred), self.compute_prauc(y_pred, yt),
+                    self.compute_rce(y_pred, yt))
         dm = getattr(self, "_dev_metrics", None)
         if dm is None or dm.device != dev:
             dm = self._dev_metrics = metrics.DeviceMetrics(dev)
@@ -485,10 +514,17 @@ class DeepFMs(nn.Module):
         return size
 
     def time_forward_pass(self, model, batch_xi, batch_xv, cuda=True):
-        """Milliseconds for one forward, timed with HIP events on the current stream (reference :1012-1028)."""
+        """Milliseconds for one forward (reference :1012-1028): HIP events on the current stream for a module on
+        the device; on the CPU a host clock (fractional ms -- the reference's time_ns() // 1e6 truncates to whole
+        milliseconds, :1024-1027, which reads 0 for most forwards of the host kernel)."""
         dev = self._device()
         batch_xi = batch_xi.to(dev)
         batch_xv = batch_xv.to(dev)
+        if dev.type == "cpu":
+            t0 = time_ns()
+            with torch.no_grad():
+                model(batch_xi, batch_xv)
+            return (time_ns() - t0) / 1e6
         start = torch.cuda.Event(enable_timing=True)
         end = torch.cuda.Event(enable_timing=True)
         start.record()
@@ -499,7 +535,11 @@ class DeepFMs(nn.Module):
         return start.elapsed_time(end)
 
     def run_benchmark(self, Xi, Xv, y, batch_size=8192, cuda=True, quantization_aware=False):
-        """Reference :947-1009 minus its CPU thread sweep: metrics, per-batch and per-sample forward times."""
+        """Reference :947-1009: metrics, per-batch and per-sample forward times -- on the device with HIP events,
+        or (a module on the CPU) the reference's thread sweep: per-batch times at 1 and 4 threads
+        (torch.set_num_threads, the host kernel's thread count) and 1000 single-sample latencies at 1 thread."""
+        if self._device().type == "cpu":
+            return self._run_benchmark_cpu(Xi, Xv, y, batch_size)
         Xi = self._fit_layout(Xi)
         Xv = np.asarray(Xv)
         y = np.asarray(y)
@@ -525,6 +565,42 @@ class DeepFMs(nn.Module):
                       for i in range(min(1000, x_size))]
             if single:
                 self.logger.info("\tAvg forward pass time (ms):\t{:.3f}".format(np.mean(single)))
+        return loss, total_metric, prauc, rce
+
+    def _run_benchmark_cpu(self, Xi, Xv, y, batch_size):
+        Xi = self._fit_layout(Xi)
+        Xv = np.asarray(Xv)
+        y = np.asarray(y)
+        x_size = Xi.shape[0]
+        loss, total_metric, prauc, rce = self.eval_by_batch(Xi, Xv, y, x_size)
+        self.logger.info("\tLoss: " + str(loss))
+        self.logger.info("\tAcc: " + str(total_metric))
+        self.logger.info("\tPRAUC: " + str(prauc))
+        self.logger.info("\tRCE: " + str(rce))
+        self.eval()
+        prev = torch.get_num_threads()
+        batch_iter = x_size // batch_size
+        try:
+            with self.deferred_index_check():
+                for threads in (1, 4):
+                    torch.set_num_threads(threads)
+                    spent = [self.time_forward_pass(self, torch.as_tensor(Xi[i * batch_size:(i + 1) * batch_size]),
+                                                    torch.as_tensor(Xv[i * batch_size:(i + 1) * batch_size],
+                                                                    dtype=torch.float32))
+                             for i in range(batch_iter)]
+                    # logged even without a full batch (nan), as the reference does
+                    mean = float(np.mean(spent)) if spent else float("nan")
+                    self.logger.info("\tAvg forward pass time per batch ({}-Threads)(ms):\t{:.3f}".format(threads, mean))
+                    self.logger.info("\tAvg forward pass time (batch) ({}-Threads)(ms):\t{:.6f}".format(
+                        threads, mean / batch_size))
+                torch.set_num_threads(1)
+                single = [self.time_forward_pass(self, torch.as_tensor(Xi[i:i + 1]),
+                                                 torch.as_tensor(Xv[i:i + 1], dtype=torch.float32))
+                          for i in range(min(1000, x_size))]
+                if single:
+                    self.logger.info("\tAvg forward pass time (ms):\t{:.3f}".format(np.mean(single)))
+        finally:
+            torch.set_num_threads(prev)
         return loss, total_metric, prauc, rce
 
     def fetch_teacher_outputs(self, teacher_model, Xi, Xv, x_size):

@@ -39,6 +39,9 @@ def _units():
     return u
 HEADERS = ["dfwfm_internal.h", "dfwfm_device.h", os.path.join("..", "..", "include", "dfwfm.h")]
 ARCH = os.environ.get("DFWFM_OFFLOAD_ARCH", "gfx950")
+CPU_PATH = os.path.join(PKG_DIR, "libdfwfm_cpu.so")
+CPU_SOURCES = ["dfwfm_cpu.cpp"]
+CPU_HEADERS = [os.path.join("..", "..", "include", "dfwfm_cpu.h"), os.path.join("..", "..", "include", "dfwfm.h")]
 INGEST_PATH = os.path.join(PKG_DIR, "libdfwfm_ingest.so")
 INGEST_SOURCES = ["dfwfm_ingest.cpp"]
 INGEST_HEADERS = [os.path.join("..", "..", "include", "dfwfm_ingest.h")]
@@ -175,10 +178,35 @@ def build_ingest(force: bool = False, verbose: bool = False) -> str:
     return INGEST_PATH
 
 
+def _stale_cpu() -> bool:
+    if not os.path.exists(CPU_PATH):
+        return True
+    t = os.path.getmtime(CPU_PATH)
+    deps = [os.path.join(CSRC, s) for s in CPU_SOURCES + CPU_HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_cpu(force: bool = False, verbose: bool = False) -> str:
+    """Compile the host forward / backward library (g++, AVX2 + FMA, std::thread; include/dfwfm_cpu.h): the CPU
+    kernel of torch.ops.dfwfm.forward for modules on the CPU."""
+    if not force and not _stale_cpu():
+        return CPU_PATH
+    cxx = os.environ.get("CXX", "g++")
+    tmp = CPU_PATH + ".tmp"
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-mavx2", "-mfma", "-o", tmp] + \
+        [os.path.join(CSRC, s) for s in CPU_SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, CPU_PATH)
+    return CPU_PATH
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile libdfwfm.so for gfx950 in-tree (hipcc cross-compiles without a GPU): one object per
-    translation unit, compiled in parallel, then linked; and the host-only ingest library."""
+    translation unit, compiled in parallel, then linked; and the host-only ingest and CPU-kernel libraries."""
     build_ingest(force, verbose)
+    build_cpu(force, verbose)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"] + os.environ.get("DFWFM_HIPCC_FLAGS", "").split()
     stamp = os.path.join(CSRC, ".build_flags")  # objects (and the library) built with other flags are stale
@@ -223,6 +251,53 @@ INGEST_SIGNATURES = {
     "dfwfm_feature_map_counts": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "dfwfm_ingest_last_error": (ctypes.c_char_p, []),
 }
+
+
+class dfwfm_cpu_model(ctypes.Structure):
+    _fields_ = [("cfg", dfwfm_config), ("fields", ctypes.POINTER(dfwfm_field_tables)),
+                ("field_cov", ctypes.c_void_p), ("fwfm_lin", ctypes.c_void_p), ("fm_1st", ctypes.c_void_p),
+                ("bias", ctypes.c_void_p), ("lin_w", ctypes.POINTER(ctypes.c_void_p)),
+                ("lin_b", ctypes.POINTER(ctypes.c_void_p)), ("fc_w", ctypes.c_void_p)]
+
+
+_cpu = None
+CPU_SIGNATURES = {
+    "dfwfm_cpu_saved_floats": (ctypes.c_int64, [ctypes.POINTER(dfwfm_config)]),
+    "dfwfm_cpu_forward": (ctypes.c_int, [ctypes.POINTER(dfwfm_cpu_model), _P, ctypes.c_int64, _P, ctypes.c_int64,
+                                         ctypes.c_int64, _P, _P, ctypes.c_float, ctypes.c_uint32,
+                                         ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
+    "dfwfm_cpu_backward": (ctypes.c_int, [ctypes.POINTER(dfwfm_cpu_model), _P, ctypes.c_int64, _P, ctypes.c_int64,
+                                          ctypes.c_int64, _P, _P, ctypes.c_float, ctypes.c_uint32,
+                                          ctypes.POINTER(dfwfm_grads), ctypes.c_int32]),
+    "dfwfm_cpu_last_error": (ctypes.c_char_p, []),
+    "dfwfm_cpu_abi_version": (ctypes.c_int, []),
+}
+
+
+def cpu_lib():
+    """The host-kernel library (include/dfwfm_cpu.h); raises DfwfmError if it is missing."""
+    global _cpu
+    if _cpu is not None:
+        return _cpu
+    with _lock:
+        if _cpu is None:
+            if not os.path.exists(CPU_PATH):
+                raise DfwfmError(f"{CPU_PATH} is missing: run xsdeepfwfm_deprecated_amd.build()")
+            L = ctypes.CDLL(CPU_PATH)
+            for name, (res, args) in CPU_SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            if L.dfwfm_cpu_abi_version() != 1:
+                raise DfwfmError("libdfwfm_cpu ABI mismatch")
+            _cpu = L
+    return _cpu
+
+
+def check_cpu(rc: int, what: str) -> None:
+    if rc != DFWFM_OK:
+        msg = cpu_lib().dfwfm_cpu_last_error().decode(errors="replace")
+        raise DfwfmError(f"{what} failed ({STATUS.get(rc, rc)}): {msg}")
 
 
 def ingest_lib():

@@ -219,3 +219,119 @@ def adam_step(entries, lr, beta1, beta2, eps, weight_decay, step, device):
     _lib.check(_lib.lib().dfwfm_adam_step(arr, len(entries), float(lr), float(beta1), float(beta2), float(eps),
                                           float(weight_decay), int(step), _stream_handle(device)),
                "dfwfm_adam_step")
+
+
+class CpuEngine:
+    """The host counterpart of ForwardEngine for a DeepFMs module on the CPU (include/dfwfm_cpu.h,
+    libdfwfm_cpu.so): the CPU kernel of torch.ops.dfwfm.forward and its backward -- the reference's
+    -use_cuda 0 / -time_on_cuda 0 paths (main_all.py:42-63).  Parameters are read in place through their
+    host pointers (re-described on every sync: no copies).  Threads: torch.get_num_threads(), the knob the
+    reference's benchmark turns (model/DeepFMs.py:983, 1000)."""
+
+    device = torch.device("cpu")
+
+    def __init__(self, cfg: dict):
+        self.cfg = dict(cfg)
+        self.c = _lib.dfwfm_config(**{k: int(v) for k, v in cfg.items()})
+        self.flags = 0
+        self._token = 0
+        self._saved = None
+        self._keep = None
+        _lib.cpu_lib()  # must load: no fallback to torch ops
+
+    def close(self):
+        self._saved = None
+
+    def sync(self, fields, field_cov, fwfm_lin, fm_1st, bias, lin_w, lin_b, fc_w):
+        """fields: list of dicts(emb2, emb2_r, emb1, emb1_r, n, c, op) of CPU tensors / ints; dense tensors."""
+        names = ("emb2", "emb2_r", "emb1", "emb1_r")
+        arr = (_lib.dfwfm_field_tables * len(fields))()
+        tensors = []
+        for i, f in enumerate(fields):
+            for nm in names:
+                if f[nm] is not None:
+                    _require_f32_cpu(f[nm], f"field {i} {nm}")
+                    tensors.append(f[nm])
+            arr[i] = _lib.dfwfm_field_tables(*[None if f[nm] is None else f[nm].data_ptr() for nm in names],
+                                             int(f["n"]), int(f["c"]), int(f["op"]), 0)
+        dense = [field_cov, fwfm_lin, fm_1st, bias, fc_w] + list(lin_w) + list(lin_b)
+        for i, t in enumerate(dense):
+            if t is not None:
+                _require_f32_cpu(t, f"dense parameter {i}")
+        H = len(lin_w)
+        W = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_w])
+        Bv = (ctypes.c_void_p * max(H, 1))(*[t.data_ptr() for t in lin_b])
+        self.model = _lib.dfwfm_cpu_model(self.c, arr, *[None if t is None else t.data_ptr() for t in
+                                                         (field_cov, fwfm_lin, fm_1st, bias)],
+                                          W if H else None, Bv if H else None, None if fc_w is None else fc_w.data_ptr())
+        self._keep = (arr, W, Bv, tensors, dense)
+
+    def _inputs(self, xi, xv):
+        ncat = self.cfg["field_size"] - self.cfg["numerical"]
+        xs = xi.stride(0) if ncat > 0 else 0
+        vs = xv.stride(0) if self.cfg["numerical"] > 0 else 0
+        return ctypes.c_void_p(xi.data_ptr()), xs, ctypes.c_void_p(xv.data_ptr()), vs
+
+    def forward(self, xi, xv, out=None):
+        B = xi.shape[0]
+        if out is None:
+            out = torch.empty(B, dtype=torch.float32)
+        p, xs, v, vs = self._inputs(xi, xv)
+        flag = ctypes.c_int32(0)
+        _lib.check_cpu(_lib.cpu_lib().dfwfm_cpu_forward(ctypes.byref(self.model), p, xs, v, vs, B,
+                                                        ctypes.c_void_p(out.data_ptr()), None, 0.0, 0,
+                                                        ctypes.byref(flag), torch.get_num_threads()),
+                       "dfwfm_cpu_forward")
+        self.flags |= flag.value
+        return out
+
+    def train_forward(self, xi, xv, out, dropout_p: float, seed: int) -> int:
+        B = xi.shape[0]
+        per = int(_lib.cpu_lib().dfwfm_cpu_saved_floats(ctypes.byref(self.c)))
+        self._saved = torch.empty(max(B * per, 1), dtype=torch.float32)
+        p, xs, v, vs = self._inputs(xi, xv)
+        flag = ctypes.c_int32(0)
+        _lib.check_cpu(_lib.cpu_lib().dfwfm_cpu_forward(ctypes.byref(self.model), p, xs, v, vs, B,
+                                                        ctypes.c_void_p(out.data_ptr()),
+                                                        ctypes.c_void_p(self._saved.data_ptr()), float(dropout_p),
+                                                        int(seed) & 0xFFFFFFFF, ctypes.byref(flag),
+                                                        torch.get_num_threads()), "dfwfm_cpu_forward (train)")
+        self.flags |= flag.value
+        self._token += 1
+        self._train = (xi, xv, B, float(dropout_p), int(seed) & 0xFFFFFFFF)
+        return self._token
+
+    def backward(self, token, dlogit, field_grads, dense):
+        if token != self._token or self._saved is None:
+            raise RuntimeError("dfwfm: backward of a stale training forward (another train forward ran in "
+                               "between; one forward/backward pair at a time)")
+        xi, xv, B, p_drop, seed = self._train
+        fg = (_lib.dfwfm_field_grads * len(field_grads))()
+        for i, tup in enumerate(field_grads):
+            fg[i] = _lib.dfwfm_field_grads(*[None if t is None else t.data_ptr() for t in tup])
+        lw, lb = dense.get("lin_w") or [], dense.get("lin_b") or []
+        W = (ctypes.c_void_p * max(len(lw), 1))(*[None if t is None else t.data_ptr() for t in lw])
+        Bv = (ctypes.c_void_p * max(len(lb), 1))(*[None if t is None else t.data_ptr() for t in lb])
+        g = _lib.dfwfm_grads(fg, *[None if dense.get(k) is None else dense[k].data_ptr()
+                                   for k in ("field_cov", "fwfm_lin", "fm_1st", "bias")],
+                             W if lw else None, Bv if lb else None,
+                             None if dense.get("fc_w") is None else dense["fc_w"].data_ptr())
+        p, xs, v, vs = self._inputs(xi, xv)
+        dl = dlogit.contiguous()
+        _lib.check_cpu(_lib.cpu_lib().dfwfm_cpu_backward(ctypes.byref(self.model), p, xs, v, vs, B,
+                                                         ctypes.c_void_p(dl.data_ptr()),
+                                                         ctypes.c_void_p(self._saved.data_ptr()), p_drop, seed,
+                                                         ctypes.byref(g), torch.get_num_threads()),
+                       "dfwfm_cpu_backward")
+        self._saved = None
+
+    def read_error_flag(self) -> int:
+        v, self.flags = self.flags, 0
+        return v
+
+
+def _require_f32_cpu(t, name):
+    if t.dtype != torch.float32 or t.device.type != "cpu":
+        raise RuntimeError(f"dfwfm (CPU): {name} must be a float32 CPU tensor, got {t.dtype} on {t.device}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"dfwfm (CPU): {name} must be contiguous")

@@ -15,7 +15,8 @@ ops so main_all.py's fit()/predict() API is unchanged").  ``DeepFMs.forward`` ca
 * ``train``: keep the activations for the backward (and apply deep-tower dropout ``dropout_p`` with
   counter-hash ``seed``); ``token`` (int64 CPU scalar) names that saved state for the backward.
 
-The op itself never computes on the CPU: the HIP library must be loaded (no fallback).
+Kernels: HIP (libdfwfm.so) for tensors on the device, the host kernel (libdfwfm_cpu.so) for tensors on the CPU;
+neither stands in for the other, and a missing library raises.
 """
 import itertools
 import weakref
@@ -44,12 +45,10 @@ def _model(mid: int):
     return m
 
 
-@torch.library.custom_op("dfwfm::forward", mutates_args=())
-def forward(model_id: int, xi: torch.Tensor, xv: torch.Tensor, params: List[torch.Tensor], train: bool,
-            dropout_p: float, seed: int) -> Tuple[torch.Tensor, torch.Tensor]:
+def _run(model_id, xi, xv, train, dropout_p, seed, engine_type):
     m = _model(model_id)
     eng = m._engine
-    if eng is None or eng.device != xi.device:
+    if eng is None or not isinstance(eng, engine_type) or eng.device != xi.device:
         raise RuntimeError("dfwfm::forward: the module's engine is not synced to this device")
     out = torch.empty(xi.shape[0], dtype=torch.float32, device=xi.device)
     token = 0
@@ -58,6 +57,22 @@ def forward(model_id: int, xi: torch.Tensor, xv: torch.Tensor, params: List[torc
     else:
         eng.forward(xi, xv, out)
     return out, torch.tensor(token, dtype=torch.int64)
+
+
+@torch.library.custom_op("dfwfm::forward", mutates_args=(), device_types="cuda")
+def forward(model_id: int, xi: torch.Tensor, xv: torch.Tensor, params: List[torch.Tensor], train: bool,
+            dropout_p: float, seed: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """HIP kernel (libdfwfm.so, include/dfwfm.h)."""
+    from .engine import ForwardEngine
+    return _run(model_id, xi, xv, train, dropout_p, seed, ForwardEngine)
+
+
+@forward.register_kernel("cpu")
+def _forward_cpu(model_id, xi, xv, params, train, dropout_p, seed):
+    """CPU kernel (libdfwfm_cpu.so, include/dfwfm_cpu.h): a module on the CPU, the reference's -use_cuda 0 /
+    -time_on_cuda 0 paths; selected by the tensors' device, never as a stand-in for the HIP kernel."""
+    from .engine import CpuEngine
+    return _run(model_id, xi, xv, train, dropout_p, seed, CpuEngine)
 
 
 @forward.register_fake

@@ -11,7 +11,8 @@
   resident in HBM and, under ``torch.distributed``, data parallelism: each rank takes its slice of
   every global batch and the flat gradient buffer is all-reduced (RCCL) before the step.
 
-Nothing here computes on the CPU: without the HIP library every entry point raises.
+A module on the CPU trains through the host kernels (libdfwfm_cpu.so: the custom op's CPU kernel and its
+backward) with torch.optim.Adam -- the reference's -use_cuda 0 path; a module on the device never leaves it.
 """
 from __future__ import annotations
 
@@ -579,8 +580,10 @@ def prune_step(model, adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb
     one threshold (:652-656), every `*linear*weight` gets its own (:661-664, including
     fwfm_linear.weight), field_cov is masked by its symmetric part (:666-670)."""
     dev = model._device()
+    if dev.type == "cpu":
+        return _prune_step_host(model, adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb_corr)
     if dev.type != "cuda":
-        raise _lib.DfwfmError("pruning runs on a HIP device (no CPU fallback)")
+        raise _lib.DfwfmError(f"pruning runs on a HIP device or the CPU, not on {dev}")
     pr = getattr(model, "_pruner", None)
     if pr is None or pr.device != dev:
         pr = model._pruner = DevicePruner(dev)
@@ -597,6 +600,26 @@ def prune_step(model, adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb
             if name == "field_cov.weight" and prune_r != 0:
                 F_ = param.shape[0]
                 pr.apply(param.data, pr.threshold([(param.data, F_)], adaptive_sparse * emb_corr), F_)
+
+
+def _prune_step_host(model, adaptive_sparse, prune_fm, prune_r, prune_deep, emb_r, emb_corr):
+    """prune_step for a module on the CPU: the reference's host bisection (:647-673, :807-823) as it stands."""
+    with torch.no_grad():
+        named = list(model.named_parameters())
+        if prune_fm != 0:
+            embs = [p.data for n, p in named if "fm_2nd_embeddings" in n]
+            flat = torch.cat([e.reshape(-1) for e in embs])
+            thr = binary_search_threshold(flat, adaptive_sparse * emb_r, flat.numel())
+            for e in embs:
+                e[e.abs() < thr] = 0
+        for name, param in named:
+            if "linear" in name and "weight" in name and prune_deep != 0:
+                thr = binary_search_threshold(param.data, adaptive_sparse, param.numel())
+                param.data[param.data.abs() < thr] = 0
+            if name == "field_cov.weight" and prune_r != 0:
+                sym = (param.data + param.data.t()) * 0.5
+                thr = binary_search_threshold(sym, adaptive_sparse * emb_corr, param.numel())
+                param.data[sym.abs() < thr] = 0
 
 
 # --------------------------------------------------------------------------------------- fit
@@ -628,8 +651,11 @@ def allreduce_grads(model):
 
 
 def make_optimizer(model):
-    """Reference :553-561: SGD(momentum) unless adam / rmsp / adag; adam runs on the HIP kernel."""
+    """Reference :553-561: SGD(momentum) unless adam / rmsp / adag; adam runs on the HIP kernel for a module on
+    the device, and is torch.optim.Adam -- the reference's own optimizer -- for a module on the CPU."""
     if model.optimizer_type == "adam":
+        if model._device().type == "cpu":
+            return torch.optim.Adam(model.parameters(), lr=model.learning_rate, weight_decay=model.weight_decay)
         return Adam(model.parameters(), lr=model.learning_rate, weight_decay=model.weight_decay)
     if model.optimizer_type == "rmsp":
         return torch.optim.RMSprop(model.parameters(), lr=model.learning_rate, weight_decay=model.weight_decay)
@@ -663,9 +689,9 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
     torch.distributed every global batch of world * batch_size rows is split over the ranks."""
     log = model.logger
     device = model._device()
-    if device.type != "cuda":
+    if device.type not in ("cuda", "cpu"):
         from ._lib import DfwfmError
-        raise DfwfmError("fit runs only on a HIP device (no CPU fallback): move the module with .cuda() first")
+        raise DfwfmError(f"fit runs on a HIP device or the CPU, not on {device}")
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     ncat = model.field_size - model.num
@@ -692,7 +718,8 @@ def fit(model, Xi_train, Xv_train, y_train, Xi_valid=None, Xv_valid=None, y_vali
                                   "the whole batch (model/DeepFMs.py:1060-1061) and does not split over ranks")
     # Adam without distillation (the reference default) runs as a graph-replayed fused step;
     # other optimizers / the KD loss go through autograd + the optimizer
-    fused = model.optimizer_type == "adam" and not teacher_model and getattr(model, "fused_fit", True)
+    fused = model.optimizer_type == "adam" and not teacher_model and getattr(model, "fused_fit", True) and \
+        device.type == "cuda"  # on the CPU: the host kernels through autograd + torch.optim.Adam
     bs = model.batch_size
     gbs = bs * world
     trainer = FusedTrainStep(model, bs, lr=model.learning_rate, weight_decay=model.weight_decay,
