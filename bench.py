@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU sample per thread count")
     ap.add_argument("--inputs", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--table-scale", type=int, default=1,
+                    help="multiply every categorical table's row count by K (Criteo-39's 53 MB of second-order rows "
+                         "fit the 256 MB Infinity Cache; K = 8 gives 424 MB, so the gather reads HBM)")
     ap.add_argument("--no-gate", action="store_true",
                     help="start the timed region without holding the streams until all K steps are enqueued")
     ap.add_argument("--sparse-mlp", type=float, default=None,
@@ -191,7 +194,8 @@ def main():
             dist.init_process_group(backend)
 
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
-    sizes = synth.CRITEO_FEATURE_SIZES
+    K = max(1, a.table_scale)
+    sizes = synth.CRITEO_FEATURE_SIZES[:13] + [n * K for n in synth.CRITEO_FEATURE_SIZES[13:]]
     fwlw = a.first_order == "fwlw"
     qr = a.config == "qr"
     deep = int(a.config not in ("fwfm", "fwfm_pruned"))
@@ -380,7 +384,8 @@ def main():
     if a.config == "pruned" and sparse_on:
         kname = "dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::sparse_mlp_kernel<64>"
         mfma_bound = "valu"  # the sparse MLP runs on the f32 vector FMAs (same 157.3 TF/s peak on gfx950)
-    traffic = pmc_traffic(kname)
+    workload_id = f"{a.config}/{a.first_order}/scale{K}/{a.inputs}"
+    traffic = pmc_traffic(kname, workload_id)
 
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
@@ -394,7 +399,10 @@ def main():
                                   "pruned": ", pruned (sparse 0.90, emb_r 0.444, prune_r 1)",
                                   "fwfm_pruned": ", pruned (sparse 0.90, emb_r 0.444, prune_r 1; FwFM over R's "
                                                  "nonzero pairs)"}[a.config]
+                               + (f", tables x{K} ({sum(sizes[13:]) * 40 / 1e6:.0f} MB of second-order rows)"
+                                  if K > 1 else "")
                                + f"; batch {BATCH} per GPU",
+                   "workload_id": workload_id,
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
                    "launch": ("eager" if a.no_graph else f"hipGraph replay, {G} forwards per graph")
@@ -417,7 +425,7 @@ def main():
         result["roofline"] = {**hbm, **common}
         if traffic:      # the fabric rate of the PMC-counted bytes (40-B rows fetched as 128-B lines)
             result["roofline"]["traffic_gbs"] = round(traffic * S / (launch_ms / 1e3) / 1e9, 1)
-        if a.config in ("fwfm", "fwfm_pruned") and a.inputs == "uniform":
+        if a.config in ("fwfm", "fwfm_pruned") and a.inputs == "uniform" and K == 1:
             # the same 26 rows x 4096 samples from the same tables and nothing else (tools/ubench_gather.hip,
             # one lane per row, three batches in flight): what the gather alone costs at this concurrency
             floor_us = 1.596
@@ -433,18 +441,19 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def pmc_traffic(kname):
-    """HBM bytes per launch of `kname` from the committed PMC summary (tools/pmc.sh + tools/pmc_summary.py):
-    2 x FETCH_SIZE + WRITE_SIZE, FETCH doubled per the gfx950 calibration; None when not profiled."""
+def pmc_traffic(kname, workload_id):
+    """HBM bytes per launch of kernel `kname` on workload `workload_id` from the committed PMC summary
+    (tools/pmc.sh + tools/pmc_summary.py: rocprofv3 --pmc over this bench's own command): 2 x FETCH_SIZE +
+    WRITE_SIZE, FETCH doubled per the gfx950 calibration; None unless that kernel was counted on that workload."""
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(pmc))
     except Exception:
         return None
-    if "kernels" in d:
-        e = d["kernels"].get(kname)
-        return None if e is None else e.get("hbm_bytes_per_launch")
-    return d.get("hbm_bytes_per_launch") if d.get("kernel") == kname else None
+    for e in d.get("entries", []):
+        if e.get("kernel") == kname and e.get("workload") == workload_id:
+            return e.get("hbm_bytes_per_launch")
+    return None
 
 
 def _time_port(torch_port, cfg, tp, xi, xv, seconds, threads):

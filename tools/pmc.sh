@@ -1,16 +1,18 @@
 #!/bin/bash
-# PMC passes over the bench (one counter group per pass; kernel-trace only, no sys/runtime trace),
-# eager launches, one stream.  BENCH_ENV (e.g. DFWFM_SPLIT=1) selects the forward variant, BENCH_ARGS the config.
+# PMC passes over bench.py's own command (hipGraph replay, its streams; rocprofv3 --pmc serialises the dispatches
+# it counts), one counter group per pass, kernel-trace counters only (no sys / runtime trace).
+#   TAG=r03e BENCH_ARGS="--config fwfm --table-scale 8" bash tools/pmc.sh
+# then: python tools/pmc_summary.py TAG gpurun_out profiles/pmc_traffic.json "$BENCH_ARGS"
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r01}
+TAG=${TAG:-r03}
 [ -n "${BENCH_ENV:-}" ] && export ${BENCH_ENV}
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 -s KILL 120 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-graph --streams 1 ${BENCH_ARGS:-} > gpurun_out/pmc_${TAG}_$i.log 2>&1
+  timeout -k 10 -s KILL 150 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 60 --warmup 10 --settle-ms 0 --no-gate --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_${TAG}_$i.log 2>&1
   rc=$?
   echo "pass $i [$grp] rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi

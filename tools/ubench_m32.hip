@@ -207,15 +207,25 @@ int main() {
   unsigned* cu;
   CHECK(hipMalloc(&cu, 4096 * sizeof(unsigned)));
   run<3, 1, 8, true, true, 3, true, 0>("warm-up", w, 256, out, st, 2);
+  // streams with CU masks: A / B halves of the chip, as interleaved bits (even / odd CU ids) or as low / high ids
+  hipStream_t ms[2][4];
+  for (int mode = 0; mode < 2; ++mode)
+    for (int k = 0; k < 4; ++k) {
+      uint32_t mask[8];
+      for (int i = 0; i < 8; ++i) {
+        if (mode == 0) mask[i] = (k & 1) ? 0xAAAAAAAAu : 0x55555555u;
+        else mask[i] = ((i < 4) == ((k & 1) == 0)) ? 0xFFFFFFFFu : 0u;
+      }
+      CHECK(hipExtStreamCreateWithCUMask(&ms[mode][k], 8, mask));
+    }
   for (int rep = 0; rep < 2; ++rep) {
-    run<3, 1, 8, true, true, 3, true, 0>("MT1 TPW3 8w real (forward today)", w, 256, out, st, 2, 0, cu);
-    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 1 stream", w, 128, out, st, 1, 0, cu);
-    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 2 streams", w, 128, out, st, 2);
+    run<3, 1, 8, true, true, 3, true, 0>("MT1 TPW3 8w real (forward today)", w, 256, out, st, 2);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 256, 2 streams (ceiling)", w, 256, out, st, 2);
     run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 4 streams", w, 128, out, st, 4);
-    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 2 streams, 1 WG/CU (pad)", w, 128, out, st, 2, 40000, cu);
-    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 4 streams, 1 WG/CU (pad)", w, 128, out, st, 4, 40000);
-    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 256, 2 streams", w, 256, out, st, 2, 0, cu);
-    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 256, 1 WG/CU (pad)", w, 256, out, st, 1, 40000);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 4 masked streams even/odd", w, 128, out, ms[0], 4, 0, cu);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 4 masked streams lo/hi", w, 128, out, ms[1], 4, 0, cu);
+    run<3, 2, 8, true, true, 3, true, 0>("MT2 grid 128, 2 masked streams even/odd", w, 128, out, ms[0], 2);
+    run<3, 1, 8, true, true, 3, true, 0>("MT1 grid 256, 4 masked streams even/odd", w, 256, out, ms[0], 4);
   }
   return 0;
 }
