@@ -69,6 +69,10 @@ def parse():
                          "the hidden layers' nonzero fraction is at most this); default: the model's")
     ap.add_argument("--pair-max", type=int, default=None,
                     help="DeepFMs.fwfm_pair_max for this run (fwfm_pruned: 0 runs the dense Gram FwFM)")
+    ap.add_argument("--cu-mask", choices=["none", "even-odd", "lo-hi"], default=None,
+                    help="give even-numbered streams one half of the CUs and odd-numbered streams the other (HIP CU "
+                         "masks): with 32-sample workgroups a batch is 128 workgroups, one per CU of a half, so two "
+                         "batches share each CU (default: even-odd with the 32-sample forward, else none)")
     ap.add_argument("--streams", type=int, default=None,
                     help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
                          "batch's workgroup shares each CU, hiding the gather / FwFM phases)")
@@ -129,9 +133,43 @@ class _HostGate:
             pass
 
 
+def r32_on(config="deepfwfm"):
+    """The 32-sample-workgroup forward (fwd32_kernel) is selected (DFWFM_R32) for this deep config."""
+    return config not in ("fwfm", "fwfm_pruned") and os.environ.get("DFWFM_R32", "0") not in ("", "0")
+
+
+def masked_streams(dev, S, how):
+    """S HIP streams (torch ExternalStream): with how = even-odd / lo-hi, even streams on one half of the CUs (even
+    CU ids / the low ids) and odd streams on the other (hipExtStreamCreateWithCUMask)."""
+    if how in (None, "none"):
+        return [torch.cuda.Stream(dev) for _ in range(S)], None
+    import ctypes
+    hip = _hip_runtime()
+    if hip is None or not hasattr(hip, "hipExtStreamCreateWithCUMask"):
+        raise RuntimeError("hipExtStreamCreateWithCUMask unavailable")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    streams, handles = [], []
+    for k in range(S):
+        mask = (ctypes.c_uint32 * words)()
+        for cu in range(ncu):
+            side = (cu & 1) if how == "even-odd" else int(cu >= ncu // 2)
+            if side == (k & 1):
+                mask[cu // 32] |= 1 << (cu % 32)
+        h = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask: {rc}")
+        handles.append(h)
+        streams.append(torch.cuda.ExternalStream(h.value, device=dev))
+    return streams, handles
+
+
 def kernel_name(config="deepfwfm"):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
-    train, part, tile groups); DFWFM_NG / DFWFM_SPLIT select the A/B variants."""
+    train, part, tile groups); DFWFM_NG / DFWFM_SPLIT / DFWFM_R32 select the A/B variants."""
+    if r32_on(config):
+        return f"dfwfm::fwd32_kernel<10,{'true' if config == 'qr' else 'false'}>"
     if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
             return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
@@ -233,7 +271,11 @@ def main():
         batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
     # batches in flight: 2 fill the CUs' register files for the deep configs (two eight-wave workgroups per
     # CU); the FwFM-only forward is latency-bound and gains from a third (three eight-wave workgroups per CU)
-    S = max(1, a.streams if a.streams is not None else (3 if not deep else 2))
+    r32 = r32_on(a.config)
+    # 32-sample workgroups: a batch is 128 workgroups (one per CU of a half), so four in flight on CU-masked
+    # stream pairs put two batches on every CU
+    S = max(1, a.streams if a.streams is not None else (3 if not deep else (4 if r32 else 2)))
+    cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32 else "none")
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
 
     with torch.no_grad():
@@ -241,7 +283,7 @@ def main():
         if a.sparse_mlp is not None:
             model.sparse_mlp_max_density = a.sparse_mlp
         sparse_on = eng.sync_sparse(model.sparse_mlp_max_density) if deep else False
-        streams = [torch.cuda.Stream(dev) for _ in range(S)]
+        streams, _stream_handles = masked_streams(dev, S, cu_mask)
         for st in streams:
             st.wait_stream(torch.cuda.current_stream(dev))
 
@@ -406,7 +448,8 @@ def main():
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
                    "launch": ("eager" if a.no_graph else f"hipGraph replay, {G} forwards per graph")
-                             + (f", {S} streams (batches in flight)" if S > 1 else "")},
+                             + (f", {S} streams (batches in flight)" if S > 1 else "")
+                             + (f", CU masks {cu_mask} (stream pairs on chip halves)" if cu_mask != "none" else "")},
         "settle": {"forwards": settle_n, "ms": round(settle_ms, 1),
                    "what": "untimed back-to-back forwards before the warmup steps (clock ramp)"},
         "wall_s": round(wall, 4),

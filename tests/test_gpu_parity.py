@@ -378,3 +378,38 @@ def test_forward_extreme_shapes_match_oracle(gpu, F, num, D, N, H):
     got = run(m, xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
     assert logit_close(got, ref) < 1e-5
+
+
+@pytest.mark.parametrize("qr", [0, 1])
+@pytest.mark.parametrize("B", [1, 31, 33, 4096 + 17])
+def test_fwd32_bit_identical_to_fwd_kernel(gpu, monkeypatch, qr, B):
+    """The 32-sample-workgroup forward (fwd32_kernel, DFWFM_R32=1: both 16-row tiles per wave in the MLP) gives the
+    same bits as fwd_kernel's static 3x400 form at Criteo-39 sizes (ragged tails, QR fields) and the oracle's
+    logits at the north-star bar."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = synth.CRITEO_FEATURE_SIZES
+    cfg = dict(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0,
+               use_deep=1, use_lw=1, use_fwlw=0, h_depth=3, deep_nodes=400, numerical=13, embedding_bag=qr,
+               qr_flag=qr, qr_operation="mult", qr_collisions=4, qr_threshold=200)
+    m = DeepFMs(**model_kwargs(cfg))
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=55 + qr)
+    xi, xv = synth.synth_inputs(sizes, 13, B, seed=B)
+    outs = {}
+    for r32 in ("0", "1"):
+        monkeypatch.setenv("DFWFM_R32", r32)
+        mm = make_model(cfg, params, gpu)
+        outs[r32] = run(mm, xi, xv, gpu)
+    assert np.array_equal(outs["0"], outs["1"])
+    rows = np.arange(B) if B < 200 else np.random.default_rng(3).choice(B, 128, replace=False)
+    assert logit_close(outs["1"][rows], dfwfm_oracle.forward(cfg, params, xi[rows], xv[rows])) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_fwlw_lw", "deepfwfm_qr_mult", "deepfwfm_qr_add_fwlw",
+                                  "deepfwfm_embbag", "deepfwfm_pruned", "fm_deep"])
+def test_fwd32_matches_reference_goldens(gpu, monkeypatch, name):
+    monkeypatch.setenv("DFWFM_R32", "1")
+    cfg, params, xi, xv, y, l32, l64, auc = load_golden(name)
+    m = make_model(cfg, params, gpu)
+    got = run(m, xi, xv, gpu)
+    assert logit_close(got, l32) < 1e-5 and logit_close(got, l64) < 1e-5

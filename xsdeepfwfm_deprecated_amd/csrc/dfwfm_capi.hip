@@ -24,6 +24,8 @@ struct dfwfm_model {
   size_t lds_bytes;
   size_t lds_gather;   // split forward: LDS of the gather launch (no MLP buffers)
   int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
+  int r32;             // inference forward on 32-sample workgroups (fwd32_kernel)
+  size_t lds_r32;
   size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
   int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
   int shallow;         // no deep tower: shallow_kernel (dfwfm_shallow.hip) runs the inference forward
@@ -257,6 +259,14 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
       m->lds_inf = sizeof(float) * (size_t)lds_layout(F, D, m->MT, m->S, m->SX, m->SY, m->TPWI, 1, true,
                                                       m->tailI != 0, 8).total;
     }
+  }
+  // 32-sample workgroups (fwd32_kernel: every weight fragment feeds both 16-row tiles) for the static 3x400 form;
+  // DFWFM_R32=1 selects it
+  {
+    const char* r32 = getenv("DFWFM_R32");
+    m->r32 = (c.use_deep && r32 && atoi(r32) != 0 &&
+              fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG)) ? 1 : 0;
+    m->lds_r32 = m->r32 ? fwd32_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
   }
   // split forward (opt-in, DFWFM_SPLIT=1): the gather / shallow part and the MLP as two launches, each
   // with its own roofline (HBM-bound gather, MFMA-bound MLP) for profiling.  Measured slower than the
@@ -560,6 +570,7 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
   hipError_t e = (m->shallow && !m->big_tables) ? launch_shallow(a, m->D, m->lds_gather, (hipStream_t)stream)
+                 : (m->r32 && !a.stamps) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
                                              (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");

@@ -377,6 +377,11 @@ hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream
 // the forward without a deep tower (dfwfm_shallow.hip); lds: lds_layout(..., deep = false)
 hipError_t launch_shallow(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
+// the fused inference forward on 32-sample workgroups (dfwfm_fwd32.hip): both 16-row tiles per wave in the MLP;
+// the static 3x400 form only (fwd32_supported), bit-identical logits to fwd_kernel's
+bool fwd32_supported(int F, int D, int H, int NT, int NC0, int tailI, int NG);
+size_t fwd32_lds_bytes(int F, int D, int MT, int S, int SX);
+hipError_t launch_fwd32(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 // per-embedding-size launchers, each compiled in its own translation unit (-DDFWFM_KD=<D>)
 #define DFWFM_PER_D_CAT2(a, b) a##b
 #define DFWFM_PER_D_CAT(a, b) DFWFM_PER_D_CAT2(a, b)
