@@ -133,9 +133,14 @@ class _HostGate:
             pass
 
 
-def r32_on(config="deepfwfm"):
-    """The 32-sample-workgroup forward (fwd32_kernel) is selected (DFWFM_R32) for this deep config."""
-    return config not in ("fwfm", "fwfm_pruned") and os.environ.get("DFWFM_R32", "0") not in ("", "0")
+def r32_on(config="deepfwfm", cu_mask="even-odd"):
+    """The library runs the 32-sample-workgroup forward (fwd32_kernel) for the bench's deep configs when the
+    stream is CU-masked to half of the chip (128 workgroups per 4096-row batch cover it) or DFWFM_R32=1 forces it;
+    DFWFM_R32=0 never."""
+    env = os.environ.get("DFWFM_R32", "")
+    if config in ("fwfm", "fwfm_pruned") or env == "0":
+        return False
+    return env not in ("",) or cu_mask not in (None, "none")
 
 
 def masked_streams(dev, S, how):
@@ -165,10 +170,10 @@ def masked_streams(dev, S, how):
     return streams, handles
 
 
-def kernel_name(config="deepfwfm"):
+def kernel_name(config="deepfwfm", cu_mask="none"):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT / DFWFM_R32 select the A/B variants."""
-    if r32_on(config):
+    if r32_on(config, cu_mask):
         return f"dfwfm::fwd32_kernel<10,{'true' if config == 'qr' else 'false'}>"
     if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
@@ -271,11 +276,12 @@ def main():
         batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
     # batches in flight: 2 fill the CUs' register files for the deep configs (two eight-wave workgroups per
     # CU); the FwFM-only forward is latency-bound and gains from a third (three eight-wave workgroups per CU)
-    r32 = r32_on(a.config)
-    # 32-sample workgroups: a batch is 128 workgroups (one per CU of a half), so four in flight on CU-masked
-    # stream pairs put two batches on every CU
-    S = max(1, a.streams if a.streams is not None else (3 if not deep else (4 if r32 else 2)))
-    cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32 else "none")
+    # deep configs: four batches in flight on CU-masked stream pairs (even / odd CU ids): a 4096-row batch is 128
+    # 32-sample workgroups, which cover a half, so the library runs fwd32_kernel and every CU holds two batches
+    # (DESIGN.md section 3); DFWFM_R32=0: the 16-sample kernel on two plain streams
+    r32_default = deep and os.environ.get("DFWFM_R32", "") != "0"
+    cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32_default else "none")
+    S = max(1, a.streams if a.streams is not None else (3 if not deep else (4 if r32_default else 2)))
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
 
     with torch.no_grad():
@@ -402,6 +408,14 @@ def main():
     # where the streams start and end inside the timed region (fill / drain of a short run)
     skew = {"start_us": [round(s0[first].elapsed_time(s0[k]) * 1e3, 2) for k in range(S)],
             "end_us": [round(s1[k].elapsed_time(s1[last]) * 1e3, 2) for k in range(S)]}
+    # the graphs, then the CU-masked streams they were captured on, are released here, before the runtime's own
+    # teardown (a masked stream left to process exit crashed in __cxa_finalize under rocprofv3)
+    graphs = None
+    torch.cuda.synchronize(dev)
+    if _stream_handles:
+        hip = _hip_runtime()
+        for h in _stream_handles:
+            hip.hipStreamDestroy(h)
     if world > 1:
         t = torch.tensor([ms], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -422,7 +436,7 @@ def main():
     # the S concurrent launches takes ~S x the per-batch time): the aggregate rate over the timed region
     achieved_tf = flops * BATCH * S / (launch_ms / 1e3) / 1e12
     achieved_gbs = bytes_ * BATCH * S / (launch_ms / 1e3) / 1e9
-    kname = kernel_name(a.config)
+    kname = kernel_name(a.config, cu_mask)
     if a.config == "pruned" and sparse_on:
         kname = "dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::sparse_mlp_kernel<64>"
         mfma_bound = "valu"  # the sparse MLP runs on the f32 vector FMAs (same 157.3 TF/s peak on gfx950)

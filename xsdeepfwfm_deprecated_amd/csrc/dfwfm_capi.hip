@@ -24,8 +24,10 @@ struct dfwfm_model {
   size_t lds_bytes;
   size_t lds_gather;   // split forward: LDS of the gather launch (no MLP buffers)
   int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
-  int r32;             // inference forward on 32-sample workgroups (fwd32_kernel)
+  int r32;             // 32-sample workgroups (fwd32_kernel) usable: 0 no, 1 when the stream's CUs are covered, 2 forced
   size_t lds_r32;
+  void* cu_stream[8];  // streams whose CU counts are cached (hipExtStreamGetCUMask), round-robin replaced
+  int cu_count[8], cu_n, cu_next;
   size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
   int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
   int shallow;         // no deep tower: shallow_kernel (dfwfm_shallow.hip) runs the inference forward
@@ -260,13 +262,19 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
                                                       m->tailI != 0, 8).total;
     }
   }
-  // 32-sample workgroups (fwd32_kernel: every weight fragment feeds both 16-row tiles) for the static 3x400 form;
-  // DFWFM_R32=1 selects it
+  // 32-sample workgroups (fwd32_kernel: every weight fragment feeds both 16-row tiles) for the static 3x400 form,
+  // chosen per launch when the batch's 32-sample workgroups still cover every CU the stream may use (a stream
+  // masked to half of the chip, or a batch of >= 32 x CUs rows; else the 16-sample kernel keeps all CUs busy);
+  // DFWFM_R32=0 never, =1 always (tests)
   {
     const char* r32 = getenv("DFWFM_R32");
-    m->r32 = (c.use_deep && r32 && atoi(r32) != 0 &&
-              fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG)) ? 1 : 0;
+    const int mode = !r32 || !*r32 ? 1 : (atoi(r32) != 0 ? 2 : 0);
+    m->r32 = (c.use_deep && fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG)) ? mode : 0;
     m->lds_r32 = m->r32 ? fwd32_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
+    // DFWFM_R32_LDS=<bytes>: reserve at least this much LDS per workgroup (> 80 KiB: one workgroup per CU, so two
+    // batches in flight on plain streams take disjoint halves of the chip; A/B against CU-masked streams)
+    if (const char* pad = getenv("DFWFM_R32_LDS"))
+      if (m->r32 && (size_t)atol(pad) > m->lds_r32 && atol(pad) <= 160 * 1024) m->lds_r32 = (size_t)atol(pad);
   }
   // split forward (opt-in, DFWFM_SPLIT=1): the gather / shallow part and the MLP as two launches, each
   // with its own roofline (HBM-bound gather, MFMA-bound MLP) for profiling.  Measured slower than the
@@ -547,6 +555,31 @@ int diag_stamps_buffer(dfwfm_model* m, int64_t batch, int which, uint64_t** out)
   return DFWFM_OK;
 }
 
+// CUs a stream may use (its CU mask; cached per stream handle)
+int stream_cu_count(dfwfm_model* m, void* stream) {
+  for (int i = 0; i < m->cu_n; ++i)
+    if (m->cu_stream[i] == stream) return m->cu_count[i];
+  int n = 0;
+  uint32_t mask[64] = {0};
+  if (hipExtStreamGetCUMask((hipStream_t)stream, 64, mask) == hipSuccess) {
+    for (int i = 0; i < 64; ++i) n += __builtin_popcount(mask[i]);
+  } else {
+    (void)hipGetLastError();
+    hipDeviceProp_t prop;
+    n = hipGetDeviceProperties(&prop, m->device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+  const int slot = m->cu_n < 8 ? m->cu_n++ : (m->cu_next++ & 7);
+  m->cu_stream[slot] = stream;
+  m->cu_count[slot] = n > 0 ? n : 256;
+  return m->cu_count[slot];
+}
+
+bool use_fwd32(dfwfm_model* m, int64_t batch, void* stream) {
+  if (m->r32 == 0) return false;
+  if (m->r32 == 2) return true;
+  return (batch + 31) / 32 >= stream_cu_count(m, stream);
+}
+
 }  // namespace
 
 extern "C" {
@@ -570,7 +603,7 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
   hipError_t e = (m->shallow && !m->big_tables) ? launch_shallow(a, m->D, m->lds_gather, (hipStream_t)stream)
-                 : (m->r32 && !a.stamps) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                 : (!a.stamps && use_fwd32(m, batch, stream)) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
                                              (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
