@@ -1,6 +1,6 @@
 """Per-phase cycle breakdown of the fused forward from in-kernel s_memtime stamps (diagnostic).
 
-    DFWFM_DIAG_STAMPS=1 python tools/phase_stamps.py [--batch 4096] [--iters 20]
+    DFWFM_DIAG_STAMPS=1 [DFWFM_R32=1] python tools/phase_stamps.py [--batch 4096] [--iters 20]
 """
 import argparse
 import ctypes
@@ -42,7 +42,8 @@ else:
         for _ in range(a.iters):
             m(xi, xv)
 torch.cuda.synchronize()
-grid = (a.batch + 15) // 16
+rows = 32 if os.environ.get("DFWFM_R32") == "1" else 16  # DFWFM_R32=1: fwd32_kernel's 32-sample workgroups
+grid = (a.batch + rows - 1) // rows
 buf = (ctypes.c_uint64 * (grid * 16))()
 n = _lib.lib().dfwfm_diag_stamps(m._engine.handle, buf, grid * 16,
                                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))

@@ -603,7 +603,7 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
   hipError_t e = (m->shallow && !m->big_tables) ? launch_shallow(a, m->D, m->lds_gather, (hipStream_t)stream)
-                 : (!a.stamps && use_fwd32(m, batch, stream)) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                 : use_fwd32(m, batch, stream) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
                                              (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");

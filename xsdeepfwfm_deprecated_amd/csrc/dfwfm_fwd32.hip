@@ -162,6 +162,8 @@ fwd32_kernel(FwdArgs p) {
   float* tailr = smem + L.tailr;
   float* taild = smem + L.taild;
   const int64_t b0 = (int64_t)blockIdx.x * kRows;
+  stamp(p.stamps, 0, tid);
+  stamp_start_rt(p.stamps, tid);
   if (flags & kPrio) __builtin_amdgcn_s_setprio(1);
   const int g = wave;
 
@@ -242,6 +244,7 @@ fwd32_kernel(FwdArgs p) {
     }
     __syncthreads();
   }
+  stamp(p.stamps, 1, tid);
 
   // ---- phase G: gather the E rows (both 16-row tiles) and the table first order --------------------------------
   {
@@ -368,6 +371,7 @@ fwd32_kernel(FwdArgs p) {
     }
   }
   __syncthreads();
+  stamp(p.stamps, 2, tid);
 
   // ---- phase S: first order (fwlw) and the FwFM second order, per 16-row half as fwd_kernel's pieces -------
   if (flags & kFoFwlw) {
@@ -382,54 +386,67 @@ fwd32_kernel(FwdArgs p) {
       fo[b * Fp + f] = s;
     }
   }
+  stamp(p.stamps, 9, tid);
   if (flags & kHasSecond) {
+    // both 16-row halves of a piece at once: one U fragment read feeds two independent MFMA chains (each chain's
+    // order is fwd_kernel's, so the sums are the same bits), which halves this phase's dependent latency
     const int S = p.S;
     const int MTD = p.MT * D;
     const int p_lo = p.fw_off8[wave], p_hi = p.fw_off8[wave + 1];
+    for (int pi = p_lo; pi < p_hi; ++pi) {
+      const int pc = p.fw_list8[pi];
+      const int m = pc / D;
+      const int nt = pc - m * D;
+      const int n = nt * 16 + (lane & 15);
+      const int b = n / D;
+      const float* ecol0 = buf + b * SX + (n - b * D);  // E[b][l][d] = ecol0[l * D]; the second half 16 rows on
+      const float* ecol1 = ecol0 + 16 * SX;
+      const float* ua = upk + m * S * 64 + lane;
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      auto group = [&](int s0, auto U_) {
+        constexpr int U = decltype(U_)::value;
+        float av[U], bv0[U], bv1[U];
 #pragma unroll
-    for (int h = 0; h < kRT; ++h) {
-      const float* bh = buf + h * 16 * SX;
-      for (int pi = p_lo; pi < p_hi; ++pi) {
-        const int pc = p.fw_list8[pi];
-        const int m = pc / D;
-        const int nt = pc - m * D;
-        const int n = nt * 16 + (lane & 15);
-        const int b = n / D;
-        const float* ecol = bh + b * SX + (n - b * D);  // E[16h + b][l][d] = ecol[l * D]
-        const float* ua = upk + m * S * 64 + lane;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        auto group = [&](int s0, auto U_) {
-          constexpr int U = decltype(U_)::value;
-          float av[U], bv[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            av[u] = ua[(s0 + u) * 64];
-            bv[u] = ecol[(4 * (s0 + u) + (lane >> 4)) * D];
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
-        };
-        int s0 = 4 * m;
-        for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
-        const int rem = S - s0;
-        if (rem == 3) group(s0, std::integral_constant<int, 3>{});
-        else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
-        else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
-        float v = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * m + 4 * (lane >> 4) + r;
-          const float e = ecol[(k < F ? k : 0) * D];
-          v = fmaf(k < F ? e : 0.f, acc[r], v);
+        for (int u = 0; u < U; ++u) {
+          const int l = (4 * (s0 + u) + (lane >> 4)) * D;
+          av[u] = ua[(s0 + u) * 64];
+          bv0[u] = ecol0[l];
+          bv1[u] = ecol1[l];
         }
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if (lane < 16) part2[(h * MTD + pc) * 16 + lane] = v;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv0[u], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv1[u], acc1, 0, 0, 0);
+        }
+      };
+      int s0 = 4 * m;
+      for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
+      const int rem = S - s0;
+      if (rem == 3) group(s0, std::integral_constant<int, 3>{});
+      else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
+      else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
+      float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * m + 4 * (lane >> 4) + r;
+        const int kk = (k < F ? k : 0) * D;
+        v0 = fmaf(k < F ? ecol0[kk] : 0.f, acc0[r], v0);
+        v1 = fmaf(k < F ? ecol1[kk] : 0.f, acc1[r], v1);
+      }
+      v0 += __shfl_xor(v0, 16);
+      v1 += __shfl_xor(v1, 16);
+      v0 += __shfl_xor(v0, 32);
+      v1 += __shfl_xor(v1, 32);
+      if (lane < 16) {
+        part2[pc * 16 + lane] = v0;
+        part2[(MTD + pc) * 16 + lane] = v1;
       }
     }
   }
+  stamp(p.stamps, 10, tid);
   __syncthreads();
+  stamp(p.stamps, 11, tid);
   {
     // first[b] (lw projection or plain sum) and second[b]: 16 lanes per sample, every 16th term, then a 16-lane
     // butterfly -- eight waves x four samples = the 32 rows
@@ -456,6 +473,7 @@ fwd32_kernel(FwdArgs p) {
     }
     if (q == 0) fs[b] = first + second;
   }
+  stamp(p.stamps, 3, tid);
   if (flags & kPrio) __builtin_amdgcn_s_setprio(0);
 
   // ---- phase M: the MLP on MFMA, both row tiles per wave, activations in place --------------------------------
@@ -490,6 +508,7 @@ fwd32_kernel(FwdArgs p) {
     ts.init(layer_off, NC, TT, g);
     f32x4 tp[kRT];
     k_loop_rt<kTPW, kRT, kNG, kNS>(acc, buf, SX, ls, wb0, wb1, wb2, lane, ts, tp);
+    if (h == 0) stamp(p.stamps, 12, tid);
     __syncthreads();  // every wave has read the layer's input: the tile may be overwritten
 #pragma unroll
     for (int rt = 0; rt < kRT; ++rt) reinterpret_cast<f32x4*>(tailr)[(g * kRT + rt) * 64 + lane] = tp[rt];
@@ -529,6 +548,7 @@ fwd32_kernel(FwdArgs p) {
       ls.preload(wb0, wb1, lane * 16);
       load_bias(bq, h + 1, nq);
     }
+    if (h == 0) stamp(p.stamps, 13, tid);
     __syncthreads();
     // the split tile: wave g < 4 finishes neuron TT*16 + nq + g of both rows tiles' row rowl from the kNG partials
     if (g < 4) {
@@ -555,6 +575,7 @@ fwd32_kernel(FwdArgs p) {
       }
     }
     __syncthreads();
+    stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
   }
 
   if (tid < kRows && b0 + tid < p.batch) {
@@ -564,6 +585,8 @@ fwd32_kernel(FwdArgs p) {
     deepv += ((taild[tid] + taild[kRows + tid]) + taild[2 * kRows + tid]) + taild[3 * kRows + tid];
     p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
+  stamp(p.stamps, 8, tid);
+  stamp_end_rt(p.stamps, tid);
 }
 
 size_t fwd32_lds_bytes(int F, int D, int MT, int S, int SX) {
