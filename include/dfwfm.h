@@ -272,6 +272,16 @@ int dfwfm_sparse_grads_size(dfwfm_model* m, int32_t family, int64_t batch, int64
 int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, const dfwfm_sparse_dest* dest,
                        int64_t capacity, int64_t* out_dest, float* out_rows, int32_t* out_count, void* ws,
                        int64_t ws_bytes, void* stream);
+/* The same list, formed from the rank's OWN dense gradients of these tables instead of the saved activations: the
+ * backward (DFWFM_BWD_TABLES) scattered them into `local` (local_floats floats, the tables at the `dest` offsets, zero
+ * elsewhere); every touched row is claimed once through `stamp` (local_floats + 1 int32, zeroed once by the caller
+ * and then owned by these calls; the last entry counts the calls), copied to out_rows and cleared in `local` (zero
+ * again afterwards).  Entries come unsorted (destinations unique), sums in atomic order: the replicas of a
+ * data-parallel step stay identical because every rank applies the same bytes of every list.  No sort, no
+ * workspace; stream-ordered, graph-capturable. */
+int dfwfm_sparse_grads_local(dfwfm_model* m, int32_t family, const dfwfm_sparse_dest* dest, int64_t capacity,
+                             float* local, int32_t* stamp, int64_t local_floats, int64_t* out_dest, float* out_rows,
+                             int32_t* out_count, void* stream);
 /* grad[dest[e] + j] += rows[e * width + j] for e < *count (one list; lists with shared destinations must be
  * applied one after the other, in a fixed order, for bit-identical results). */
 int dfwfm_sparse_grads_apply(float* grad, int32_t width, const int64_t* dest, const float* rows, const int32_t* count,

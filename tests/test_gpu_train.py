@@ -846,3 +846,79 @@ def test_full_size_criteo_training_step_matches_oracle(gpu):
         sc = np.abs(og[k]).max()
         assert np.abs(grads[k] - og[k]).max() <= G_TOL * sc + 1e-12, k
     assert check_dp(cfg, params, grads, newp, og, onew, lr, l2) <= DP_TOL
+
+
+def _local_lists_step(m, gpu, xi, xv, y):
+    """Backward with the categorical tables scattered into a local buffer, then dfwfm_sparse_grads_local for both
+    families and the lists applied to a zero buffer: returns {param: grad}, the lists, the local buffer after."""
+    fields, dense, views, flat, _lib, ctypes = _sparse_setup(m, gpu)
+    L, eng = _lib.lib(), m._sync_engine(gpu)
+    st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+    xi_d, xv_d, y_d = (torch.from_numpy(a).to(gpu) for a in (xi.reshape(len(xi), -1), xv, y))
+    out = torch.empty(len(xi), device=gpu)
+    eng.train_forward(xi_d, xv_d, out, 0.0, 0)
+    dl = torch.empty(len(xi), device=gpu)
+    _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(y_d.data_ptr()), len(xi),
+                                float(len(xi)), ctypes.c_void_p(dl.data_ptr()), None, st), "bce")
+    local = torch.zeros_like(flat)
+    stamp = torch.zeros(flat.numel() + 1, dtype=torch.int32, device=gpu)
+    lb, fb = local.data_ptr(), flat.data_ptr()
+    ptr = lambda t, f: None if t is None else ((lb if f >= m.num else fb) + views[id(t)][0] * 4)  # noqa: E731
+    fg = (_lib.dfwfm_field_grads * len(fields))(*[_lib.dfwfm_field_grads(*[ptr(t, f) for t in tup])
+                                                  for f, tup in enumerate(fields)])
+    H = len(dense["lin_w"])
+    gW = (ctypes.c_void_p * max(H, 1))(*[views[id(t)][1].data_ptr() for t in dense["lin_w"]])
+    gB = (ctypes.c_void_p * max(H, 1))(*[views[id(t)][1].data_ptr() for t in dense["lin_b"]])
+    dp = lambda k: None if dense[k] is None else views[id(dense[k])][1].data_ptr()  # noqa
+    grads = _lib.dfwfm_grads(fg, dp("field_cov"), dp("fwfm_lin"), dp("fm_1st"), dp("bias"), gW if H else None,
+                             gB if H else None, dp("fc_w"))
+    _lib.check(L.dfwfm_backward(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), st), "bwd")
+    lists = []
+    for fam, (iq, ir) in ((0, (0, 1)), (1, (2, 3))):
+        o = lambda t: -1 if t is None else views[id(t)][0]  # noqa
+        dest = (_lib.dfwfm_sparse_dest * len(fields))(
+            *[_lib.dfwfm_sparse_dest(o(tup[iq]) if f >= m.num else -1, o(tup[ir]) if f >= m.num else -1)
+              for f, tup in enumerate(fields)])
+        cap, w, wsb = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int64(0)
+        _lib.check(L.dfwfm_sparse_grads_size(eng.handle, fam, len(xi), ctypes.byref(cap), ctypes.byref(w),
+                                             ctypes.byref(wsb)), "size")
+        if cap.value == 0:
+            continue
+        od = torch.full((cap.value,), -7, dtype=torch.int64, device=gpu)
+        orow = torch.zeros(cap.value * w.value, device=gpu)
+        cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+        _lib.check(L.dfwfm_sparse_grads_local(eng.handle, fam, dest, cap.value, ctypes.c_void_p(lb),
+                                              ctypes.c_void_p(stamp.data_ptr()), local.numel(),
+                                              ctypes.c_void_p(od.data_ptr()), ctypes.c_void_p(orow.data_ptr()),
+                                              ctypes.c_void_p(cnt.data_ptr()), st), "local lists")
+        _lib.check(L.dfwfm_sparse_grads_apply(ctypes.c_void_p(fb), w.value, ctypes.c_void_p(od.data_ptr()),
+                                              ctypes.c_void_p(orow.data_ptr()), ctypes.c_void_p(cnt.data_ptr()),
+                                              cap.value, st), "apply")
+        lists.append((fam, w.value, od, orow, cnt))
+    torch.cuda.synchronize()
+    names = {id(p): k for k, p in m.named_parameters()}
+    g = {names[i]: v.detach().cpu().numpy().copy() for i, (o, v) in views.items()}
+    return g, lists, local, stamp
+
+
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult", "train_deepfwfm_fwlw", "train_fwfm_nolw"])
+def test_local_row_lists_equal_dense_table_grads(gpu, name):
+    """dfwfm_sparse_grads_local (the data-parallel step's list builder: claim + copy of the rank's dense table
+    gradients, no sort) gives the categorical tables' gradients back through apply, one entry per touched row, and
+    leaves the local buffer zero (the data-parallel tests run it over several steps with one stamp array)."""
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    gd, _, _ = _sparse_step(m, gpu, xi, xv, y, sparse=False)
+    for rep in range(2):
+        gl, lists, local, stamp = _local_lists_step(m, gpu, xi, xv, y)
+        assert float(local.abs().max()) == 0.0
+        assert int(stamp[-1].item()) == len(lists)  # one epoch per family call
+        for k in gd:
+            sc = np.abs(gd[k]).max()
+            assert np.abs(gl[k] - gd[k]).max() <= G_TOL * sc + 1e-12, (k, rep)
+        ncat = cfg["field_size"] - cfg["numerical"]
+        for fam, w, od, orow, cnt in lists:
+            n = int(cnt.item())
+            d = od[:n].cpu().numpy()
+            assert n > 0 and len(np.unique(d)) == n
+            assert n <= len(xi) * ncat * 2

@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--mode", choices=["fused", "autograd"], default="fused",
                     help="fused: FusedTrainStep (HIP-graph replay, what fit() runs); autograd: model() + "
                          "loss.backward() + HIP Adam")
+    ap.add_argument("--exchange-world1", action="store_true",
+                    help="one rank, but through the data-parallel step (a world-size-1 process group: touched-row "
+                         "lists built, all-gathered and applied) -- the exchange kernels' cost without a second GPU")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; started here unless "
                                                            "torchrun already set WORLD_SIZE)")
     a = ap.parse_args()
@@ -48,10 +51,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or a.exchange_world1:
         import torch.distributed as dist
         backend = os.environ.get("DFWFM_BENCH_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
-        if backend == "nccl":
+        if a.exchange_world1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group(backend, rank=0, world_size=1, **({"device_id": dev} if backend == "nccl" else {}))
+        elif backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
@@ -76,7 +83,7 @@ def main():
 
     trainer = None
     if a.mode == "fused":
-        dist = torch.distributed if world > 1 else None
+        dist = torch.distributed if (world > 1 or a.exchange_world1) else None
         # the four resident batches are read in place (one captured graph set each), like a loader's ring of
         # device input buffers; --copy-inputs copies each batch into the step's own buffers first
         trainer = FusedTrainStep(model, B, lr=1e-3, weight_decay=3e-7, dist=dist, resident_inputs=not a.copy_inputs)
@@ -126,7 +133,7 @@ def main():
                            "mlp_bucket_bytes": 4 * (trainer.grad.numel() - trainer.n_bucket_a)}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if world > 1 or a.exchange_world1:
         torch.distributed.destroy_process_group()
 
 

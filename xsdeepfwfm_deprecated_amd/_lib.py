@@ -131,6 +131,8 @@ SIGNATURES = {
     "dfwfm_sparse_grads": (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.POINTER(dfwfm_sparse_dest), ctypes.c_int64,
                                           _P, _P, _P, _P, ctypes.c_int64, _P]),
     "dfwfm_sparse_grads_apply": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, _P, ctypes.c_int64, _P]),
+    "dfwfm_sparse_grads_local": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(dfwfm_sparse_dest), ctypes.c_int64,
+                                                _P, _P, ctypes.c_int64, _P, _P, _P, _P]),
     "dfwfm_prune_workspace_bytes": (ctypes.c_int64, [ctypes.c_int64]),
     "dfwfm_prune_threshold": (ctypes.c_int, [ctypes.POINTER(dfwfm_prune_source), ctypes.c_int32, ctypes.c_double,
                                              _P, _P, ctypes.c_int64, _P]),

@@ -1190,6 +1190,40 @@ int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, cons
   return e == hipSuccess ? DFWFM_OK : hip_fail(e, "sparse grads");
 }
 
+int dfwfm_sparse_grads_local(dfwfm_model* m, int32_t family, const dfwfm_sparse_dest* dest, int64_t capacity,
+                             float* local, int32_t* stamp, int64_t local_floats, int64_t* out_dest, float* out_rows,
+                             int32_t* out_count, void* stream) {
+  if (!m || !dest || !out_count || !local || !stamp) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (family != DFWFM_FAMILY_SECOND && family != DFWFM_FAMILY_FIRST) return fail(DFWFM_ERR_INVALID_ARG, "bad family");
+  if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_sparse_grads_local needs a preceding dfwfm_train_forward");
+  SparseArgs a;
+  memset(&a, 0, sizeof a);
+  a.ntasks = sparse_tasks(m, family, dest, &a);
+  a.D = m->D;
+  a.F = m->F;
+  a.num = m->num;
+  a.w = family == DFWFM_FAMILY_SECOND ? m->D : 1;
+  a.fields = m->d_fields;
+  a.xi = m->t_xi;
+  a.xi_stride = m->t_xs;
+  a.batch = m->t_batch;
+  const int64_t bound = sparse_capacity(m, family, dest, a.batch);
+  if (bound > capacity)
+    return fail(DFWFM_ERR_INVALID_ARG, "capacity %lld < %lld entries", (long long)capacity, (long long)bound);
+  if (bound > 0 && (!out_dest || !out_rows)) return fail(DFWFM_ERR_INVALID_ARG, "null buffer");
+  // every row a task can touch must lie inside the caller's local buffer (its stamp has local_floats + 1 entries)
+  for (int k = 0; k < a.ntasks; ++k) {
+    const SparseTask& T = a.t[k];
+    const FieldDev& fd = m->h_fields[T.field];
+    const int64_t rows = T.kind == 0 ? fd.n : (T.kind == 1 ? fd.n / fd.c : (int64_t)fd.c);
+    if (T.dest < 0 || T.dest + rows * a.w > local_floats)
+      return fail(DFWFM_ERR_INVALID_ARG, "table of field %d outside the local buffer", (int)T.field);
+  }
+  hipError_t e = launch_sparse_local(a, local, stamp, stamp + local_floats, capacity, out_dest, out_rows, out_count,
+                                     (hipStream_t)stream);
+  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "sparse grads (local)");
+}
+
 int dfwfm_sparse_grads_apply(float* grad, int32_t width, const int64_t* dest, const float* rows, const int32_t* count,
                              int64_t capacity, void* stream) {
   if (capacity < 0 || width < 1) return fail(DFWFM_ERR_INVALID_ARG, "bad size");

@@ -197,10 +197,16 @@ class FusedTrainStep:
         self.adam_mlp = ctypes.cast(ctypes.addressof(adam) + self.n_main * ctypes.sizeof(_lib.dfwfm_adam_tensor),
                                     ctypes.POINTER(_lib.dfwfm_adam_tensor))
         ptr = lambda t: None if t is None else views[id(t)].data_ptr()  # noqa: E731
-        # sparse exchange: the backward leaves the categorical tables alone (no dense scatter); their rows
-        # come from every rank's touched-row lists (_apply_sparse)
+        # sparse exchange: the backward scatters the categorical tables' gradients into a rank-local buffer (same
+        # offsets as in self.grad, whose categorical region the lists fill); dfwfm_sparse_grads_local turns its
+        # touched rows into the lists (and clears them), and every rank adds every rank's lists (_apply_sparse)
+        if self.sparse:
+            self.grad_local = torch.zeros(self.n_tables, dtype=torch.float32, device=dev)
+            self.stamp = torch.zeros(self.n_tables + 1, dtype=torch.int32, device=dev)
+            lbase, gbase = self.grad_local.data_ptr(), self.grad.data_ptr()
+            lptr = lambda t: None if t is None else lbase + (views[id(t)].data_ptr() - gbase)  # noqa: E731
         self.fg = (_lib.dfwfm_field_grads * len(fields))(
-            *[_lib.dfwfm_field_grads(*[None if (self.sparse and f >= model.num) else ptr(t) for t in tup])
+            *[_lib.dfwfm_field_grads(*[(lptr(t) if (self.sparse and f >= model.num) else ptr(t)) for t in tup])
               for f, tup in enumerate(fields)])
         H = len(dense["lin_w"])
         self.gW = (ctypes.c_void_p * max(H, 1))(*[ptr(t) for t in dense["lin_w"]])
@@ -272,20 +278,20 @@ class FusedTrainStep:
         world = self.dist.get_world_size()
         self.sp_send = torch.zeros(nbytes, dtype=torch.uint8, device=self.dev)
         self.sp_recv = torch.zeros(world, nbytes, dtype=torch.uint8, device=self.dev)
-        self.sp_ws = torch.empty(max([f["ws_bytes"] for f in fams] + [1]), dtype=torch.uint8, device=self.dev)
         for i, f in enumerate(fams):
             f["o_cnt"] = o_cnt + 4 * i
         self.sp_fams = fams
         self.sp_bytes = nbytes
 
     def _sparse_lists(self, st):
-        """This rank's touched-row lists of the step just run (part of the first graph)."""
+        """This rank's touched-row lists of the step just run (part of the first graph): the touched rows of the
+        rank-local dense table gradients the backward scattered (claimed once each, copied, cleared)."""
         for f in self.sp_fams:
             sb = self.sp_send.data_ptr()
-            _lib.check(self.L.dfwfm_sparse_grads(
-                self.eng.handle, f["fam"], ctypes.c_void_p(self.dlogit.data_ptr()), f["dest"], f["cap"],
-                ctypes.c_void_p(sb + f["o_dest"]), ctypes.c_void_p(sb + f["o_rows"]), ctypes.c_void_p(sb + f["o_cnt"]),
-                ctypes.c_void_p(self.sp_ws.data_ptr()), self.sp_ws.numel(), st), "dfwfm_sparse_grads")
+            _lib.check(self.L.dfwfm_sparse_grads_local(
+                self.eng.handle, f["fam"], f["dest"], f["cap"], ctypes.c_void_p(self.grad_local.data_ptr()),
+                ctypes.c_void_p(self.stamp.data_ptr()), self.n_tables, ctypes.c_void_p(sb + f["o_dest"]),
+                ctypes.c_void_p(sb + f["o_rows"]), ctypes.c_void_p(sb + f["o_cnt"]), st), "dfwfm_sparse_grads_local")
 
     def _gather_sparse(self):
         return gather_packed(self.dist, self.sp_send, self.sp_recv)
