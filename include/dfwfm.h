@@ -274,8 +274,8 @@ int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, cons
                        int64_t ws_bytes, void* stream);
 /* The same list, formed from the rank's OWN dense gradients of these tables instead of the saved activations: the
  * backward (DFWFM_BWD_TABLES) scattered them into `local` (local_floats floats, the tables at the `dest` offsets, zero
- * elsewhere); every touched row is claimed once through `stamp` (local_floats + 1 int32, zeroed once by the caller
- * and then owned by these calls; the last entry counts the calls), copied to out_rows and cleared in `local` (zero
+ * elsewhere); every touched row is claimed once through `stamp` (local_floats int32 of scratch, any contents: each
+ * call writes the stamps of exactly the rows it reads back), copied to out_rows and cleared in `local` (zero
  * again afterwards).  Entries come unsorted (destinations unique), sums in atomic order: the replicas of a
  * data-parallel step stay identical because every rank applies the same bytes of every list.  No sort, no
  * workspace; stream-ordered, graph-capturable. */

@@ -912,7 +912,6 @@ def test_local_row_lists_equal_dense_table_grads(gpu, name):
     for rep in range(2):
         gl, lists, local, stamp = _local_lists_step(m, gpu, xi, xv, y)
         assert float(local.abs().max()) == 0.0
-        assert int(stamp[-1].item()) == len(lists)  # one epoch per family call
         for k in gd:
             sc = np.abs(gd[k]).max()
             assert np.abs(gl[k] - gd[k]).max() <= G_TOL * sc + 1e-12, (k, rep)

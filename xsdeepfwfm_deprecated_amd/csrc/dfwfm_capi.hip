@@ -1211,7 +1211,7 @@ int dfwfm_sparse_grads_local(dfwfm_model* m, int32_t family, const dfwfm_sparse_
   if (bound > capacity)
     return fail(DFWFM_ERR_INVALID_ARG, "capacity %lld < %lld entries", (long long)capacity, (long long)bound);
   if (bound > 0 && (!out_dest || !out_rows)) return fail(DFWFM_ERR_INVALID_ARG, "null buffer");
-  // every row a task can touch must lie inside the caller's local buffer (its stamp has local_floats + 1 entries)
+  // every row a task can touch must lie inside the caller's local buffer (and its stamp array, as long)
   for (int k = 0; k < a.ntasks; ++k) {
     const SparseTask& T = a.t[k];
     const FieldDev& fd = m->h_fields[T.field];
@@ -1219,8 +1219,7 @@ int dfwfm_sparse_grads_local(dfwfm_model* m, int32_t family, const dfwfm_sparse_
     if (T.dest < 0 || T.dest + rows * a.w > local_floats)
       return fail(DFWFM_ERR_INVALID_ARG, "table of field %d outside the local buffer", (int)T.field);
   }
-  hipError_t e = launch_sparse_local(a, local, stamp, stamp + local_floats, capacity, out_dest, out_rows, out_count,
-                                     (hipStream_t)stream);
+  hipError_t e = launch_sparse_local(a, local, stamp, capacity, out_dest, out_rows, out_count, (hipStream_t)stream);
   return e == hipSuccess ? DFWFM_OK : hip_fail(e, "sparse grads (local)");
 }
 

@@ -251,8 +251,8 @@ hipError_t launch_sparse_grads(const SparseArgs& a, int64_t* out_dest, float* ou
                                size_t ws_bytes, hipStream_t s);
 hipError_t launch_sparse_apply(float* grad, int w, const int64_t* dest, const float* rows, const int32_t* count,
                                int64_t cap, hipStream_t s);
-hipError_t launch_sparse_local(const SparseArgs& a, float* local, int32_t* stamp, int32_t* epoch, int64_t cap,
-                               int64_t* out_dest, float* out_rows, int32_t* out_count, hipStream_t s);
+hipError_t launch_sparse_local(const SparseArgs& a, float* local, int32_t* stamp, int64_t cap, int64_t* out_dest,
+                               float* out_rows, int32_t* out_count, hipStream_t s);
 
 // Sparse deep tower (dfwfm_spmlp.hip): per layer, neurons in groups of four; a group's slot holds its rows'
 // nonzero (k, w bits) pairs in k order, interleaved [entry j][neuron u], padded with (0, 0) to the

@@ -141,22 +141,36 @@ __global__ void __launch_bounds__(256) sparse_apply_kernel(float* __restrict__ g
 
 // ---- touched-row lists from the rank's own dense table gradients (dfwfm_sparse_grads_local) ----------------------
 // The backward scatters the rank's categorical-table gradients into a local dense buffer (as the single-GPU step does
-// into its gradient buffer); the lists are then the touched rows of that buffer: one claim per (table, row) through a
-// per-float stamp (first (table, sample) to exchange the current epoch into a row's stamp appends the row), then
-// every claimed row is copied out and cleared (the buffer is zero again for the next step).  The entries come in no
-// particular order and their sums in no fixed order -- harmless for the replicas: every rank applies the SAME bytes
-// of every rank's list, in rank order, and destinations are unique within a list.
-__global__ void __launch_bounds__(64) local_epoch_kernel(int32_t* __restrict__ epoch, int32_t* __restrict__ count) {
-  if (threadIdx.x == 0) {
-    *epoch = *epoch + 1;
-    *count = 0;
-  }
+// into its gradient buffer); the lists are then the touched rows of that buffer, deduplicated without atomics: every
+// (table, sample) writes its sample index into its row's stamp (plain stores, some sample wins), then the sample
+// whose index the stamp holds appends the row (only rows touched in this call are ever read back, so stale stamps
+// of other rows never matter and the stamps need no reset); every appended row is copied out and cleared (the buffer
+// is zero again for the next step).  Entries come in no particular order and their sums in atomic order -- harmless
+// for the replicas: every rank applies the SAME bytes of every rank's list, in rank order, and destinations are
+// unique within a list.
+__device__ __forceinline__ int64_t local_row_off(const SparseArgs& a, int k, int64_t b) {
+  const SparseTask T = a.t[k];
+  const FieldDev fd = a.fields[T.field];
+  int64_t idx = a.xi[b * a.xi_stride + (T.field - a.num)];
+  if (idx < 0 || idx >= fd.n) idx = 0;  // the forward and the scatter clamped it the same way
+  int64_t row = idx;
+  if (T.kind == 1) row = idx / T.c;
+  else if (T.kind == 2) row = idx % T.c;
+  return T.dest + row * a.w;
+}
+
+__global__ void __launch_bounds__(256) local_mark_kernel(const SparseArgs a, int32_t* __restrict__ stamp,
+                                                         int32_t* __restrict__ count) {
+  const int k = blockIdx.y;
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k == 0 && b == 0) *count = 0;
+  if (k < a.ntasks && b < a.batch) stamp[local_row_off(a, k, b)] = (int32_t)b;
 }
 
 constexpr int kClaimThreads = 1024;  // one list-counter atomic per 1024 (table, sample) pairs
 
-__global__ void __launch_bounds__(kClaimThreads) local_claim_kernel(const SparseArgs a, int32_t* __restrict__ stamp,
-                                                                    const int32_t* __restrict__ epoch,
+__global__ void __launch_bounds__(kClaimThreads) local_claim_kernel(const SparseArgs a,
+                                                                    const int32_t* __restrict__ stamp,
                                                                     int64_t* __restrict__ out_dest,
                                                                     int32_t* __restrict__ count) {
   __shared__ int32_t wave_n[kClaimThreads / 64];
@@ -166,19 +180,10 @@ __global__ void __launch_bounds__(kClaimThreads) local_claim_kernel(const Sparse
   bool claim = false;
   int64_t off = 0;
   if (k < a.ntasks && b < a.batch) {
-    const SparseTask T = a.t[k];
-    const FieldDev fd = a.fields[T.field];
-    int64_t idx = a.xi[b * a.xi_stride + (T.field - a.num)];
-    if (idx < 0 || idx >= fd.n) idx = 0;  // the forward and the scatter clamped it the same way
-    int64_t row = idx;
-    if (T.kind == 1) row = idx / T.c;
-    else if (T.kind == 2) row = idx % T.c;
-    off = T.dest + row * a.w;
-    const int32_t ep = *epoch;
-    claim = atomicExch(stamp + off, ep) != ep;
+    off = local_row_off(a, k, b);
+    claim = stamp[off] == (int32_t)b;
   }
-  // slots: a prefix over the workgroup's waves, one counter atomic per workgroup (a single counter taking one
-  // returning atomic per wave serialised at ~15 ns each: 25 us per family at Criteo-39)
+  // slots: a prefix over the workgroup's waves, one counter atomic per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t mask = __ballot(claim);
   if (lane == 0) wave_n[wave] = (int32_t)__popcll(mask);
@@ -208,18 +213,17 @@ __global__ void __launch_bounds__(256) local_gather_kernel(float* __restrict__ l
   *src = 0.f;
 }
 
-hipError_t launch_sparse_local(const SparseArgs& a, float* local, int32_t* stamp, int32_t* epoch, int64_t cap,
-                               int64_t* out_dest, float* out_rows, int32_t* out_count, hipStream_t s) {
-  hipLaunchKernelGGL(local_epoch_kernel, dim3(1), dim3(64), 0, s, epoch, out_count);
+hipError_t launch_sparse_local(const SparseArgs& a, float* local, int32_t* stamp, int64_t cap, int64_t* out_dest,
+                               float* out_rows, int32_t* out_count, hipStream_t s) {
   const int64_t n = (int64_t)a.ntasks * a.batch;
-  if (n > 0) {
-    const unsigned gb = (unsigned)((a.batch + kClaimThreads - 1) / kClaimThreads);
-    hipLaunchKernelGGL(local_claim_kernel, dim3(gb, a.ntasks), dim3(kClaimThreads), 0, s, a, stamp, epoch, out_dest,
-                       out_count);
-    if (cap > 0)
-      hipLaunchKernelGGL(local_gather_kernel, dim3((unsigned)((cap * a.w + 255) / 256)), dim3(256), 0, s, local, a.w,
-                         out_dest, out_count, cap, out_rows);
-  }
+  if (n == 0) return hipMemsetAsync(out_count, 0, sizeof(int32_t), s);
+  hipLaunchKernelGGL(local_mark_kernel, dim3((unsigned)((a.batch + 255) / 256), a.ntasks), dim3(256), 0, s, a, stamp,
+                     out_count);
+  hipLaunchKernelGGL(local_claim_kernel, dim3((unsigned)((a.batch + kClaimThreads - 1) / kClaimThreads), a.ntasks),
+                     dim3(kClaimThreads), 0, s, a, stamp, out_dest, out_count);
+  if (cap > 0)
+    hipLaunchKernelGGL(local_gather_kernel, dim3((unsigned)((cap * a.w + 255) / 256)), dim3(256), 0, s, local, a.w,
+                       out_dest, out_count, cap, out_rows);
   return hipGetLastError();
 }
 

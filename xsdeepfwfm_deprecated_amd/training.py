@@ -202,7 +202,7 @@ class FusedTrainStep:
         # touched rows into the lists (and clears them), and every rank adds every rank's lists (_apply_sparse)
         if self.sparse:
             self.grad_local = torch.zeros(self.n_tables, dtype=torch.float32, device=dev)
-            self.stamp = torch.zeros(self.n_tables + 1, dtype=torch.int32, device=dev)
+            self.stamp = torch.empty(self.n_tables, dtype=torch.int32, device=dev)  # scratch, any contents
             lbase, gbase = self.grad_local.data_ptr(), self.grad.data_ptr()
             lptr = lambda t: None if t is None else lbase + (views[id(t)].data_ptr() - gbase)  # noqa: E731
         self.fg = (_lib.dfwfm_field_grads * len(fields))(
