@@ -729,10 +729,12 @@ def test_resident_inputs_graphs_equal_copied_inputs(gpu):
     assert np.median(e) < 1e-4 and np.quantile(e, 0.999) < 0.02, (np.median(e), np.quantile(e, 0.999))
 
 
-def _nccl_world1_worker(port, q, name):
+def _nccl_world1_worker(port, q, name, graph_comm):
     """A world-size-1 RCCL process group (backend "nccl" is RCCL on ROCm): the packed touched-row all-gather
-    (all_gather_into_tensor branch of gather_packed) and FusedTrainStep's bucketed exchange run over RCCL."""
+    (all_gather_into_tensor branch of gather_packed) and FusedTrainStep's bucketed exchange run over RCCL --
+    captured into the step's graph (graph_comm) or issued between its graphs."""
     import torch.distributed as dist
+    os.environ["DFWFM_DP_GRAPH_COMM"] = "1" if graph_comm else "0"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -746,8 +748,8 @@ def _nccl_world1_worker(port, q, name):
         recv = torch.zeros(1, send.numel(), dtype=torch.uint8, device=dev)
         gather_packed(dist, send, recv, async_op=True).wait()
         gathered_ok = bool(torch.equal(recv[0], send))
-        sparse = _dp_steps(name, True, 2, dist, 0, 1)   # touched-row lists over all_gather_into_tensor
-        dense = _dp_steps(name, False, 2, dist, 0, 1)   # bucketed all-reduces of the whole buffer
+        sparse = _dp_steps(name, True, 3, dist, 0, 1)   # touched-row lists over all_gather_into_tensor
+        dense = _dp_steps(name, False, 3, dist, 0, 1)   # bucketed all-reduces of the whole buffer
         q.put(("ok", gathered_ok, sparse, dense))
     except Exception as e:  # report, do not hang the parent
         q.put(("error", repr(e), None, None))
@@ -755,11 +757,13 @@ def _nccl_world1_worker(port, q, name):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("graph_comm", [True, False])
 @pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult"])
-def test_rccl_exchange_world_one_matches_single_process(gpu, name):
+def test_rccl_exchange_world_one_matches_single_process(gpu, name, graph_comm):
     """The RCCL branch of the data-parallel exchange runs: with a world-size-1 nccl group the packed
-    all-gather returns the buffer, and two FusedTrainSteps through the sparse and the dense exchange give the
-    single-process gradients (2e-5 of each tensor's largest entry) and logits (1e-5 * max(1, |ref|))."""
+    all-gather returns the buffer, and three FusedTrainSteps (eager, captured, replayed) through the sparse and
+    the dense exchange give the single-process gradients (2e-5 of each tensor's largest entry), logits
+    (1e-5 * max(1, |ref|)) and parameters, with the collectives inside the step's graph or between its graphs."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -767,14 +771,14 @@ def test_rccl_exchange_world_one_matches_single_process(gpu, name):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_nccl_world1_worker, args=(port, q, name))
+    p = ctx.Process(target=_nccl_world1_worker, args=(port, q, name, graph_comm))
     p.start()
     status, gathered_ok, sparse, dense = q.get(timeout=300)
     p.join(60)
     assert status == "ok", gathered_ok
     assert p.exitcode == 0
     assert gathered_ok
-    (gs, os_), ps = _dp_steps(name, True, 2, None, 0, 1)
+    (gs, os_), ps = _dp_steps(name, True, 3, None, 0, 1)
     for (g, o), pr in (sparse, dense):
         assert logit_close(o, os_) < 1e-5
         for k in gs:

@@ -70,9 +70,7 @@ def test_binary_search_threshold_hits_target():
 
 def _dp_worker(rank, world, port, q):
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         from xsdeepfwfm_deprecated_amd.training import allreduce_grads
         m = torch.nn.Module()
@@ -94,11 +92,9 @@ def _dp_worker(rank, world, port, q):
 
 
 def test_dp_grad_allreduce_gloo_world2():
-    import socket
+    import tempfile
     import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = os.path.join(tempfile.mkdtemp(), "store")  # a file rendezvous: no port to race for under pytest -n
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
@@ -120,9 +116,7 @@ def _sparse_protocol_worker(rank, world, port, q):
     normalised by the global batch) -> (dest, row) list at fixed capacity packed into one byte buffer ->
     training.gather_packed over gloo -> every rank's lists added in rank order."""
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         from xsdeepfwfm_deprecated_amd.training import gather_packed
         cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_lw")
@@ -163,11 +157,9 @@ def test_touched_row_exchange_protocol_gloo_world2():
     """configs[4] exchange at oracle level on CPU: two gloo ranks' touched-row lists, all-gathered at fixed
     capacity and added in rank order, equal the dense table gradients of one process on the global batch,
     identically on both ranks."""
-    import socket
+    import tempfile
     import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = os.path.join(tempfile.mkdtemp(), "store")  # a file rendezvous: no port to race for under pytest -n
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_sparse_protocol_worker, args=(r, 2, port, q)) for r in range(2)]

@@ -19,6 +19,7 @@ from __future__ import annotations
 import ctypes
 import logging
 import math
+import os
 from time import time
 
 import numpy as np
@@ -410,6 +411,46 @@ class FusedTrainStep:
         wa.wait()
         wb.wait()
 
+    def _replay_dp(self, g1b, ga, g2, g2b):
+        """The data-parallel step after the first graph, as two streams: a side stream runs the weight-gradient
+        GEMM (queued first, so the GPU has it while the host issues the collectives), the MLP bucket's
+        all-reduce and the MLP's Adam; the current stream waits for the first bucket (and the touched-row
+        lists), adds the lists and runs the main Adam (tables and the shallow part).  The two halves write
+        disjoint parameters and Adam states, so the order between them is free."""
+        if self.dist is None:  # one process without an MLP: the backward is whole in the first graph
+            g2.replay()
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        if g1b is not None:
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(self.dev)
+            side = self._side
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                g1b.replay()
+        lo, hi = (self.n_tables if self.sparse else 0), self.n_bucket_a
+        works = [self._gather_sparse()] if self.sparse else []
+        if hi > lo:
+            works.append(self.dist.all_reduce(self.grad[lo:hi], async_op=True))
+        if g1b is not None:
+            with torch.cuda.stream(side):
+                if self.grad.numel() > hi:
+                    self.dist.all_reduce(self.grad[hi:], async_op=True).wait()
+                g2b.replay()
+        for w in works:
+            w.wait()
+        if ga is not None:
+            ga.replay()
+        g2.replay()
+        if g1b is not None:
+            cur.wait_stream(side)
+
+    def _comm_in_graph(self):
+        """Whether the step's collectives are captured into its graph: RCCL (gloo's are host calls), unless
+        DFWFM_DP_GRAPH_COMM=0."""
+        return (self.dist is not None and self.dist.get_backend() == "nccl"
+                and os.environ.get("DFWFM_DP_GRAPH_COMM", "1") != "0")
+
     def _capture(self, denom):
         """Graphs: forward + backward (its MLP-weight part separately under DP, see _exchange), then Adam;
         the RCCL all-reduces run between them."""
@@ -431,7 +472,39 @@ class FusedTrainStep:
                     self._adam_main()
                     s.wait_stream(s1)
             torch.cuda.current_stream(self.dev).wait_stream(s)
-            return g1, None, None, None
+            return g1, None, None, None, None
+        if self._comm_in_graph():
+            # RCCL: the collectives are captured too, so the whole data-parallel step is one graph (no host
+            # round trips between its parts).  The first bucket and the lists go out right after the backward's
+            # first part; the weight-gradient GEMM, the MLP bucket and the MLP's Adam fork onto s1 (the RCCL
+            # stream runs the collectives in issue order: lists, first bucket, then the MLP bucket behind the GEMM)
+            s1 = torch.cuda.Stream(self.dev)
+            lo, hi = (self.n_tables if self.sparse else 0), self.n_bucket_a
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g1, stream=s):
+                    self._part1(self.B, denom)
+                    bucketed = self._bucketed()
+                    if bucketed:
+                        s1.wait_stream(s)
+                    if self.sparse:
+                        gather_packed(self.dist, self.sp_send, self.sp_recv, async_op=False)
+                    if hi > lo:
+                        self.dist.all_reduce(self.grad[lo:hi])
+                    if bucketed:
+                        with torch.cuda.stream(s1):
+                            self._part1b()
+                            if self.grad.numel() > hi:
+                                self.dist.all_reduce(self.grad[hi:])
+                            self._adam_mlp()
+                    if self.sparse:
+                        self._apply_sparse()
+                    if bucketed:
+                        self._adam_main()
+                        s.wait_stream(s1)
+                    else:
+                        self._part2()
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            return g1, None, None, None, None
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s):
                 self._part1(self.B, denom)
@@ -444,10 +517,20 @@ class FusedTrainStep:
                 ga = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga, stream=s):
                     self._apply_sparse()
+            # bucketed: the MLP's Adam is its own graph, replayed on a side stream behind the weight-gradient
+            # GEMM and the MLP bucket's all-reduce, while the main Adam runs behind the first bucket (_replay_dp)
+            g2b = None
             with torch.cuda.graph(g2, stream=s):
-                self._part2()
+                if g1b is not None:
+                    self._adam_main()
+                else:
+                    self._part2()
+            if g1b is not None:
+                g2b = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2b, stream=s):
+                    self._adam_mlp()
         torch.cuda.current_stream(self.dev).wait_stream(s)
-        return g1, g1b, ga, g2
+        return g1, g1b, ga, g2, g2b
 
     def _direct_inputs(self, xi, xv, y, n):
         """(xi, xv, y) as the graphs can read them in place, or None (then they are copied): a full batch of
@@ -504,12 +587,10 @@ class FusedTrainStep:
             self._graph_sets[key] = hit  # most recently used last
             self.graphs = hit[0]
             self._graph_key = key
-            g1, g1b, ga, g2 = self.graphs
+            g1, g1b, ga, g2, g2b = self.graphs
             g1.replay()
             if g2 is not None:  # else the whole step (backward parts and Adam) is in g1
-                self._exchange(lambda: g1b.replay() if g1b is not None else None,
-                               lambda: ga.replay() if ga is not None else None)
-                g2.replay()
+                self._replay_dp(g1b, ga, g2, g2b)
         else:
             self._in = inputs
             self._part1(n, denom)
