@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--exchange-world1", action="store_true",
                     help="one rank, but through the data-parallel step (a world-size-1 process group: touched-row "
                          "lists built, all-gathered and applied) -- the exchange kernels' cost without a second GPU")
+    ap.add_argument("--apply-worlds", default="",
+                    help="with --exchange-world1: afterwards time the apply of W ranks' lists (comma list of W; the "
+                         "lists of W distinct batches built by the step itself)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; started here unless "
                                                            "torchrun already set WORLD_SIZE)")
     a = ap.parse_args()
@@ -131,10 +134,53 @@ def main():
         res["exchange"] = {"backend": torch.distributed.get_backend(), "packed_bytes_per_rank": trainer.sp_bytes,
                            "dense_bucket_bytes": 4 * (trainer.n_bucket_a - trainer.n_tables),
                            "mlp_bucket_bytes": 4 * (trainer.grad.numel() - trainer.n_bucket_a)}
+    if a.apply_worlds and trainer is not None and getattr(trainer, "sparse", False):
+        res["apply"] = apply_bench(trainer, model, sizes, B, dev, [int(w) for w in a.apply_worlds.split(",")])
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1 or a.exchange_world1:
         torch.distributed.destroy_process_group()
+
+
+def apply_bench(trainer, model, sizes, B, dev, worlds, reps=50):
+    """The receive side of the touched-row exchange at world sizes the box cannot host: the step's own lists for
+    max(worlds) distinct batches stacked as an all-gathered buffer and applied (one launch per rank and family, in
+    rank order, as the step does) to a copy of the gradient buffer, graph-replayed."""
+    import ctypes
+    from xsdeepfwfm_deprecated_amd import _lib, synth
+    L = _lib.lib()
+    snaps = []
+    for i in range(max(worlds)):
+        xi, xv = synth.synth_inputs(sizes, 13, B, seed=7000 + i)
+        y = synth.synth_labels(B, seed=7000 + i)
+        trainer.step(*(torch.from_numpy(t).to(dev) for t in (xi, xv)), torch.from_numpy(y).float().to(dev))
+        snaps.append(trainer.sp_send.clone())
+    torch.cuda.synchronize(dev)
+    counts = [[int(sn[f["o_cnt"]:f["o_cnt"] + 4].view(torch.int32).item()) for sn in snaps] for f in trainer.sp_fams]
+    grad = trainer.grad.clone()
+    out = {"entries_per_rank": {"width%d" % f["w"]: sum(c) / len(c) for f, c in zip(trainer.sp_fams, counts)},
+           "capacity": {"width%d" % f["w"]: f["cap"] for f in trainer.sp_fams}}
+    for w in worlds:
+        recv = torch.stack(snaps[:w])
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)  # the capture stream
+            for r in range(w):
+                rb = recv[r].data_ptr()
+                for f in trainer.sp_fams:
+                    _lib.check(L.dfwfm_sparse_grads_apply(
+                        ctypes.c_void_p(grad.data_ptr()), f["w"], ctypes.c_void_p(rb + f["o_dest"]),
+                        ctypes.c_void_p(rb + f["o_rows"]), ctypes.c_void_p(rb + f["o_cnt"]), f["cap"], st), "apply")
+        for _ in range(3):
+            g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        out["world%d_us" % w] = round(e0.elapsed_time(e1) * 1e3 / reps, 2)
+    return out
 
 
 if __name__ == "__main__":
