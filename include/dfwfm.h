@@ -190,6 +190,11 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads
  * in this order, on one stream. */
 #define DFWFM_BWD_TABLES 1
 #define DFWFM_BWD_MLP_WEIGHTS 2
+/* DFWFM_BWD_TABLES in two halves: the per-tile backward (TILES: dE, the G chain, per-tile partials) and what
+ * sums over the batch (SPREAD: the shallow reductions' final sums and the table scatter).  SPREAD and
+ * DFWFM_BWD_MLP_WEIGHTS both only read what TILES saved, so they may run concurrently on two streams. */
+#define DFWFM_BWD_TILES 4
+#define DFWFM_BWD_SPREAD 8
 int dfwfm_backward_phases(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads, int32_t phases,
                           void* stream);
 
@@ -212,8 +217,8 @@ int dfwfm_adam_step(const dfwfm_adam_tensor* tensors, int32_t n, double lr, doub
 /* ---- graph-replayable training step -------------------------------------------------------
  * A training step whose every launch reads its per-step scalars from device memory can be captured
  * once into a HIP graph and replayed (no host work per step).  The per-step state is one
- * caller-allocated, zero-initialised device block of DFWFM_ADAM_STATE_BYTES: an int64 step counter
- * followed by the step's Adam scalars. */
+ * caller-allocated, zero-initialised device block of DFWFM_ADAM_STATE_BYTES: an int64 step counter,
+ * the last step's Adam scalars and a completion counter (zero between steps). */
 #define DFWFM_ADAM_STATE_BYTES 48
 
 /* From now on the dropout masks of dfwfm_train_forward / dfwfm_backward mix the device step counter
@@ -227,8 +232,9 @@ int dfwfm_set_step_source(dfwfm_model* m, const int64_t* step_dev);
  * capture time and re-captures when it differs. */
 int dfwfm_workspace_generation(const dfwfm_model* m, int64_t* gen);
 
-/* dfwfm_adam_step with the step counter and bias corrections on the device: increments the counter
- * in `state_dev`, derives the scalars there (double, then f32) and updates every tensor. */
+/* dfwfm_adam_step with the step counter and bias corrections on the device: every workgroup derives the
+ * scalars of step (counter + 1) there (double, then f32) and updates its tensors; the last workgroup of the
+ * call's last launch advances the counter (no separate scalar launch). */
 int dfwfm_adam_step_dev(const dfwfm_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,
                         double eps, double weight_decay, void* state_dev, void* stream);
 

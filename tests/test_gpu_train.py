@@ -524,7 +524,7 @@ def _sparse_setup(m, gpu):
     return fields, dense, views, flat, _lib, ctypes
 
 
-def _sparse_step(m, gpu, xi, xv, y, sparse):
+def _sparse_step(m, gpu, xi, xv, y, sparse, split=False):
     """One backward of m on (xi, xv, y): dense scatter (sparse=False) or touched-row lists applied to a zero
     buffer (sparse=True).  Returns {param name: grad}, the lists (for sparse) and the flat buffer."""
     fields, dense, views, flat, _lib, ctypes = _sparse_setup(m, gpu)
@@ -545,7 +545,17 @@ def _sparse_step(m, gpu, xi, xv, y, sparse):
     dp = lambda k: None if dense[k] is None else views[id(dense[k])][1].data_ptr()  # noqa
     grads = _lib.dfwfm_grads(fg, dp("field_cov"), dp("fwfm_lin"), dp("fm_1st"), dp("bias"), gW if H else None,
                              gB if H else None, dp("fc_w"))
-    _lib.check(L.dfwfm_backward(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), st), "bwd")
+    if split:  # the per-tile backward, then the weight GEMM on a side stream beside the reductions + scatter
+        ph = lambda bits, s_: _lib.check(L.dfwfm_backward_phases(  # noqa: E731
+            eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), bits, s_), "bwd phases")
+        ph(_lib.BWD_TILES, st)
+        side = torch.cuda.Stream(gpu)
+        side.wait_stream(torch.cuda.current_stream(gpu))
+        ph(_lib.BWD_MLP_WEIGHTS, ctypes.c_void_p(side.cuda_stream))
+        ph(_lib.BWD_SPREAD, st)
+        torch.cuda.current_stream(gpu).wait_stream(side)
+    else:
+        _lib.check(L.dfwfm_backward(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), st), "bwd")
     lists = []
     if sparse:
         for fam, (iq, ir) in ((0, (0, 1)), (1, (2, 3))):
@@ -925,3 +935,28 @@ def test_local_row_lists_equal_dense_table_grads(gpu, name):
             d = od[:n].cpu().numpy()
             assert n > 0 and len(np.unique(d)) == n
             assert n <= len(xi) * ncat * 2
+
+
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult", "train_fwfm_nolw"])
+def test_backward_tiles_spread_split_equals_whole(gpu, name):
+    """DFWFM_BWD_TILES, then DFWFM_BWD_MLP_WEIGHTS on a second stream beside DFWFM_BWD_SPREAD (the one-GPU step's
+    fork) gives dfwfm_backward's gradients; SPREAD without a per-tile backward for the last forward is refused."""
+    import ctypes
+    from xsdeepfwfm_deprecated_amd import _lib
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    g0, _, o0 = _sparse_step(m, gpu, xi, xv, y, sparse=False)
+    g1, _, o1 = _sparse_step(m, gpu, xi, xv, y, sparse=False, split=True)
+    assert np.array_equal(o0, o1)
+    for k in g0:
+        sc = np.abs(g0[k]).max()
+        assert np.abs(g1[k] - g0[k]).max() <= G_TOL * sc + 1e-12, k
+    L, eng = _lib.lib(), m._sync_engine(gpu)
+    xi_d, xv_d = (torch.from_numpy(a).to(gpu) for a in (xi.reshape(len(xi), -1), xv))
+    out = torch.empty(len(xi), device=gpu)
+    eng.train_forward(xi_d, xv_d, out, 0.0, 0)
+    grads = _lib.dfwfm_grads(None, None, None, None, None, None, None, None)
+    rc = L.dfwfm_backward_phases(eng.handle, ctypes.c_void_p(out.data_ptr()), ctypes.byref(grads), _lib.BWD_SPREAD,
+                                 ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream))
+    torch.cuda.synchronize()
+    assert rc != 0  # every golden model gathers second-order embeddings (needs the per-tile backward)

@@ -81,12 +81,12 @@ def _dp_worker(rank, world, port, q):
         m.b.grad = flat[3:].view(2, 2)
         m._grad_flat = flat
         allreduce_grads(m)  # the single flat all-reduce
-        r1 = (m.a.grad.clone(), m.b.grad.clone())
+        r1 = (m.a.grad.numpy().copy(), m.b.grad.numpy().copy())  # by value: the worker may exit before the read
         m._grad_flat = None
         m.a.grad = torch.ones(3) * (rank + 1)
         m.b.grad = torch.ones(2, 2) * 10 * (rank + 1)
         allreduce_grads(m)  # the coalesced fallback
-        q.put((rank, r1, (m.a.grad.clone(), m.b.grad.clone())))
+        q.put((rank, r1, (m.a.grad.numpy().copy(), m.b.grad.numpy().copy())))
     finally:
         dist.destroy_process_group()
 
@@ -100,7 +100,8 @@ def test_dp_grad_allreduce_gloo_world2():
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in procs))
+    res = dict((r, tuple(tuple(torch.from_numpy(x) for x in ab) for ab in (a, b)))
+               for r, a, b in (q.get(timeout=120) for _ in procs))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0

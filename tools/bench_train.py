@@ -114,6 +114,7 @@ def main():
     t0.record()
     for i in range(a.steps):
         loss = step(i)
+    host = time.perf_counter() - wall0  # the host's enqueue time (ahead of the GPU if well under the step time)
     t1.record()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - wall0
@@ -127,6 +128,7 @@ def main():
            "value": round(world * B * a.steps / (ms / 1e3), 1), "unit": "samples/s", "n_gpus": world,
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms / a.steps, 4), "per_gpu_batch": B,
            "first_order": a.first_order, "dropout": not a.no_dropout, "wall_s": round(wall, 3),
+           "host_enqueue_us_per_step": round(host * 1e6 / a.steps, 1),
            "mode": a.mode, "inputs": "copied" if (a.copy_inputs or a.mode != "fused") else "resident (read in place)",
            "final_loss_sum": round(float(loss.item()), 4)}
     if trainer is not None and getattr(trainer, "sparse", False):

@@ -87,6 +87,7 @@ struct dfwfm_model {
   const int64_t* step_src;  // dfwfm_set_step_source
   bool trained;
   bool bwd_tables;  // the per-tile backward (sv_de) ran for the last dfwfm_train_forward
+  bool bwd_fused_red;  // ... with the dense shallow reductions fused in (per-tile partials written)
   bool tables_set;
   bool dense_set;
 };
@@ -760,6 +761,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
   m->trained = false;
   m->bwd_tables = false;
+  m->bwd_fused_red = false;
   int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
   if (rc != DFWFM_OK) return rc;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(DFWFM_ERR_INVALID_ARG, "dropout_p outside [0, 1)");
@@ -803,7 +805,10 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
 
 static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, int phases, void* stream) {
   if (!m || !g) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
-  if (phases & ~(DFWFM_BWD_TABLES | DFWFM_BWD_MLP_WEIGHTS)) return fail(DFWFM_ERR_INVALID_ARG, "unknown phase bits");
+  if (phases & ~(DFWFM_BWD_TABLES | DFWFM_BWD_MLP_WEIGHTS | DFWFM_BWD_TILES | DFWFM_BWD_SPREAD))
+    return fail(DFWFM_ERR_INVALID_ARG, "unknown phase bits");
+  // DFWFM_BWD_TABLES = the per-tile backward (TILES) + the reductions and the table scatter (SPREAD)
+  if (phases & DFWFM_BWD_TABLES) phases |= DFWFM_BWD_TILES | DFWFM_BWD_SPREAD;
   if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_backward needs a preceding dfwfm_train_forward");
   const int64_t batch = m->t_batch;
   if (batch == 0) return DFWFM_OK;
@@ -812,10 +817,12 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   const int F = m->F, D = m->D, num = m->num, H = m->H;
   const bool drop = H > 0 && m->t_drop > 0.f;
   hipError_t e;
-  bool fused_red = false;
+  if ((phases & DFWFM_BWD_SPREAD) && !(phases & DFWFM_BWD_TILES) && !m->bwd_tables && (m->flags & kNeedE))
+    return fail(DFWFM_ERR_STATE, "DFWFM_BWD_SPREAD needs the per-tile backward (DFWFM_BWD_TILES) first");
+  bool fused_red = (phases & DFWFM_BWD_TILES) ? false : m->bwd_fused_red;
 
   // 1. per-tile backward: dE and the G chain (no atomics)
-  if ((phases & DFWFM_BWD_TABLES) && (m->flags & kNeedE)) {
+  if ((phases & DFWFM_BWD_TILES) && (m->flags & kNeedE)) {
     BwdArgs a;
     memset(&a, 0, sizeof a);
     a.batch = batch;
@@ -875,10 +882,11 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     e = launch_backward(a, D, tpw > 0 ? tpw : 1, ng8 ? 8 : 4, lds, s);
     if (e != hipSuccess) return hip_fail(e, "backward launch");
     m->bwd_tables = true;
+    m->bwd_fused_red = fused_red;
   }
 
   // 2. dense shallow reductions: per 16-row tile, then summed over tiles
-  if (phases & DFWFM_BWD_TABLES) {
+  if (phases & DFWFM_BWD_SPREAD) {
     RedArgs r;
     memset(&r, 0, sizeof r);
     r.batch = batch;
@@ -911,7 +919,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   }
 
   // 3. categorical tables: privatised (LDS) tasks for small tables, atomic tasks for large ones
-  if ((phases & DFWFM_BWD_TABLES) && g->fields) {
+  if ((phases & DFWFM_BWD_SPREAD) && g->fields) {
     ScatterArgs priv, atom;
     memset(&priv, 0, sizeof priv);
     priv.D = D;
@@ -1011,8 +1019,9 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       per_split += d.nnb * d.nkb[l];
     }
     if (per_split > 0) {
-      // split the batch so the launch holds ~4 workgroups per CU, each over >= 128 rows
-      int64_t splits = (1024 + per_split - 1) / per_split;
+      // split the batch so the launch holds ~3 workgroups per CU (each over >= 128 rows): in the one-GPU step it
+      // runs beside the reductions, the scatter and the main Adam, which need CUs too (4 per CU: 7 % slower step)
+      int64_t splits = 768 / per_split;
       if (const char* ds = getenv("DFWFM_DW_SPLITS")) splits = atoi(ds);  // tuning only
       const int64_t max_splits = (batch + 127) / 128;
       if (splits > max_splits) splits = max_splits;
@@ -1064,19 +1073,19 @@ int dfwfm_adam_step(const dfwfm_adam_tensor* t, int32_t n, double lr, double bet
   };
   for (int i = 0; i < n; ++i) {
     if (!t[i].grad || t[i].numel <= 0) continue;  // torch skips parameters without a grad
-    const int64_t nb = (t[i].numel + 1023) / 1024;
+    const int64_t nb = (t[i].numel + kAdamBlock - 1) / kAdamBlock;
     if (nb > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "adam tensor %d too large", i);
     if (list.n == kAdamList || blocks + nb > 0x7fffffff) {
       int rc = flush();
       if (rc != DFWFM_OK) return rc;
     }
-    AdamTensor& a = list.t[list.n++];
+    AdamTensor& a = list.t[list.n];
     a.p = t[i].param;
     a.g = t[i].grad;
     a.m = t[i].exp_avg;
     a.v = t[i].exp_avg_sq;
     a.n = t[i].numel;
-    a.block0 = blocks;
+    list.block0[list.n++] = (int32_t)blocks;
     blocks += nb;
   }
   return flush();
@@ -1252,31 +1261,39 @@ int dfwfm_adam_step_dev(const dfwfm_adam_tensor* t, int32_t n, double lr, double
     if (t[i].grad && t[i].numel > 0 && (!t[i].param || !t[i].exp_avg || !t[i].exp_avg_sq))
       return fail(DFWFM_ERR_INVALID_ARG, "adam tensor %d: null state pointer", i);
   AdamDevState* st = reinterpret_cast<AdamDevState*>(state_dev);
-  hipError_t e = launch_adam_prep(st, lr, beta1, beta2, eps, weight_decay, (hipStream_t)stream);
-  if (e != hipSuccess) return hip_fail(e, "adam prep launch");
+  const AdamHyper h{lr, beta1, beta2, eps, weight_decay};
+  // the tensors' launches (<= kAdamList tensors each); the last one advances the device step counter (a list
+  // without tensors still advances it: one empty workgroup)
+  std::vector<int> keep;
+  for (int i = 0; i < n; ++i)
+    if (t[i].grad && t[i].numel > 0) keep.push_back(i);
   AdamList list;
   memset(&list, 0, sizeof list);
   int64_t blocks = 0;
-  for (int i = 0; i <= n; ++i) {
-    const bool last = i == n;
-    if (!last && (!t[i].grad || t[i].numel <= 0)) continue;
-    const int64_t nb = last ? 0 : (t[i].numel + 1023) / 1024;
-    if (nb > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "adam tensor %d too large", i);
+  for (size_t k = 0; k <= keep.size(); ++k) {
+    const bool last = k == keep.size();
+    const int64_t nb = last ? 0 : (t[keep[k]].numel + kAdamBlock - 1) / kAdamBlock;
+    if (nb > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "adam tensor %d too large", keep[k]);
     if (list.n > 0 && (last || list.n == kAdamList || blocks + nb > 0x7fffffff)) {
-      e = launch_adam_dev(list, (int)blocks, st, (hipStream_t)stream);
+      hipError_t e = launch_adam_dev(list, (int)blocks, st, h, last, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(e, "adam launch");
       list.n = 0;
       blocks = 0;
     }
     if (last) break;
-    AdamTensor& a = list.t[list.n++];
-    a.p = t[i].param;
-    a.g = t[i].grad;
-    a.m = t[i].exp_avg;
-    a.v = t[i].exp_avg_sq;
-    a.n = t[i].numel;
-    a.block0 = blocks;
+    const dfwfm_adam_tensor& x = t[keep[k]];
+    AdamTensor& a = list.t[list.n];
+    a.p = x.param;
+    a.g = x.grad;
+    a.m = x.exp_avg;
+    a.v = x.exp_avg_sq;
+    a.n = x.numel;
+    list.block0[list.n++] = (int32_t)blocks;
     blocks += nb;
+  }
+  if (keep.empty()) {
+    hipError_t e = launch_adam_dev(list, 1, st, h, true, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "adam launch");
   }
   return DFWFM_OK;
 }

@@ -310,11 +310,12 @@ struct AdamTensor {
   float* m;
   float* v;
   int64_t n;
-  int64_t block0;                // first workgroup of this tensor
 };
-constexpr int kAdamList = 40;    // tensors per Adam launch (the list is a kernel argument, < 4 KiB)
+constexpr int kAdamBlock = 4096;  // elements per Adam work unit (16 per thread: four float4 of each array in flight)
+constexpr int kAdamList = 84;    // tensors per Adam launch (the list is a kernel argument, < 4 KiB)
 struct AdamList {
   AdamTensor t[kAdamList];
+  int32_t block0[kAdamList];     // first workgroup of each tensor
   int32_t n;
 };
 
@@ -410,10 +411,18 @@ hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, 
 // device-side step: state = {int64 step; float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt}
 struct AdamDevState {
   int64_t step;
-  float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt, pad[3];
+  float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt;  // the last step's scalars (diagnostics)
+  int32_t ticket;                                       // workgroups done in the step's last launch
+  int32_t pad[2];
 };
-hipError_t launch_adam_prep(AdamDevState* st, double lr, double b1, double b2, double eps, double wd, hipStream_t s);
-hipError_t launch_adam_dev(const AdamList& list, int total_blocks, const AdamDevState* st, hipStream_t s);
+constexpr int kAdamGrid = 2048;  // workgroups of a device-counter Adam launch (8 per CU), walking the blocks
+struct AdamHyper {
+  double lr, b1, b2, eps, wd;
+};
+// one launch of a device-counter Adam step: every workgroup derives the scalars of step (counter + 1); with `bump`
+// (the step's last launch) the last workgroup to finish advances the counter
+hipError_t launch_adam_dev(const AdamList& list, int total_blocks, AdamDevState* st, const AdamHyper& h, bool bump,
+                           hipStream_t s);
 hipError_t launch_bce_grad(const float* z, const float* y, int64_t n, float denom, float* dz, float* loss_sum,
                            hipStream_t s);
 

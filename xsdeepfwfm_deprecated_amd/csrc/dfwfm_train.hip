@@ -811,15 +811,13 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 #endif
 constexpr int kDwRB = DFWFM_DW_RB;   // batch rows per staged chunk (one barrier pair per chunk)
 constexpr int kDwU = kDwRB * 16 / 256;
-__global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
-  // row stride 80 = 16 mod 64 banks: the four 16-lane row groups of an MFMA fragment read hit
-  // disjoint banks (68 overlapped them ~2.3-way)
-  __shared__ __attribute__((aligned(16))) float gs[kDwRB][64 + 16];
-  __shared__ __attribute__((aligned(16))) float xs[kDwRB][64 + 16];
+// row stride 80 = 16 mod 64 banks: the four 16-lane row groups of an MFMA fragment read hit disjoint banks (68
+// overlapped them ~2.3-way)
+typedef float DwTile[kDwRB][64 + 16];
+__device__ __forceinline__ void dw_block(const DwArgs& a, int bid, DwTile& gs, DwTile& xs) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  int bid = blockIdx.x;
   int l = 1;
   while (l < a.H && bid >= a.blk0[l + 1]) ++l;
   bid -= a.blk0[l];
@@ -920,6 +918,11 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
+  __shared__ __attribute__((aligned(16))) DwTile gs, xs;
+  dw_block(a, blockIdx.x, gs, xs);
+}
+
 // ---------------------------------------------------------------------------
 // Adam (torch.optim.Adam, single-tensor form, torch/optim/adam.py _single_tensor_adam):
 // g += wd * p; m = lerp(m, g, 1 - b1);
@@ -939,77 +942,113 @@ __device__ __forceinline__ void adam_elem(const AdamCoef& c, float& p, float g, 
   p = __fadd_rn(p, __fdiv_rn(__fmul_rn(-c.step_size, m), denom));  // addcdiv_(m, denom, -lr/bc1)
 }
 
-// a block's 1024 elements: when the tensor's four arrays are 16-byte aligned thread t owns [4t, 4t+4) -- one
-// 16-byte load of each of p, g, m, v and three 16-byte stores, every load in flight at once -- else the
-// lanes take consecutive elements
-__device__ __forceinline__ void adam_block(const AdamList& list, const AdamCoef& c) {
+// a block's kAdamBlock (4096) elements: when the tensor's four arrays are 16-byte aligned thread t owns the four
+// float4 [4t + 1024u, 4t + 1024u + 4), u < 4 -- all sixteen 16-byte loads issued before any update (bytes in flight
+// for HBM), three 16-byte stores each -- else the lanes take consecutive elements
+template <typename TList>
+__device__ __forceinline__ void adam_block(const TList& list, const AdamCoef& c, int bid) {
+  if (list.n <= 0) return;
   int lo = 0, hi = list.n - 1;
-  const int bid = blockIdx.x;
   while (lo < hi) {  // last tensor whose block0 <= bid
     const int mid = (lo + hi + 1) >> 1;
-    if (list.t[mid].block0 <= bid) lo = mid;
+    if (list.block0[mid] <= bid) lo = mid;
     else hi = mid - 1;
   }
   const AdamTensor T = list.t[lo];
-  const int64_t i0 = (int64_t)(bid - T.block0) * 1024;
-  const int64_t i = i0 + 4 * threadIdx.x;
+  const int64_t i0 = (int64_t)(bid - list.block0[lo]) * kAdamBlock;
   const bool vec = (((uintptr_t)T.p | (uintptr_t)T.g | (uintptr_t)T.m | (uintptr_t)T.v) & 15) == 0;
   if (!vec) {
     // unaligned arrays (a gradient view at an odd offset of the flat buffer): lane-consecutive elements
-    for (int64_t j = i0 + threadIdx.x; j < i0 + 1024 && j < T.n; j += 256) {
+    for (int64_t j = i0 + threadIdx.x; j < i0 + kAdamBlock && j < T.n; j += 256) {
       float p = T.p[j], m = T.m[j], v = T.v[j];
       adam_elem(c, p, T.g[j], m, v);
       T.m[j] = m;
       T.v[j] = v;
       T.p[j] = p;
     }
-  } else if (i + 3 < T.n) {
-    float4 p = *reinterpret_cast<const float4*>(T.p + i);
-    const float4 g = *reinterpret_cast<const float4*>(T.g + i);
-    float4 m = *reinterpret_cast<const float4*>(T.m + i);
-    float4 v = *reinterpret_cast<const float4*>(T.v + i);
-    adam_elem(c, p.x, g.x, m.x, v.x);
-    adam_elem(c, p.y, g.y, m.y, v.y);
-    adam_elem(c, p.z, g.z, m.z, v.z);
-    adam_elem(c, p.w, g.w, m.w, v.w);
-    *reinterpret_cast<float4*>(T.m + i) = m;
-    *reinterpret_cast<float4*>(T.v + i) = v;
-    *reinterpret_cast<float4*>(T.p + i) = p;
-  } else {
-    for (int k = 0; k < 4; ++k) {
-      if (i + k >= T.n) break;
-      float p = T.p[i + k], m = T.m[i + k], v = T.v[i + k];
-      adam_elem(c, p, T.g[i + k], m, v);
-      T.m[i + k] = m;
-      T.v[i + k] = v;
-      T.p[i + k] = p;
+    return;
+  }
+  constexpr int U = kAdamBlock / 1024;
+  float4 p[U], g[U], m[U], v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = i0 + 1024 * u + 4 * threadIdx.x;
+    if (i + 3 < T.n) {
+      p[u] = *reinterpret_cast<const float4*>(T.p + i);
+      g[u] = *reinterpret_cast<const float4*>(T.g + i);
+      m[u] = *reinterpret_cast<const float4*>(T.m + i);
+      v[u] = *reinterpret_cast<const float4*>(T.v + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = i0 + 1024 * u + 4 * threadIdx.x;
+    if (i + 3 < T.n) {
+      adam_elem(c, p[u].x, g[u].x, m[u].x, v[u].x);
+      adam_elem(c, p[u].y, g[u].y, m[u].y, v[u].y);
+      adam_elem(c, p[u].z, g[u].z, m[u].z, v[u].z);
+      adam_elem(c, p[u].w, g[u].w, m[u].w, v[u].w);
+      *reinterpret_cast<float4*>(T.m + i) = m[u];
+      *reinterpret_cast<float4*>(T.v + i) = v[u];
+      *reinterpret_cast<float4*>(T.p + i) = p[u];
+    } else {
+      for (int k = 0; k < 4; ++k) {
+        if (i + k >= T.n) break;
+        float pp = T.p[i + k], mm = T.m[i + k], vv = T.v[i + k];
+        adam_elem(c, pp, T.g[i + k], mm, vv);
+        T.m[i + k] = mm;
+        T.v[i + k] = vv;
+        T.p[i + k] = pp;
+      }
     }
   }
 }
 
 __global__ void __launch_bounds__(256) adam_kernel(const AdamList list, float step_size, float omb1, float b2,
                                                    float omb2, float eps, float wd, float bc2_sqrt) {
-  adam_block(list, AdamCoef{step_size, omb1, b2, omb2, eps, wd, bc2_sqrt});
+  adam_block(list, AdamCoef{step_size, omb1, b2, omb2, eps, wd, bc2_sqrt}, blockIdx.x);
 }
 
-// Graph-replayable Adam: one thread bumps the device step and derives the step's scalars in double
-// (as torch does from Python floats), the update kernels read them from device memory.
-__global__ void adam_prep_kernel(AdamDevState* st, double lr, double b1, double b2, double eps, double wd) {
-  const int64_t step = st->step + 1;
-  st->step = step;
-  const double bc1 = 1.0 - pow(b1, (double)step);
-  const double bc2 = 1.0 - pow(b2, (double)step);
-  st->step_size = (float)(lr / bc1);
-  st->omb1 = (float)(1.0 - b1);
-  st->b2 = (float)b2;
-  st->omb2 = (float)(1.0 - b2);
-  st->eps = (float)eps;
-  st->wd = (float)wd;
-  st->bc2_sqrt = (float)sqrt(bc2);
+// Graph-replayable Adam: every workgroup derives the step's scalars from the device counter + 1 (in double, as
+// torch does from Python floats, then f32) -- no separate prep launch; in the step's last launch the last workgroup
+// to finish (a ticket counter) advances the counter, after every workgroup of the step has read it.
+__device__ __forceinline__ AdamCoef adam_coef(int64_t step, const AdamHyper& h) {
+  const double bc1 = 1.0 - pow(h.b1, (double)step);
+  const double bc2 = 1.0 - pow(h.b2, (double)step);
+  return AdamCoef{(float)(h.lr / bc1), (float)(1.0 - h.b1), (float)h.b2, (float)(1.0 - h.b2), (float)h.eps,
+                  (float)h.wd, (float)sqrt(bc2)};
 }
 
-__global__ void __launch_bounds__(256) adam_dev_kernel(const AdamList list, const AdamDevState* __restrict__ st) {
-  adam_block(list, AdamCoef{st->step_size, st->omb1, st->b2, st->omb2, st->eps, st->wd, st->bc2_sqrt});
+// (a bounded grid walking the 1024-element blocks: one ticket atomic per workgroup, a few thousand at most -- one
+// per block serialised on the counter's address)
+template <typename TList>
+__device__ __forceinline__ void adam_dev_part(const TList& list, AdamDevState* __restrict__ st, const AdamHyper& h,
+                                              int bump, int nblocks, int wg, int nwg) {
+  __shared__ AdamCoef sc;
+  __shared__ int64_t s_step;
+  if (threadIdx.x == 0) {
+    s_step = st->step + 1;
+    sc = adam_coef(s_step, h);
+  }
+  __syncthreads();
+  for (int b = wg; b < nblocks; b += nwg) adam_block(list, sc, b);
+  if (bump && threadIdx.x == 0 && atomicAdd(&st->ticket, 1) == nwg - 1) {
+    const AdamCoef c = sc;
+    st->step_size = c.step_size;
+    st->omb1 = c.omb1;
+    st->b2 = c.b2;
+    st->omb2 = c.omb2;
+    st->eps = c.eps;
+    st->wd = c.wd;
+    st->bc2_sqrt = c.bc2_sqrt;
+    st->ticket = 0;
+    st->step = s_step;
+  }
+}
+
+__global__ void __launch_bounds__(256) adam_dev_kernel(const AdamList list, AdamDevState* __restrict__ st,
+                                                       const AdamHyper h, int bump, int nblocks) {
+  adam_dev_part(list, st, h, bump, nblocks, blockIdx.x, gridDim.x);
 }
 
 // dL/dz of BCE-with-logits with the loss normalised by `denom` (torch: (sigmoid(z) - y) * 1, then
@@ -1155,14 +1194,11 @@ hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, 
   return hipGetLastError();
 }
 
-hipError_t launch_adam_prep(AdamDevState* st, double lr, double b1, double b2, double eps, double wd, hipStream_t s) {
-  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, s, st, lr, b1, b2, eps, wd);
-  return hipGetLastError();
-}
-
-hipError_t launch_adam_dev(const AdamList& list, int total_blocks, const AdamDevState* st, hipStream_t s) {
+hipError_t launch_adam_dev(const AdamList& list, int total_blocks, AdamDevState* st, const AdamHyper& h, bool bump,
+                           hipStream_t s) {
   if (total_blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(adam_dev_kernel, dim3(total_blocks), dim3(256), 0, s, list, st);
+  const int grid = total_blocks < kAdamGrid ? total_blocks : kAdamGrid;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid), dim3(256), 0, s, list, st, h, bump ? 1 : 0, total_blocks);
   return hipGetLastError();
 }
 

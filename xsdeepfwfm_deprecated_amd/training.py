@@ -353,6 +353,11 @@ class FusedTrainStep:
         if self.sparse:
             self._sparse_lists(st)
 
+    def _backward_phase(self, phases):
+        _lib.check(self.L.dfwfm_backward_phases(self.eng.handle, ctypes.c_void_p(self.dlogit.data_ptr()),
+                                                ctypes.byref(self.grads), phases, self._stream()),
+                   "dfwfm_backward_phases")
+
     def _part1b(self):
         """The MLP weight gradients (dW_l, db_l): the backward's second part under data parallelism."""
         _lib.check(self.L.dfwfm_backward_phases(self.eng.handle, ctypes.c_void_p(self.dlogit.data_ptr()),
@@ -459,16 +464,29 @@ class FusedTrainStep:
         g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         ga = None
         if self.dist is None and self.n_adam > self.n_main:
-            # one process: a single graph that forks after the backward's first part -- the weight-gradient
-            # GEMM and the MLP's Adam on a side stream, the other tensors' Adam (the 58 MB of tables) beside it
+            # one process: a single graph that forks after the per-tile backward -- the weight-gradient GEMM
+            # and the MLP's Adam on a side stream; the reductions, the table scatter and the other tensors' Adam
+            # (the 58 MB of tables) beside them
+            # (A/B only, DFWFM_TRAIN_FORK: spread = fork after the scatter, none = one stream)
+            fork = os.environ.get("DFWFM_TRAIN_FORK", "tiles")
+            if fork == "none":
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g1, stream=s):
+                        self._part1(self.B, denom)
+                        self._part2()
+                torch.cuda.current_stream(self.dev).wait_stream(s)
+                return g1, None, None, None, None
+            late = fork == "spread"
             s1 = torch.cuda.Stream(self.dev)
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g1, stream=s):
-                    self._part1(self.B, denom, phases=_lib.BWD_TABLES)
+                    self._part1(self.B, denom, phases=_lib.BWD_TABLES if late else _lib.BWD_TILES)
                     s1.wait_stream(s)
                     with torch.cuda.stream(s1):
                         self._part1b()
                         self._adam_mlp()
+                    if not late:
+                        self._backward_phase(_lib.BWD_SPREAD)
                     self._adam_main()
                     s.wait_stream(s1)
             torch.cuda.current_stream(self.dev).wait_stream(s)
