@@ -7,6 +7,9 @@
 //   1  five lanes per row, one dwordx2 each (12 rows per instruction, 60 lanes busy)
 //   2  ten lanes per row, one dword each (6 rows per instruction)
 //   3  one lane per row, two 16-B aligned dwordx4 + one dwordx2 placed by the row's alignment (3 loads per row)
+//   4  one lane per row of a PACKED copy: rows at a 16-float (64-B) stride, 64-B aligned -- every row one line,
+//      two dwordx4 + one dwordx2
+// argv: [NB batches in flight] [table scale K: every table K x as many rows, e.g. 8 -> 424 MB, HBM-resident]
 // TILES: 16-sample tiles per workgroup (walked with the next tile's loads issued before this tile's
 // LDS stores: TILES > 1 is the persistent form).  Reports microseconds per 4096-sample batch with
 // NB batches in flight (one launch over NB batches, as NB streams would).
@@ -23,6 +26,7 @@ constexpr int F = 26, D = 10, BM = 16, NTH = 512;
 
 struct Args {
   const float* const* tabs;  // [F] table bases
+  const float* const* ptabs; // [F] packed (16-float stride) table bases
   const int64_t* xi;         // [NB*B][F]
   float* out;                // [NB*B]
   int64_t total;             // samples
@@ -53,6 +57,18 @@ __device__ __forceinline__ void tile_loads(const Args& a, int64_t b0, int tid, f
       v1[0] = al ? x0.x : c.x; v1[1] = al ? x0.y : c.y; v1[2] = al ? x0.z : x0.x; v1[3] = al ? x0.w : x0.y;
       v1[4] = al ? x1.x : x0.z; v1[5] = al ? x1.y : x0.w; v1[6] = al ? x1.z : x1.x; v1[7] = al ? x1.w : x1.y;
       v1[8] = al ? c.x : x1.z; v1[9] = al ? c.y : x1.w;
+    }
+  } else if constexpr (V == 4) {
+    const int r = tid;
+    if (r < F * BM) {
+      const int f = r >> 4;
+      const int64_t idx = a.xi[(b0 + (r & 15)) * F + f];
+      const float* src = a.ptabs[f] + idx * 16;
+      const float4 x0 = reinterpret_cast<const float4*>(src)[0], x1 = reinterpret_cast<const float4*>(src)[1];
+      const float2 c = reinterpret_cast<const float2*>(src)[4];
+      v1[0] = x0.x; v1[1] = x0.y; v1[2] = x0.z; v1[3] = x0.w;
+      v1[4] = x1.x; v1[5] = x1.y; v1[6] = x1.z; v1[7] = x1.w;
+      v1[8] = c.x; v1[9] = c.y;
     }
   } else if constexpr (V == 1) {
     const int w = tid >> 6, lane = tid & 63;
@@ -90,7 +106,7 @@ __device__ __forceinline__ void tile_stores(float* E, int tid, const float2 (&v2
 #pragma unroll
       for (int j = 0; j < 5; ++j) dst[j] = v2[j];
     }
-  } else if constexpr (V == 3) {
+  } else if constexpr (V == 3 || V == 4) {
     const int r = tid;
     if (r < F * BM) {
       float2* dst = reinterpret_cast<float2*>(E + (r & 15) * (F * D + 2) + (r >> 4) * D);
@@ -147,8 +163,10 @@ static const int64_t kSizes[F] = {1458, 556, 245197, 166166, 306, 20, 12055, 634
 int main(int argc, char** argv) {
   const int B = 4096;
   const int NB = argc > 1 ? atoi(argv[1]) : 3;
+  const int K = argc > 2 ? atoi(argv[2]) : 1;
   const int reps = 200;
   std::vector<int64_t> n(kSizes, kSizes + F);
+  for (auto& x : n) x *= K;
   int64_t rows = 0;
   for (int f = 0; f < F; ++f) rows += n[f];
   float* tab;
@@ -160,6 +178,16 @@ int main(int argc, char** argv) {
   const float** dtabs;
   CHECK(hipMalloc(&dtabs, F * sizeof(float*)));
   CHECK(hipMemcpy(dtabs, hb.data(), F * sizeof(float*), hipMemcpyHostToDevice));
+  float* ptab;
+  CHECK(hipMalloc(&ptab, rows * 16 * 4));
+  CHECK(hipMemset(ptab, 0, rows * 16 * 4));
+  std::vector<const float*> hp(F);
+  off = 0;
+  for (int f = 0; f < F; ++f) { hp[f] = ptab + off * 16; off += n[f]; }
+  const float** dptabs;
+  CHECK(hipMalloc(&dptabs, F * sizeof(float*)));
+  CHECK(hipMemcpy(dptabs, hp.data(), F * sizeof(float*), hipMemcpyHostToDevice));
+  printf("tables x%d: %.0f MB of 40-B rows, %.0f MB packed\n", K, rows * D * 4 / 1e6, rows * 64 / 1e6);
   const int64_t total = (int64_t)NB * B;
   std::vector<int64_t> hx(total * F);
   uint64_t s = 88172645463325252ull;
@@ -170,7 +198,7 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&dx, hx.size() * 8));
   CHECK(hipMemcpy(dx, hx.data(), hx.size() * 8, hipMemcpyHostToDevice));
   CHECK(hipMalloc(&dout, total * 4));
-  Args a{dtabs, dx, dout, total};
+  Args a{dtabs, dptabs, dx, dout, total};
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -189,6 +217,7 @@ int main(int argc, char** argv) {
            tiles, grid, us_batch, alg / (us_batch * 1e-6) / 1e12);
   };
   run(gather_kernel<0, 1>, 1, "lane per row (5 x dwordx2)");
+  run(gather_kernel<4, 1>, 1, "packed 64-B rows (2 x4 + x2)");
   run(gather_kernel<3, 1>, 1, "lane per row (2 x4 + 1 x2)");
   run(gather_kernel<1, 1>, 1, "5 lanes per row (dwordx2)");
   run(gather_kernel<2, 1>, 1, "10 lanes per row (dword)");
