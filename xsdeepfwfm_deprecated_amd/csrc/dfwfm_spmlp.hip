@@ -12,8 +12,9 @@
 //                      (dfwfm_model_build_sparse_mlp), not per forward;
 //   sparse_mlp_kernel  64 samples per workgroup (lane = sample), the E tile of the gather launch
 //                      (fwd_kernel PART = 1) transposed into LDS as x[k][64]; eight waves own neuron
-//                      groups g = wave + 8i, a group's pairs come in as scalar loads (wave-uniform, 32 per
-//                      step: eight entries of four neurons, so 32 LDS reads are in flight per wait), and a
+//                      groups g = wave + 8i, a group's entries staged through the wave's LDS slot (loaded
+//                      one unit ahead, read back as broadcasts: 32 pairs per step, all LDS reads in flight
+//                      before the FMAs), and a
 //                      pair costs one LDS read of x[k][lane] plus one FMA -- 47.6 k FMAs per sample at
 //                      Criteo-39 / 90 % instead of the dense 476 k; a layer's outputs stay in registers
 //                      until every wave has finished reading x, then overwrite it in place; net_1_fc and
@@ -29,8 +30,9 @@
 namespace dfwfm {
 
 namespace {
-constexpr int kSpS = 64;  // samples per workgroup (lane = sample)
-constexpr int kSpW = 8;   // waves per workgroup
+constexpr int kSpS = 64;   // samples per workgroup (lane = sample)
+constexpr int kSpW = 8;    // waves per workgroup
+constexpr int kSpCap = 64;  // ELL entries (of four neurons) a wave stages in LDS at once
 }  // namespace
 
 // one wave per group of four neurons 4g..4g+3: each row's nonzeros compacted in k order (ballot + mbcnt),
@@ -130,75 +132,104 @@ sparse_mlp_kernel(const SpMlpArgs p) {
   __syncthreads();
 
   float dpart = 0.f;
+  // each wave's ELL entries come through its own LDS slot: a unit (group g, entries [j0, j0 + n), n <= kSpCap)
+  // is loaded into registers (every lane 16 bytes, coalesced) while the previous unit is processed, then stored to
+  // the slot, where the walk reads it with broadcast LDS reads -- no global-memory round trip inside the walk
+  int4* eslot = reinterpret_cast<int4*>(red + kSpW * kSpS) + wave * (2 * kSpCap);
+  constexpr int kRegs = 2 * kSpCap / 64;  // int4 per lane per unit
   for (int h = 0; h < p.H; ++h) {
-    const int2* ell = p.ell + p.off[h];
-    const int W4 = p.W[h] * 4;
+    const int4* ell = reinterpret_cast<const int4*>(p.ell + p.off[h]);
+    const int64_t W2 = (int64_t)p.W[h] * 2;  // int4 per group slot (W entries x 4 neurons x 8 bytes)
     const int* gcnt = p.gcnt + h * G;
     const float* bh = p.mlp_b + h * p.NT * 16;
     const bool last = h == p.H - 1;
     float acc[NGW][4];
 #pragma unroll
-    for (int i = 0; i < NGW; ++i) {
-      const int g = wave + kSpW * i;
+    for (int i = 0; i < NGW; ++i)
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[i][u] = 0.f;
-      if (g < G) {
-        // four neurons at once: eight entries of each per step (32 scalar pairs), 32 LDS reads in flight
-        float a[4];
+    // units of this wave: groups g = wave + kSpW i, each in chunks of kSpCap entries
+    int ui = 0, uj = 0;  // next unit to load: group index i, first entry
+    auto unit_n = [&](int i, int j) -> int {
+      const int g = wave + kSpW * i;
+      if (i >= NGW || g >= G) return -1;
+      const int c = gcnt[g];
+      return c - j < kSpCap ? c - j : kSpCap;
+    };
+    int4 rq[kRegs];
+    auto load_unit = [&](int i, int j, int n) {
+      const int4* src = ell + (int64_t)(wave + kSpW * i) * W2 + 2 * j;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) a[u] = bh[4 * g + u];  // padded biases: zero past N
-        // entries as vector loads (every lane the same 16 bytes: {k, k', w, w'} of a neuron pair), the next
-        // step's in flight while this step's LDS reads and FMAs run -- scalar loads of these lists miss the
-        // scalar cache (1.3 MB per layer) and serialised the loop on their latency
-        int vz = 0;
-        asm volatile("" : "+v"(vz));  // a VGPR offset: keeps these loads on the vector path (uniform
-                                      // addresses would otherwise become scalar loads)
-        const int4* e = reinterpret_cast<const int4*>(ell + (int64_t)g * W4) + vz;
-        const int c = gcnt[g];
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
-        f32x2 a01 = {a[0], a[1]}, a23 = {a[2], a[3]};
-        auto step = [&](const int4 (&q)[2 * kEllPad]) {
-          f32x2 xv[2 * kEllPad];
+      for (int r = 0; r < kRegs; ++r) {
+        const int q = lane + 64 * r;
+        if (q < 2 * n) rq[r] = src[q];
+      }
+    };
+    int cur_n = unit_n(0, 0);
+    if (cur_n >= 0) load_unit(0, 0, cur_n);
+    int ci = 0, cj = 0;  // unit being processed
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+    if (cur_n >= 0) {
+      const int g0 = wave;
+      a01 = f32x2{bh[4 * g0], bh[4 * g0 + 1]};  // padded biases: zero past N
+      a23 = f32x2{bh[4 * g0 + 2], bh[4 * g0 + 3]};
+    }
+    while (cur_n >= 0) {
+      // the unit's entries -> this wave's slot (the previous unit's broadcast reads retired in order)
 #pragma unroll
-          for (int t = 0; t < 2 * kEllPad; ++t)
-            xv[t] = f32x2{x[q[t].x * kSpS + lane], x[q[t].y * kSpS + lane]};
+      for (int r = 0; r < kRegs; ++r) {
+        const int q = lane + 64 * r;
+        if (q < 2 * cur_n) eslot[q] = rq[r];
+      }
+      // the following unit's loads go out now
+      int ni = ci, nj = cj + cur_n;
+      int nn = nj < gcnt[wave + kSpW * ci] ? unit_n(ni, nj) : -1;
+      if (nn < 0) {
+        ni = ci + 1;
+        nj = 0;
+        nn = unit_n(ni, 0);
+      }
+      if (nn >= 0) load_unit(ni, nj, nn);
+      // walk: eight entries (32 pairs) per step, every LDS read of the step in flight before its FMAs
+      for (int j = 0; j < cur_n; j += 8) {
+        int4 q[16];
 #pragma unroll
-          for (int t = 0; t < 2 * kEllPad; ++t) {
-            const f32x2 w = {__int_as_float(q[t].z), __int_as_float(q[t].w)};
-            if (t & 1) a23 = __builtin_elementwise_fma(w, xv[t], a23);
-            else a01 = __builtin_elementwise_fma(w, xv[t], a01);
-          }
-        };
-        int4 qa[2 * kEllPad], qb[2 * kEllPad];
-        if (c > 0) {
+        for (int t = 0; t < 16; ++t) q[t] = eslot[2 * j + t];
+        f32x2 xv[16];
 #pragma unroll
-          for (int t = 0; t < 2 * kEllPad; ++t) qa[t] = e[t];
-        }
-        for (int j = 0; j < c; j += 2 * kEllPad) {
-          if (j + kEllPad < c) {
+        for (int t = 0; t < 16; ++t) xv[t] = f32x2{x[q[t].x * kSpS + lane], x[q[t].y * kSpS + lane]};
 #pragma unroll
-            for (int t = 0; t < 2 * kEllPad; ++t) qb[t] = e[2 * (j + kEllPad) + t];
-          }
-          step(qa);
-          if (j + kEllPad >= c) break;
-          if (j + 2 * kEllPad < c) {
-#pragma unroll
-            for (int t = 0; t < 2 * kEllPad; ++t) qa[t] = e[2 * (j + 2 * kEllPad) + t];
-          }
-          step(qb);
-        }
-        a[0] = a01.x;
-        a[1] = a01.y;
-        a[2] = a23.x;
-        a[3] = a23.y;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int n = 4 * g + u;
-          const float r = a[u] < 0.f ? 0.f : a[u];  // ReLU (NaN kept, as relu_keep_nan)
-          acc[i][u] = n < N ? r : 0.f;
-          if (last && n < N) dpart = fmaf(r, p.fc[n], dpart);
+        for (int t = 0; t < 16; ++t) {
+          const f32x2 w = {__int_as_float(q[t].z), __int_as_float(q[t].w)};
+          if (t & 1) a23 = __builtin_elementwise_fma(w, xv[t], a23);
+          else a01 = __builtin_elementwise_fma(w, xv[t], a01);
         }
       }
+      if (ni != ci) {
+        // group done: ReLU, the last layer's net_1_fc, the register copy for the in-place overwrite
+        const int g = wave + kSpW * ci;
+        const float av[4] = {a01.x, a01.y, a23.x, a23.y};
+#pragma unroll
+        for (int i = 0; i < NGW; ++i)
+          if (i == ci) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int n = 4 * g + u;
+              const float r = av[u] < 0.f ? 0.f : av[u];  // ReLU (NaN kept, as relu_keep_nan)
+              acc[i][u] = n < N ? r : 0.f;
+              if (last && n < N) dpart = fmaf(r, p.fc[n], dpart);
+            }
+          }
+        if (nn >= 0) {
+          const int g2 = wave + kSpW * ni;
+          a01 = f32x2{bh[4 * g2], bh[4 * g2 + 1]};
+          a23 = f32x2{bh[4 * g2 + 2], bh[4 * g2 + 3]};
+        }
+      }
+      ci = ni;
+      cj = nj;
+      cur_n = nn;
     }
     if (!last) {
       __syncthreads();  // every wave has finished reading this layer's input
@@ -230,7 +261,7 @@ hipError_t launch_ell_build(const EllArgs& a, int rows, hipStream_t s) {  // row
 
 size_t sparse_mlp_lds_bytes(int K0p, int N) {
   const int XK = K0p > N ? K0p : N;
-  return sizeof(float) * ((size_t)XK * kSpS + kSpW * kSpS);
+  return sizeof(float) * ((size_t)XK * kSpS + kSpW * kSpS) + sizeof(int4) * 2 * kSpCap * kSpW;
 }
 
 template <int NGW>
