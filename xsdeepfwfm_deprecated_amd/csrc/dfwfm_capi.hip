@@ -805,10 +805,12 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
 
 static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, int phases, void* stream) {
   if (!m || !g) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
-  if (phases & ~(DFWFM_BWD_TABLES | DFWFM_BWD_MLP_WEIGHTS | DFWFM_BWD_TILES | DFWFM_BWD_SPREAD))
+  if (phases & ~(DFWFM_BWD_TABLES | DFWFM_BWD_MLP_WEIGHTS | DFWFM_BWD_TILES | DFWFM_BWD_SPREAD | DFWFM_BWD_REDUCE |
+                 DFWFM_BWD_SCATTER))
     return fail(DFWFM_ERR_INVALID_ARG, "unknown phase bits");
-  // DFWFM_BWD_TABLES = the per-tile backward (TILES) + the reductions and the table scatter (SPREAD)
+  // DFWFM_BWD_TABLES = the per-tile backward (TILES) + the reductions (REDUCE) and the table scatter (SCATTER)
   if (phases & DFWFM_BWD_TABLES) phases |= DFWFM_BWD_TILES | DFWFM_BWD_SPREAD;
+  if (phases & DFWFM_BWD_SPREAD) phases |= DFWFM_BWD_REDUCE | DFWFM_BWD_SCATTER;
   if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_backward needs a preceding dfwfm_train_forward");
   const int64_t batch = m->t_batch;
   if (batch == 0) return DFWFM_OK;
@@ -817,7 +819,8 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   const int F = m->F, D = m->D, num = m->num, H = m->H;
   const bool drop = H > 0 && m->t_drop > 0.f;
   hipError_t e;
-  if ((phases & DFWFM_BWD_SPREAD) && !(phases & DFWFM_BWD_TILES) && !m->bwd_tables && (m->flags & kNeedE))
+  if ((phases & (DFWFM_BWD_REDUCE | DFWFM_BWD_SCATTER)) && !(phases & DFWFM_BWD_TILES) && !m->bwd_tables &&
+      (m->flags & kNeedE))
     return fail(DFWFM_ERR_STATE, "DFWFM_BWD_SPREAD needs the per-tile backward (DFWFM_BWD_TILES) first");
   bool fused_red = (phases & DFWFM_BWD_TILES) ? false : m->bwd_fused_red;
 
@@ -886,7 +889,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   }
 
   // 2. dense shallow reductions: per 16-row tile, then summed over tiles
-  if (phases & DFWFM_BWD_SPREAD) {
+  if (phases & DFWFM_BWD_REDUCE) {
     RedArgs r;
     memset(&r, 0, sizeof r);
     r.batch = batch;
@@ -919,7 +922,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   }
 
   // 3. categorical tables: privatised (LDS) tasks for small tables, atomic tasks for large ones
-  if ((phases & DFWFM_BWD_SPREAD) && g->fields) {
+  if ((phases & DFWFM_BWD_SCATTER) && g->fields) {
     ScatterArgs priv, atom;
     memset(&priv, 0, sizeof priv);
     priv.D = D;

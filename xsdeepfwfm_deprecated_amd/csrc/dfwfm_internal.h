@@ -283,6 +283,7 @@ struct SpMlpArgs {
   float* out;
   int64_t batch;
   int32_t H, N, NT;
+  int32_t ecap;            // ELL entries per LDS staging unit (set by the launcher)
 };
 hipError_t launch_ell_build(const EllArgs& a, int rows, hipStream_t s);
 hipError_t launch_sparse_mlp(const SpMlpArgs& a, hipStream_t s);

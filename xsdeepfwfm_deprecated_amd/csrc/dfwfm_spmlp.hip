@@ -135,8 +135,9 @@ sparse_mlp_kernel(const SpMlpArgs p) {
   // each wave's ELL entries come through its own LDS slot: a unit (group g, entries [j0, j0 + n), n <= kSpCap)
   // is loaded into registers (every lane 16 bytes, coalesced) while the previous unit is processed, then stored to
   // the slot, where the walk reads it with broadcast LDS reads -- no global-memory round trip inside the walk
-  int4* eslot = reinterpret_cast<int4*>(red + kSpW * kSpS) + wave * (2 * kSpCap);
-  constexpr int kRegs = 2 * kSpCap / 64;  // int4 per lane per unit
+  const int cap = p.ecap;  // entries per unit (<= kSpCap)
+  int4* eslot = reinterpret_cast<int4*>(red + kSpW * kSpS) + wave * (2 * cap);
+  constexpr int kRegs = 2 * kSpCap / 64;  // int4 per lane per unit (at most)
   for (int h = 0; h < p.H; ++h) {
     const int4* ell = reinterpret_cast<const int4*>(p.ell + p.off[h]);
     const int64_t W2 = (int64_t)p.W[h] * 2;  // int4 per group slot (W entries x 4 neurons x 8 bytes)
@@ -154,7 +155,7 @@ sparse_mlp_kernel(const SpMlpArgs p) {
       const int g = wave + kSpW * i;
       if (i >= NGW || g >= G) return -1;
       const int c = gcnt[g];
-      return c - j < kSpCap ? c - j : kSpCap;
+      return c - j < cap ? c - j : cap;
     };
     int4 rq[kRegs];
     auto load_unit = [&](int i, int j, int n) {
@@ -259,13 +260,26 @@ hipError_t launch_ell_build(const EllArgs& a, int rows, hipStream_t s) {  // row
   return hipGetLastError();
 }
 
+// ELL entries per staging unit: kSpCap, or what the LDS left by the x tile holds (multiple of 8; 0: no room)
+static int sparse_mlp_cap(int K0p, int N) {
+  const int XK = K0p > N ? K0p : N;
+  const int64_t base = (int64_t)sizeof(float) * ((int64_t)XK * kSpS + kSpW * kSpS);
+  const int64_t room = (160 * 1024 - base) / (int64_t)(sizeof(int4) * 2 * kSpW);
+  const int64_t cap = room < kSpCap ? room / 8 * 8 : kSpCap;
+  return cap > 0 ? (int)cap : 0;
+}
+
 size_t sparse_mlp_lds_bytes(int K0p, int N) {
   const int XK = K0p > N ? K0p : N;
-  return sizeof(float) * ((size_t)XK * kSpS + kSpW * kSpS) + sizeof(int4) * 2 * kSpCap * kSpW;
+  const int cap = sparse_mlp_cap(K0p, N);
+  if (cap == 0) return (size_t)-1;  // does not fit
+  return sizeof(float) * ((size_t)XK * kSpS + kSpW * kSpS) + sizeof(int4) * 2 * (size_t)cap * kSpW;
 }
 
 template <int NGW>
-static hipError_t launch_sp_t(const SpMlpArgs& a, hipStream_t s) {
+static hipError_t launch_sp_t(SpMlpArgs a, hipStream_t s) {
+  a.ecap = sparse_mlp_cap(a.K0p, a.N);
+  if (a.ecap == 0) return hipErrorInvalidValue;
   const size_t lds = sparse_mlp_lds_bytes(a.K0p, a.N);
   auto k = sparse_mlp_kernel<NGW>;
   hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
