@@ -4,7 +4,7 @@
 // per layer.  PW = 8400 per wave ~ 67 k pairs per workgroup: Criteo-39's three 400-wide layers at 90 % zero
 // (40 nonzeros per row, padded to the group of four's longest row rounded to 8 -> ~48 entries per neuron).
 // How a wave obtains each pair's (k, w):
-//   A  computed from the loop counter (no list at all): the LDS x-read + FMA floor
+//   A  computed from the loop counter (no list at all; a few VALU ops per pair): the LDS x-read + FMA floor
 //   B  the list staged in LDS, read back as wave-uniform ds_read_b128 broadcasts (two pairs each) -- the kernel
 //   C  the list in VGPRs, one entry per lane (one coalesced 512-B load per 64 pairs), v_readlane to SGPRs per pair
 //   D  the list read with wave-uniform (scalar) loads from global memory
@@ -29,11 +29,12 @@ __global__ void __launch_bounds__(64 * NW) walk(const int2* __restrict__ list, f
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < K * S; i += 64 * NW) x[i] = (float)(i & 7) * 0.25f;
   __syncthreads();
-  const int2* L = list + ((int64_t)blockIdx.x * NW + wave) * PW;
+  // every workgroup walks the SAME lists (one per wave), as every workgroup of the kernel walks the same weights
+  const int2* L = list + (int64_t)wave * PW;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if constexpr (V == 0) {
     for (int j = 0; j < PW; j += 4) {
-      const int k0 = (j * 97 + wave * 13) % K, k1 = (k0 + 131) % K, k2 = (k0 + 257) % K, k3 = (k0 + 389) % K;
+      const int k0 = (j * 37 + wave * 13) & 255, k1 = k0 + 131, k2 = (k0 + 57) & 255, k3 = k0 + 9;
       a0 = fmaf(0.5f, x[k0 * S + lane], a0);
       a1 = fmaf(0.5f, x[k1 * S + lane], a1);
       a2 = fmaf(0.5f, x[k2 * S + lane], a2);
@@ -104,7 +105,7 @@ __global__ void __launch_bounds__(64 * NW) walk(const int2* __restrict__ list, f
 
 int main() {
   const int grid = 256;
-  const int64_t n = (int64_t)grid * NW * PW;
+  const int64_t n = (int64_t)NW * PW;
   std::vector<int2> h(n);
   uint64_t s = 88172645463325252ull;
   for (int64_t i = 0; i < n; ++i) {
