@@ -195,6 +195,9 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads
  * DFWFM_BWD_MLP_WEIGHTS both only read what TILES saved, so they may run concurrently on two streams. */
 #define DFWFM_BWD_TILES 4
 #define DFWFM_BWD_SPREAD 8
+/* The two halves of DFWFM_BWD_SPREAD on their own: the shallow reductions' final sums, the table scatter. */
+#define DFWFM_BWD_REDUCE 16
+#define DFWFM_BWD_SCATTER 32
 int dfwfm_backward_phases(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads, int32_t phases,
                           void* stream);
 

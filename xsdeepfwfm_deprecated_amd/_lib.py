@@ -49,7 +49,7 @@ INGEST_HEADERS = [os.path.join("..", "..", "include", "dfwfm_ingest.h")]
 DFWFM_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported", -3: "HIP error", -4: "bad state"}
 FLAG_INDEX_OUT_OF_RANGE = 1
-BWD_TABLES, BWD_MLP_WEIGHTS, BWD_TILES, BWD_SPREAD = 1, 2, 4, 8  # dfwfm_backward_phases
+BWD_TABLES, BWD_MLP_WEIGHTS, BWD_TILES, BWD_SPREAD, BWD_REDUCE, BWD_SCATTER = 1, 2, 4, 8, 16, 32  # dfwfm_backward_phases
 FAMILY_SECOND, FAMILY_FIRST = 0, 1  # dfwfm_sparse_grads
 ADAM_STATE_BYTES = 48
 
