@@ -924,6 +924,156 @@ __global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// dW_l += G_l^T X_{l-1} with the MFMA operands loaded straight from global memory into registers (no LDS
+// staging, no barrier in the K loop).  Workgroup = one 80 (n) x 80 (k) block of one layer over one batch split;
+// its four waves each take a contiguous quarter of the split's rows and own the whole block: 5 x 5 16x16 MFMA
+// tiles, 100 accumulators.  A k-step is four batch rows; for it a lane (m = lane & 15, row = lane >> 4) loads
+// ONE float4 + ONE float of G and the same of X: tile t < 4 of the block maps its row / column m to n0 + 4m + t
+// (the float4's element t), tile 4 to n0 + 64 + m -- so 16 lanes read 320 contiguous bytes of a row and every
+// k-step is 4 loads for 25 MFMAs (the LDS kernel above: 8 staging loads, 8 LDS stores and 80 LDS reads per 64).
+// Loads run kDwrP k-steps ahead.  The four waves' blocks are summed through LDS in a fixed order ((w0 + w2) +
+// (w1 + w3)) and added to dW with one coalesced atomic per element per workgroup; db_l = sum G_l rides on the
+// k-block-0 workgroups, from the A operands they already hold.
+// ---------------------------------------------------------------------------
+constexpr int kDwrT = 80;       // block edge (5 MFMA tiles)
+constexpr int kDwrLd = kDwrT;   // LDS row stride of the reduction blocks (52.5 KB: three workgroups per CU)
+__device__ __forceinline__ int dwr_local(int t, int m) { return t < 4 ? 4 * m + t : 64 + m; }
+
+// kDwrP: k-steps of loads in flight per wave; NW: waves per workgroup (each a contiguous 1/NW of the split's rows)
+template <int kDwrP, int NW>
+__global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[2][kDwrT][kDwrLd];
+  __shared__ float bred[NW][kDwrT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x;
+  int l = 1;
+  while (l < a.H && bid >= a.blk0[l + 1]) ++l;
+  bid -= a.blk0[l];
+  const int per_layer_blocks = a.nnb * a.nkb[l];
+  const int split = bid / per_layer_blocks;
+  const int rem = bid - split * per_layer_blocks;
+  const int nb = rem / a.nkb[l];
+  const int kb = rem - nb * a.nkb[l];
+  const int N = a.N, K = a.K[l], ldx = a.ldx[l];
+  const int n0 = nb * kDwrT, k0 = kb * kDwrT;
+  // this wave's rows: a contiguous 1/NW of the split (rows_per_split is a multiple of 16 NW)
+  const int64_t q = a.rows_per_split / NW;
+  const int64_t r_lo = (int64_t)split * a.rows_per_split + wave * q;
+  int64_t r_hi = r_lo + q;
+  if (r_hi > a.batch) r_hi = a.batch;
+  const int nsteps = r_hi > r_lo ? (int)((r_hi - r_lo + 3) >> 2) : 0;
+  const int m = lane & 15, kk = lane >> 4;
+  // raw buffers over this wave's rows from column n0 / k0 on: rows past r_hi (another wave's) and everything past
+  // the array read as 0; columns n >= N / k >= K of a valid row read the next row's values, which only reach
+  // accumulators of outputs that are never stored
+  const int64_t nrows = r_hi > r_lo ? r_hi - r_lo : 0;
+  const int64_t g_bytes = nrows > 0 ? (nrows * N - n0) * 4 : 0;
+  const int64_t x_bytes = nrows > 0 ? (nrows * ldx - k0) * 4 : 0;
+  const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.G[l] + r_lo * N + n0), (short)0, (int)(g_bytes > 0 ? g_bytes : 0), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.X[l] + r_lo * ldx + k0), (short)0, (int)(x_bytes > 0 ? x_bytes : 0), 0x00020000);
+  const int gvo = (kk * N + 4 * m) * 4, xvo = (kk * ldx + 4 * m) * 4;  // this lane's float4 in a k-step
+  const int gvo1 = (kk * N + 64 + m) * 4, xvo1 = (kk * ldx + 64 + m) * 4;  // and its float of tile 4
+  const int gstep = 16 * N, xstep = 16 * ldx;                          // bytes per k-step (four rows)
+  f32x4 ga[kDwrP], xa[kDwrP];
+  float gb[kDwrP], xb[kDwrP];
+#define DWR_LOAD(J, S)                                                                                  \
+  do {                                                                                                  \
+    const int go_ = (J) * gstep, xo_ = (J) * xstep;                                                     \
+    ga[S] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(grs, gvo, go_, 0));         \
+    gb[S] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, gvo1, go_, 0));         \
+    xa[S] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xvo, xo_, 0));         \
+    xb[S] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, xvo1, xo_, 0));         \
+  } while (0)
+  f32x4 acc[5][5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bs0 = 0.f, bs1 = 0.f, bs2 = 0.f, bs3 = 0.f, bs4 = 0.f;
+  // whole groups of kDwrP k-steps, every load unconditional: steps past the wave's rows read 0 (the buffer's
+  // range), so the last group's prefetch and a ragged tail cost no branches and no register copies; a slot is
+  // refilled right after the MFMAs that read it, kDwrP - 1 k-steps before it is needed
+  const int nit = (nsteps + kDwrP - 1) / kDwrP;
+#pragma unroll
+  for (int s = 0; s < kDwrP; ++s) {
+    DWR_LOAD(s, s);  // slot by slot, in the loop's order (so the loop's waits count the same loads)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int it = 0; it < nit; ++it) {
+#pragma unroll
+    for (int s = 0; s < kDwrP; ++s) {
+      const float a0 = ga[s][0], a1 = ga[s][1], a2 = ga[s][2], a3 = ga[s][3], a4 = gb[s];
+      const float b0 = xa[s][0], b1 = xa[s][1], b2 = xa[s][2], b3 = xa[s][3], b4 = xb[s];
+      bs0 += a0; bs1 += a1; bs2 += a2; bs3 += a3; bs4 += a4;
+#define DWR_ROW(TN, A)                                                                       \
+  acc[TN][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(A, b0, acc[TN][0], 0, 0, 0);             \
+  acc[TN][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(A, b1, acc[TN][1], 0, 0, 0);             \
+  acc[TN][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(A, b2, acc[TN][2], 0, 0, 0);             \
+  acc[TN][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(A, b3, acc[TN][3], 0, 0, 0);             \
+  acc[TN][4] = __builtin_amdgcn_mfma_f32_16x16x4f32(A, b4, acc[TN][4], 0, 0, 0)
+      DWR_ROW(0, a0);
+      DWR_ROW(1, a1);
+      DWR_ROW(2, a2);
+      DWR_ROW(3, a3);
+      DWR_ROW(4, a4);
+#undef DWR_ROW
+      __builtin_amdgcn_sched_barrier(0);  // the refill after every MFMA that reads the slot (no register copies)
+      DWR_LOAD((it + 1) * kDwrP + s, s);
+      __builtin_amdgcn_sched_barrier(0);  // and before the next slot's MFMAs (the scheduler sinks it to the loop end)
+    }
+  }
+#undef DWR_LOAD
+  float bs[5] = {bs0, bs1, bs2, bs3, bs4};
+
+  // db_l: the block's column sums of G over the four rows of each lane group, then over the waves
+  float* gB = kb == 0 ? a.gB[l] : nullptr;
+  if (gB) {
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      bs[t] += __shfl_xor(bs[t], 16);
+      bs[t] += __shfl_xor(bs[t], 32);
+    }
+    if (kk == 0)
+#pragma unroll
+      for (int t = 0; t < 5; ++t) bred[wave][dwr_local(t, m)] = bs[t];
+  }
+  // the NW waves' blocks: waves 0 / 1 store, then waves 2 / 3, 4 / 5, ... add theirs in turn (a fixed order), and
+  // every thread adds the two sums into dW row by row (coalesced atomics)
+  float* gW = a.gW[l];
+  for (int g = 0; g < NW / 2; ++g) {
+    if (g > 0) __syncthreads();
+    if (wave >> 1 == g) {
+      float(&rb)[kDwrT][kDwrLd] = red[wave & 1];
+#pragma unroll
+      for (int tn = 0; tn < 5; ++tn)
+#pragma unroll
+        for (int tk = 0; tk < 5; ++tk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float& r = rb[dwr_local(tn, 4 * kk + i)][dwr_local(tk, m)];
+            r = g == 0 ? acc[tn][tk][i] : r + acc[tn][tk][i];
+          }
+    }
+  }
+  __syncthreads();
+  if (gB && tid < kDwrT && n0 + tid < N) {
+    float b = bred[0][tid];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) b += bred[w][tid];
+    atomicAdd(gB + n0 + tid, b);
+  }
+  if (!gW) return;
+  // one atomic per element, consecutive lanes on consecutive k of a row (a wave's atomics cover 256 contiguous bytes)
+  for (int e = tid; e < kDwrT * kDwrT; e += 64 * NW) {
+    const int r = e / kDwrT, c = e - r * kDwrT;
+    const int n = n0 + r, k = k0 + c;
+    if (n < N && k < K) atomicAdd(gW + (int64_t)n * K + k, red[0][r][c] + red[1][r][c]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Adam (torch.optim.Adam, single-tensor form, torch/optim/adam.py _single_tensor_adam):
 // g += wd * p; m = lerp(m, g, 1 - b1);
 // v = v * b2 + (1 - b2) * g * g; p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
@@ -1180,9 +1330,12 @@ hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream
   return hipGetLastError();
 }
 
-hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
+hipError_t launch_dw(const DwArgs& a, int total_blocks, bool staged, hipStream_t s) {
   if (total_blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(dw_kernel, dim3(total_blocks), dim3(256), 0, s, a);
+  if (staged) hipLaunchKernelGGL(dw_kernel, dim3(total_blocks), dim3(256), 0, s, a);
+  else if (a.nw == 8) hipLaunchKernelGGL((dwr_kernel<4, 8>), dim3(total_blocks), dim3(512), 0, s, a);
+  else if (a.pf == 6) hipLaunchKernelGGL((dwr_kernel<6, 4>), dim3(total_blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(total_blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
