@@ -1008,8 +1008,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     memset(&d, 0, sizeof d);
     d.H = H;
     d.N = m->N;
-    static const bool staged = getenv("DFWFM_DW_STAGED") && atoi(getenv("DFWFM_DW_STAGED")) != 0;  // A/B only
-    const int edge = dw_block_edge(staged), quantum = dw_row_quantum(staged);
+    const int edge = kDwEdge, quantum = kDwRows;
     d.nnb = (m->N + edge - 1) / edge;
     d.batch = batch;
     int per_split = 0;
@@ -1024,22 +1023,21 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       per_split += d.nnb * d.nkb[l];
     }
     if (per_split > 0) {
-      // batch splits: the register-direct kernel at one workgroup per CU at most (tools/ubench_dw, Criteo-39,
-      // B = 4096: 3 splits = 225 workgroups 42 us; 6 splits 47 us; past one round of workgroups 60+ us); the staged
-      // kernel at ~3 workgroups per CU (each over >= 128 rows), beside the one-GPU step's reductions, scatter and Adam
-      int64_t splits = staged ? 768 / per_split : 256 / per_split;
+      // batch splits: one workgroup per CU at most (tools/ubench_dw, Criteo-39, B = 4096: 3 splits = 225
+      // workgroups 42 us; 6 splits 47 us; past one round of workgroups 60+ us), each over >= 128 rows
+      int64_t splits = 256 / per_split;
       if (const char* ds = getenv("DFWFM_DW_SPLITS")) splits = atoi(ds);  // tuning only
       const int64_t max_splits = (batch + 127) / 128;
       if (splits > max_splits) splits = max_splits;
       if (splits < 1) splits = 1;
       int64_t rows = (batch + splits - 1) / splits;
-      rows = (rows + quantum - 1) / quantum * quantum;  // whole dw_kernel chunks / dwr_kernel wave shares
+      rows = (rows + quantum - 1) / quantum * quantum;  // whole k-step groups per wave
       splits = (batch + rows - 1) / rows;
       d.splits = (int32_t)splits;
       d.rows_per_split = rows;
       d.blk0[1] = 0;
       for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
-      e = launch_dw(d, d.blk0[H + 1], staged, s);
+      e = launch_dw(d, d.blk0[H + 1], s);
       if (e != hipSuccess) return hip_fail(e, "dw launch");
     }
   }

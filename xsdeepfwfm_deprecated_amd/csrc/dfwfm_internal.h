@@ -298,12 +298,10 @@ struct DwArgs {
   int32_t K[kMaxH + 1];          // input width of layer l
   int32_t ldx[kMaxH + 1];        // row stride of X_{l-1} (multiple of 4)
   int32_t blk0[kMaxH + 2];       // first workgroup of layer l (prefix over layers)
-  int32_t nkb[kMaxH + 1];        // 64-wide K blocks of layer l
+  int32_t nkb[kMaxH + 1];        // 80-wide K blocks of layer l
   int32_t H, N, nnb, splits;
   int64_t batch;
   int64_t rows_per_split;
-  int32_t pf;                    // dwr_kernel: k-steps of loads in flight per wave (4, 6; 0 = 4)
-  int32_t nw;                    // dwr_kernel: waves per workgroup (4 or 8; 0 = 4); rows_per_split % (16 nw) == 0
 };
 
 // One tensor of a fused Adam step.
@@ -404,11 +402,10 @@ DFWFM_DECL_PER_D(16)
 DFWFM_DECL_PER_D(32)
 hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds, hipStream_t s);
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
-// staged: the LDS-staged 64 x 64 dw_kernel (A/B only, DFWFM_DW_STAGED=1); else the register-direct 80 x 80
-// dwr_kernel (nnb / nkb / rows_per_split sized by dw_block_edge / dw_row_quantum)
-hipError_t launch_dw(const DwArgs& a, int total_blocks, bool staged, hipStream_t s);
-inline int dw_block_edge(bool staged) { return staged ? 64 : 80; }
-inline int dw_row_quantum(bool) { return 128; }  // dwr_kernel: up to eight waves x whole groups of four k-steps
+// the register-direct dwr_kernel: 80 x 80 blocks (nnb, nkb), batch splits of a multiple of kDwRows rows
+hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s);
+constexpr int kDwEdge = 80;
+constexpr int kDwRows = 64;  // four waves x whole groups of four four-row k-steps
 hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages
 hipError_t launch_reduce_final(const RedArgs& a, hipStream_t s);  // the second stage only (bwd_kernel red)
 hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s);

@@ -12,7 +12,7 @@
 //                   dlogit-weighted Gram matrix on MFMA), net_1_fc, the numerical fields' tables.
 //   scatter_kernel  dE / dfo into the categorical tables' dense grads (nn.Embedding(sparse=False)):
 //                   small tables accumulate privately in LDS, large ones take global atomics.
-//   dw_kernel       dW_l += G_l^T X_{l-1} and db_l += sum G_l for all layers in one launch.
+//   dwr_kernel      dW_l += G_l^T X_{l-1} and db_l += sum G_l for all layers in one launch.
 //   adam_kernel     torch.optim.Adam's update (coupled L2, bias correction) over a tensor list.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -802,135 +802,14 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// dW_l += G_l^T X_{l-1}: workgroup = 64 (n) x 64 (k) block of one layer over one batch split;
-// wave w owns n rows 16w..16w+15 and the 4 k tiles.  32-row chunks of G and X are staged in LDS,
-// the next chunk's global loads in registers while the current chunk's MFMAs run.
-// ---------------------------------------------------------------------------
-#ifndef DFWFM_DW_RB
-#define DFWFM_DW_RB 64
-#endif
-constexpr int kDwRB = DFWFM_DW_RB;   // batch rows per staged chunk (one barrier pair per chunk)
-constexpr int kDwU = kDwRB * 16 / 256;
-// row stride 80 = 16 mod 64 banks: the four 16-lane row groups of an MFMA fragment read hit disjoint banks (68
-// overlapped them ~2.3-way)
-typedef float DwTile[kDwRB][64 + 16];
-__device__ __forceinline__ void dw_block(const DwArgs& a, int bid, DwTile& gs, DwTile& xs) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  int l = 1;
-  while (l < a.H && bid >= a.blk0[l + 1]) ++l;
-  bid -= a.blk0[l];
-  const int per_layer_blocks = a.nnb * a.nkb[l];
-  const int split = bid / per_layer_blocks;
-  const int rem = bid - split * per_layer_blocks;
-  const int nb = rem / a.nkb[l];
-  const int kb = rem - nb * a.nkb[l];
-  const int N = a.N, K = a.K[l];
-  const int n0 = nb * 64, k0 = kb * 64;
-  const int64_t r_begin = (int64_t)split * a.rows_per_split;
-  int64_t r_end = r_begin + a.rows_per_split;
-  if (r_end > a.batch) r_end = a.batch;
-  const float* G = a.G[l];
-  const float* X = a.X[l];
-  const int ldx = a.ldx[l];
-
-  // staging map: kDwRB rows x 64 cols = kDwRB*16 float4 per operand, kDwU per thread
-  float4 pg[kDwU], px[kDwU];
-  auto fetch = [&](int64_t rbase) {
-#pragma unroll
-    for (int u = 0; u < kDwU; ++u) {
-      const int i = tid + u * 256;
-      const int rr = i >> 4;
-      const int c4 = (i & 15) * 4;
-      const int64_t row = rbase + rr;
-      // whole float4 loads only (N and the X row stride are multiples of 4, dfwfm_train_begin): no
-      // per-element branches, whose merges made the compiler wait for each load inside the prefetch;
-      // X columns in [K, ldx) are zeroed when the chunk is stored to LDS
-      float4 vg = make_float4(0.f, 0.f, 0.f, 0.f), vx = vg;
-      if (row < r_end && n0 + c4 < N) vg = *reinterpret_cast<const float4*>(G + row * N + n0 + c4);
-      if (row < r_end && k0 + c4 < ldx) vx = *reinterpret_cast<const float4*>(X + row * ldx + k0 + c4);
-      pg[u] = vg;
-      px[u] = vx;
-    }
-  };
-  f32x4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float* gB = kb == 0 ? a.gB[l] : nullptr;  // db_l = sum_b G_l[b, :] rides on the k-block-0 workgroups
-  float bsum = 0.f;
-  const bool k_edge = k0 + 64 > K;
-  fetch(r_begin);
-  for (int64_t rb = r_begin; rb < r_end; rb += kDwRB) {
-#pragma unroll
-    for (int u = 0; u < kDwU; ++u) {
-      const int i = tid + u * 256;
-      float4 vx = px[u];
-      if (k_edge) {
-        const int c = k0 + (i & 15) * 4;
-        vx.x = c < K ? vx.x : 0.f; vx.y = c + 1 < K ? vx.y : 0.f;
-        vx.z = c + 2 < K ? vx.z : 0.f; vx.w = c + 3 < K ? vx.w : 0.f;
-      }
-      *reinterpret_cast<float4*>(&gs[i >> 4][(i & 15) * 4]) = pg[u];
-      *reinterpret_cast<float4*>(&xs[i >> 4][(i & 15) * 4]) = vx;
-    }
-    __syncthreads();
-    if (rb + kDwRB < r_end) fetch(rb + kDwRB);
-    // fragments of k-step s+1 are read from LDS while step s's MFMAs run
-    float av = gs[lane >> 4][16 * wave + (lane & 15)];
-    float bv[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) bv[t] = xs[lane >> 4][16 * t + (lane & 15)];
-#pragma unroll
-    for (int s = 0; s < kDwRB / 4; ++s) {
-      float an = 0.f, bn[4] = {0.f, 0.f, 0.f, 0.f};
-      if (s + 1 < kDwRB / 4) {
-        const int rn = 4 * (s + 1) + (lane >> 4);
-        an = gs[rn][16 * wave + (lane & 15)];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bn[t] = xs[rn][16 * t + (lane & 15)];
-      }
-      // pin the order: the next fragments' reads issue before this step's MFMAs, their wait after
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[t], acc[t], 0, 0, 0);
-      asm volatile("" ::"v"(an), "v"(bn[0]), "v"(bn[1]), "v"(bn[2]), "v"(bn[3]));
-      av = an;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) bv[t] = bn[t];
-    }
-    if (gB && tid < 64)
-#pragma unroll 8
-      for (int rr = 0; rr < kDwRB; ++rr) bsum += gs[rr][tid];
-    __syncthreads();
-  }
-  if (gB && tid < 64 && n0 + tid < N) atomicAdd(gB + n0 + tid, bsum);
-  float* gW = a.gW[l];
-  if (!gW) return;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int k = k0 + 16 * t + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + 16 * wave + (lane >> 4) * 4 + r;
-      if (n < N && k < K) atomicAdd(gW + (int64_t)n * K + k, acc[t][r]);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) dw_kernel(DwArgs a) {
-  __shared__ __attribute__((aligned(16))) DwTile gs, xs;
-  dw_block(a, blockIdx.x, gs, xs);
-}
-
-// ---------------------------------------------------------------------------
 // dW_l += G_l^T X_{l-1} with the MFMA operands loaded straight from global memory into registers (no LDS
 // staging, no barrier in the K loop).  Workgroup = one 80 (n) x 80 (k) block of one layer over one batch split;
 // its four waves each take a contiguous quarter of the split's rows and own the whole block: 5 x 5 16x16 MFMA
 // tiles, 100 accumulators.  A k-step is four batch rows; for it a lane (m = lane & 15, row = lane >> 4) loads
 // ONE float4 + ONE float of G and the same of X: tile t < 4 of the block maps its row / column m to n0 + 4m + t
 // (the float4's element t), tile 4 to n0 + 64 + m -- so 16 lanes read 320 contiguous bytes of a row and every
-// k-step is 4 loads for 25 MFMAs (the LDS kernel above: 8 staging loads, 8 LDS stores and 80 LDS reads per 64).
+// k-step is 4 loads for 25 MFMAs (round 2's LDS-staged 64 x 64 kernel: 8 staging loads, 8 LDS stores and 80 LDS
+// reads per 64 MFMAs, 59.5 us against 42.1 for this one at Criteo-39, B = 4096; tools/ubench_dw).
 // Loads run kDwrP k-steps ahead.  The four waves' blocks are summed through LDS in a fixed order ((w0 + w2) +
 // (w1 + w3)) and added to dW with one coalesced atomic per element per workgroup; db_l = sum G_l rides on the
 // k-block-0 workgroups, from the A operands they already hold.
@@ -939,7 +818,8 @@ constexpr int kDwrT = 80;       // block edge (5 MFMA tiles)
 constexpr int kDwrLd = kDwrT;   // LDS row stride of the reduction blocks (52.5 KB: three workgroups per CU)
 __device__ __forceinline__ int dwr_local(int t, int m) { return t < 4 ? 4 * m + t : 64 + m; }
 
-// kDwrP: k-steps of loads in flight per wave; NW: waves per workgroup (each a contiguous 1/NW of the split's rows)
+// kDwrP: k-steps of loads in flight per wave; NW: waves per workgroup (each a contiguous 1/NW of the split's rows).
+// Measured alike: kDwrP 4 / 6 / 8 (42.1 / 43.5 / 43.6 us) and eight waves per workgroup (43.7 us).
 template <int kDwrP, int NW>
 __global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
   __shared__ __attribute__((aligned(16))) float red[2][kDwrT][kDwrLd];
@@ -1330,12 +1210,9 @@ hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream
   return hipGetLastError();
 }
 
-hipError_t launch_dw(const DwArgs& a, int total_blocks, bool staged, hipStream_t s) {
+hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
   if (total_blocks <= 0) return hipSuccess;
-  if (staged) hipLaunchKernelGGL(dw_kernel, dim3(total_blocks), dim3(256), 0, s, a);
-  else if (a.nw == 8) hipLaunchKernelGGL((dwr_kernel<4, 8>), dim3(total_blocks), dim3(512), 0, s, a);
-  else if (a.pf == 6) hipLaunchKernelGGL((dwr_kernel<6, 4>), dim3(total_blocks), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(total_blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(total_blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
