@@ -73,6 +73,10 @@ def parse():
                     help="give even-numbered streams one half of the CUs and odd-numbered streams the other (HIP CU "
                          "masks): with 32-sample workgroups a batch is 128 workgroups, one per CU of a half, so two "
                          "batches share each CU (default: even-odd with the 32-sample forward, else none)")
+    ap.add_argument("--batch-set", type=int, default=20,
+                    help="batches per forward launch (dfwfm_forward_batches: one grid over that many resident "
+                         "batches, each batch its own inputs and logits); 1: one launch per batch (graph replay, "
+                         "CU-masked stream pairs for the 32-sample forward)")
     ap.add_argument("--streams", type=int, default=None,
                     help="independent batch-4096 forwards in flight on this many HIP streams (2: a second "
                          "batch's workgroup shares each CU, hiding the gather / FwFM phases)")
@@ -133,14 +137,14 @@ class _HostGate:
             pass
 
 
-def r32_on(config="deepfwfm", cu_mask="even-odd"):
+def r32_on(config="deepfwfm", cu_mask="even-odd", batch_set=1):
     """The library runs the 32-sample-workgroup forward (fwd32_kernel) for the bench's deep configs when the
-    stream is CU-masked to half of the chip (128 workgroups per 4096-row batch cover it) or DFWFM_R32=1 forces it;
-    DFWFM_R32=0 never."""
+    launch's 32-sample workgroups cover every CU of its stream: a batch set (>= 2 batches of 4096 on the whole
+    chip), or one batch on a stream CU-masked to half of the chip; DFWFM_R32=1 forces it, DFWFM_R32=0 never."""
     env = os.environ.get("DFWFM_R32", "")
     if config in ("fwfm", "fwfm_pruned") or env == "0":
         return False
-    return env not in ("",) or cu_mask not in (None, "none")
+    return env not in ("",) or cu_mask not in (None, "none") or batch_set > 1
 
 
 def masked_streams(dev, S, how):
@@ -170,10 +174,10 @@ def masked_streams(dev, S, how):
     return streams, handles
 
 
-def kernel_name(config="deepfwfm", cu_mask="none"):
+def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT / DFWFM_R32 select the A/B variants."""
-    if r32_on(config, cu_mask):
+    if r32_on(config, cu_mask, batch_set):
         return f"dfwfm::fwd32_kernel<10,{'true' if config == 'qr' else 'false'}>"
     if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
@@ -265,7 +269,7 @@ def main():
         torch.cuda.synchronize(dev)
         params = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
 
-    n_bufs = 4  # distinct resident batches, rotated, so gathers are not L2-hot repeats
+    n_bufs = 8  # distinct resident batches, rotated, so gathers are not L2-hot repeats
     batches = []
     for i in range(n_bufs):
         seed = 1000 * rank + i
@@ -279,10 +283,17 @@ def main():
     # deep configs: four batches in flight on CU-masked stream pairs (even / odd CU ids): a 4096-row batch is 128
     # 32-sample workgroups, which cover a half, so the library runs fwd32_kernel and every CU holds two batches
     # (DESIGN.md section 3); DFWFM_R32=0: the 16-sample kernel on two plain streams
+    # batch sets (default): every launch is one grid over M resident batches on the whole chip (the 32-sample
+    # forward for the deep configs: a set's workgroups cover every CU twice over), two streams so that the next
+    # set's workgroups take the CU slots the current one frees while it drains.  --batch-set 1: one launch per
+    # batch from captured graphs; the deep configs then run four batches in flight on CU-masked stream pairs
+    M = max(1, a.batch_set)
     r32_default = deep and os.environ.get("DFWFM_R32", "") != "0"
-    cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32_default else "none")
-    S = max(1, a.streams if a.streams is not None else (3 if not deep else (4 if r32_default else 2)))
+    cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32_default and M == 1 else "none")
+    S = max(1, a.streams if a.streams is not None else (2 if M > 1 else (3 if not deep else (4 if r32_default else 2))))
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
+    set_outs = [[torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(M)] for _ in range(S)] \
+        if M > 1 else None
 
     with torch.no_grad():
         eng = model._sync_engine(dev)
@@ -305,7 +316,17 @@ def main():
             return [n // S + (1 if k < n % S else 0) for k in range(S)]
         G = max(1, min(a.graph_steps, max(per_stream(a.steps))))
         graphs = None
-        if not a.no_graph:
+        set_pos = [0] * S
+        if M > 1:
+            def launch_set(k, n):
+                # n batches (rotating over the resident ones) in one dfwfm_forward_batches launch on stream k
+                i0 = set_pos[k] * S + k
+                set_pos[k] += n
+                eng.forward_batches([batches[(i0 + j * S) % n_bufs] for j in range(n)], set_outs[k][:n])
+            for k in range(S):
+                with torch.cuda.stream(streams[k]):
+                    launch_set(k, M)  # initialise everything outside the timed region
+        elif not a.no_graph:
             def capture(n, k):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=streams[k]):
@@ -329,6 +350,18 @@ def main():
             # progress(steps enqueued so far) after every round
             ns = per_stream(n_total)
             done = 0
+            if M > 1:
+                for r in range(max(ns) // M + 1):
+                    for k in range(S):
+                        left = ns[k] - r * M
+                        if left <= 0:
+                            continue
+                        with torch.cuda.stream(streams[k]):
+                            launch_set(k, min(M, left))
+                        done += min(M, left)
+                    if progress:
+                        progress(done)
+                return
             if graphs is None:
                 for i in range(max(ns)):
                     for k in range(S):
@@ -404,7 +437,10 @@ def main():
     first = min(range(S), key=lambda k: s0[0].elapsed_time(s0[k]))
     last = max(range(S), key=lambda k: s0[0].elapsed_time(s1[k]))
     ms = s0[first].elapsed_time(s1[last])
-    launch_ms = sum(s0[k].elapsed_time(s1[k]) for k in range(S)) / a.steps  # per launch, S side by side
+    # per launch, S side by side (what rocprofv3 reports); a launch is one batch, or a set of up to M
+    units = BATCH * (min(M, max(per_stream(a.steps))) if M > 1 else 1)
+    n_launch = sum(-(-n // M) for n in per_stream(a.steps)) if M > 1 else a.steps
+    launch_ms = sum(s0[k].elapsed_time(s1[k]) for k in range(S)) / n_launch
     # where the streams start and end inside the timed region (fill / drain of a short run)
     skew = {"start_us": [round(s0[first].elapsed_time(s0[k]) * 1e3, 2) for k in range(S)],
             "end_us": [round(s1[k].elapsed_time(s1[last]) * 1e3, 2) for k in range(S)]}
@@ -434,14 +470,14 @@ def main():
         flops = 2 * nnz + 2 * 400 + 2 * pairs * 10
     # achieved = algorithmic FLOP of one launch / its duration, times the launches in flight (each of
     # the S concurrent launches takes ~S x the per-batch time): the aggregate rate over the timed region
-    achieved_tf = flops * BATCH * S / (launch_ms / 1e3) / 1e12
-    achieved_gbs = bytes_ * BATCH * S / (launch_ms / 1e3) / 1e9
-    kname = kernel_name(a.config, cu_mask)
+    achieved_tf = flops * units * S / (launch_ms / 1e3) / 1e12
+    achieved_gbs = bytes_ * units * S / (launch_ms / 1e3) / 1e9
+    kname = kernel_name(a.config, cu_mask, M)
     if a.config == "pruned" and sparse_on:
         kname = "dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::sparse_mlp_kernel<64>"
         mfma_bound = "valu"  # the sparse MLP runs on the f32 vector FMAs (same 157.3 TF/s peak on gfx950)
-    workload_id = f"{a.config}/{a.first_order}/scale{K}/{a.inputs}"
-    traffic = pmc_traffic(kname, workload_id)
+    workload_id = f"{a.config}/{a.first_order}/scale{K}/{a.inputs}" + ("/set" if M > 1 else "")
+    traffic = pmc_traffic(kname, workload_id, units // BATCH)
 
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
@@ -461,7 +497,9 @@ def main():
                    "workload_id": workload_id,
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
-                   "launch": ("eager" if a.no_graph else f"hipGraph replay, {G} forwards per graph")
+                   "launch": (f"batch sets: {M} batches per launch (dfwfm_forward_batches, one grid; each batch its "
+                              "own resident inputs and logits)" if M > 1 else
+                              "eager" if a.no_graph else f"hipGraph replay, {G} forwards per graph")
                              + (f", {S} streams (batches in flight)" if S > 1 else "")
                              + (f", CU masks {cu_mask} (stream pairs on chip halves)" if cu_mask != "none" else "")},
         "settle": {"forwards": settle_n, "ms": round(settle_ms, 1),
@@ -473,7 +511,7 @@ def main():
             "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "flops_per_sample": flops}
     hbm = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
            "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "bytes_per_sample": bytes_}
-    common = {"traffic": traffic, "kernel": kname, "units_per_launch": BATCH, "launch_us": round(launch_ms * 1e3, 3),
+    common = {"traffic": traffic, "kernel": kname, "units_per_launch": units, "launch_us": round(launch_ms * 1e3, 3),
               "launches_in_flight": S}
     if cfg["use_deep"]:  # 98.5 % of the arithmetic is the MLP: MFMA-bound (intensity ~690 FLOP/B)
         result["roofline"] = {**mfma, **common}
@@ -498,10 +536,11 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def pmc_traffic(kname, workload_id):
+def pmc_traffic(kname, workload_id, batches=1):
     """HBM bytes per launch of kernel `kname` on workload `workload_id` from the committed PMC summary
     (tools/pmc.sh + tools/pmc_summary.py: rocprofv3 --pmc over this bench's own command): 2 x FETCH_SIZE +
-    WRITE_SIZE, FETCH doubled per the gfx950 calibration; None unless that kernel was counted on that workload."""
+    WRITE_SIZE, FETCH doubled per the gfx950 calibration; None unless that kernel was counted on that workload.
+    Batch sets: the counted bytes per batch times the `batches` of this run's launches."""
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(pmc))
@@ -509,6 +548,8 @@ def pmc_traffic(kname, workload_id):
         return None
     for e in d.get("entries", []):
         if e.get("kernel") == kname and e.get("workload") == workload_id:
+            if "hbm_bytes_per_batch" in e:
+                return e["hbm_bytes_per_batch"] * batches
             return e.get("hbm_bytes_per_launch")
     return None
 

@@ -113,6 +113,15 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
 int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv,
                   int64_t xv_stride, int64_t batch, float* out, void* stream);
 
+/* The forward of nb batches in ONE launch per (up to) 32 batches on `stream`: batch i reads xi[i] / xv[i]
+ * (device pointers, `batch` rows each, the same strides) and writes its logits to out[i].  A serving queue's
+ * batches in flight as one grid: the workgroups of all of them are dispatched as CU slots free up, so no batch
+ * waits for a launch boundary and a short run has no per-launch drain.  Every batch's logits are bit-identical to
+ * dfwfm_forward on that batch alone.  Replaces nb calls of the reference's forward (model/DeepFMs.py:285-469),
+ * e.g. eval_by_batch's per-batch loop (:750-780) over resident batches. */
+int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, int64_t xi_stride,
+                          const float* const* xv, int64_t xv_stride, int64_t batch, float* const* out, void* stream);
+
 /* The forward as two launches on `stream` -- the gather / shallow part (E tile and first + second
  * order to `workspace`), then the MLP and the combine -- so that two batches in flight on two
  * streams overlap their MLPs on every CU.  Same logits as dfwfm_forward, bit for bit.

@@ -28,7 +28,8 @@ def test_header_declares_expected_api():
     assert header_functions() == sorted([
         "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_backward_phases",
         "dfwfm_bce_grad",
-        "dfwfm_diag_stamps", "dfwfm_eval_metrics", "dfwfm_forward", "dfwfm_forward_workspace_bytes",
+        "dfwfm_diag_stamps", "dfwfm_eval_metrics", "dfwfm_forward", "dfwfm_forward_batches",
+        "dfwfm_forward_workspace_bytes",
         "dfwfm_forward_ws", "dfwfm_last_error", "dfwfm_model_build_fwfm_pairs", "dfwfm_model_build_sparse_mlp", "dfwfm_model_create", "dfwfm_model_destroy",
         "dfwfm_metrics_workspace_bytes", "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_prune_apply", "dfwfm_prune_threshold",
         "dfwfm_prune_workspace_bytes", "dfwfm_read_error_flag", "dfwfm_set_step_source", "dfwfm_sparse_grads", "dfwfm_sparse_grads_apply", "dfwfm_sparse_grads_local", "dfwfm_sparse_grads_size",
@@ -50,6 +51,7 @@ def test_abi_version_and_error_string(built):
     assert L.dfwfm_model_create(None, None) == -1
     assert b"null" in L.dfwfm_last_error()
     assert L.dfwfm_forward(None, None, 0, None, 0, 0, None, None) == -1
+    assert L.dfwfm_forward_batches(None, 2, None, 0, None, 0, 0, None, None) == -1
     assert L.dfwfm_train_forward(None, None, 0, None, 0, 0, None, 0.0, 0, None) == -1
     assert L.dfwfm_backward(None, None, None, None) == -1
     assert L.dfwfm_adam_step(None, 3, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, None) == -1

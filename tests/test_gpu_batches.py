@@ -1,0 +1,118 @@
+"""GPU: dfwfm_forward_batches -- the forward of several resident batches in one launch (one grid over all of
+them, each batch its own Xi / Xv / logits) -- against dfwfm_forward on each batch alone (bit-identical) and the
+float64 oracle (north-star bar).  The reference runs these batches one forward call at a time
+(model/DeepFMs.py:285-469, eval_by_batch's loop)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, logit_close, model_kwargs
+from oracle import dfwfm_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _criteo_model(gpu, deep=1, qr=0, seed=77):
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = synth.CRITEO_FEATURE_SIZES
+    cfg = dict(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0,
+               use_deep=deep, use_lw=1, use_fwlw=0, h_depth=3, deep_nodes=400, numerical=13, embedding_bag=qr,
+               qr_flag=qr, qr_operation="mult", qr_collisions=4, qr_threshold=200)
+    m = DeepFMs(**model_kwargs(cfg))
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    params = synth.synth_state(shapes, 39, 10, 400, True, bool(deep), seed=seed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    return cfg, params, m.to(gpu).eval()
+
+
+def _inputs(sizes, nb, B, seed):
+    from xsdeepfwfm_deprecated_amd import synth
+    return [synth.synth_inputs(sizes, 13, B, seed=seed + i) for i in range(nb)]
+
+
+def _check(cfg, params, m, gpu, host, sample=64):
+    eng = m._sync_engine(gpu)
+    dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
+    B = host[0][0].shape[0]
+    with torch.no_grad():
+        outs = [torch.full((B,), float("nan"), device=gpu) for _ in dev]
+        eng.forward_batches(dev, outs)
+        alone = [eng.forward(xi, xv) for xi, xv in dev]
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(B + len(host))
+    for i, ((xi, xv), o, a) in enumerate(zip(host, outs, alone)):
+        got = o.cpu().numpy()
+        assert np.array_equal(got, a.cpu().numpy()), f"batch {i}: set vs alone"
+        rows = np.arange(B) if B <= sample else rng.choice(B, sample, replace=False)
+        if i in (0, len(host) - 1):
+            assert logit_close(got[rows], dfwfm_oracle.forward(cfg, params, xi[rows], xv[rows])) < 1e-5
+
+
+@pytest.mark.parametrize("qr", [0, 1])
+@pytest.mark.parametrize("nb,B", [(2, 4096), (5, 4096), (3, 4096 + 17), (4, 33), (35, 256)])
+def test_batch_set_deep_bit_identical(gpu, qr, nb, B):
+    """DeepFwFM at Criteo-39 sizes (the 32-sample forward once the set covers the chip, else the 16-sample one):
+    every batch of the set equals its own forward, ragged tails included, more batches than one launch holds
+    (35 > 32: two launches)."""
+    cfg, params, m = _criteo_model(gpu, 1, qr, seed=77 + qr)
+    _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], nb, B, seed=100 * nb + B))
+
+
+@pytest.mark.parametrize("nb,B", [(3, 4096), (6, 1000)])
+def test_batch_set_fwfm_only_bit_identical(gpu, nb, B):
+    """The MLP-free forward (BASELINE configs[0]'s model at Criteo-39 sizes) as a batch set."""
+    cfg, params, m = _criteo_model(gpu, 0, 0, seed=91)
+    _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], nb, B, seed=7 * nb + B))
+
+
+@pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_qr_mult", "tiny_fwfm_lw", "fm_deep"])
+def test_batch_set_goldens(gpu, name):
+    """Reference goldens split into a set of equal batches (small tables, the generic kernels)."""
+    cfg, params, xi, xv, y, l32, l64, auc = load_golden(name)
+    from xsdeepfwfm_deprecated_amd import DeepFMs
+    m = DeepFMs(**model_kwargs(cfg))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    m = m.to(gpu).eval()
+    nb = 4
+    B = xi.shape[0] // nb
+    eng = m._sync_engine(gpu)
+    dev = [(torch.from_numpy(np.ascontiguousarray(xi[i * B:(i + 1) * B])).to(gpu),
+            torch.from_numpy(np.ascontiguousarray(xv[i * B:(i + 1) * B])).to(gpu)) for i in range(nb)]
+    outs = [torch.empty(B, device=gpu) for _ in range(nb)]
+    with torch.no_grad():
+        eng.forward_batches(dev, outs)
+    got = torch.cat(outs).cpu().numpy()
+    assert logit_close(got, l32[:nb * B]) < 1e-5 and logit_close(got, l64[:nb * B]) < 1e-5
+
+
+def test_batch_set_strided_inputs_and_errors(gpu):
+    """Row strides other than the field count (slices of wider resident arrays), an out-of-range index in one
+    batch of the set (the sticky flag, rows clamped, never a fault), and the argument checks."""
+    from xsdeepfwfm_deprecated_amd._lib import DfwfmError
+    cfg, params, m = _criteo_model(gpu, 1, 0, seed=5)
+    sizes = cfg["feature_sizes"]
+    host = _inputs(sizes, 3, 512, seed=3)
+    eng = m._sync_engine(gpu)
+    wide = [(torch.zeros(512, 40, dtype=torch.int64, device=gpu), torch.zeros(512, 20, device=gpu))
+            for _ in host]
+    for (wi, wv), (xi, xv) in zip(wide, host):
+        wi[:, :26] = torch.from_numpy(xi).to(gpu)
+        wv[:, :13] = torch.from_numpy(xv).to(gpu)
+    dev = [(wi[:, :26], wv[:, :13]) for wi, wv in wide]
+    outs = [torch.empty(512, device=gpu) for _ in dev]
+    with torch.no_grad():
+        eng.forward_batches(dev, outs)
+        alone = [eng.forward(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
+    for o, a in zip(outs, alone):
+        assert torch.equal(o, a)
+    assert eng.read_error_flag() == 0
+    wide[1][0][7, 4] = sizes[13 + 4]  # one past the last row of field 17
+    with torch.no_grad():
+        eng.forward_batches(dev, outs)
+    assert eng.read_error_flag() != 0
+    assert eng.read_error_flag() == 0  # cleared by the read
+    with pytest.raises(ValueError):
+        eng.forward_batches([dev[0], (dev[1][0][:100], dev[1][1][:100])], outs[:2])
+    with pytest.raises((DfwfmError, ValueError)):
+        eng.forward_batches(dev, outs[:2])
+    assert eng.forward_batches([], []) == []

@@ -29,8 +29,15 @@ def workload_of(args):
 
     def opt(name, default):
         return a[a.index(name) + 1] if name in a else default
+    m = int(opt('--batch-set', '20'))
     return f"{opt('--config', 'deepfwfm')}/{opt('--first-order', 'lw')}/scale{opt('--table-scale', '1')}/" \
-           f"{opt('--inputs', 'uniform')}"
+           f"{opt('--inputs', 'uniform')}" + ("/set" if m > 1 else "")
+
+
+def batches_per_launch(args):
+    """bench.py's batches per forward launch under tools/pmc.sh (80 steps, 40 warmup, two streams)."""
+    a = shlex.split(args)
+    return int(a[a.index('--batch-set') + 1]) if '--batch-set' in a else 20
 
 
 vals, durs = {}, {}
@@ -51,6 +58,9 @@ for k, v in vals.items():
          "dispatches": len(durs[k])}
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         e["hbm_bytes_per_launch"] = int(2 * med["FETCH_SIZE"] * 1024 + med["WRITE_SIZE"] * 1024)
+        if wl.endswith("/set"):  # a launch is a set of M batches: bench.py scales the per-batch bytes to its sets
+            e["batches_per_launch"] = batches_per_launch(bench_args)
+            e["hbm_bytes_per_batch"] = e["hbm_bytes_per_launch"] // e["batches_per_launch"]
     if "SQ_VALU_MFMA_BUSY_CYCLES" in med and "GRBM_GUI_ACTIVE" in med:
         e["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (med["GRBM_GUI_ACTIVE"] / 8 * 1024)
     entries.append(e)

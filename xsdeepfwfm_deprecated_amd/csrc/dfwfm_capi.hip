@@ -611,6 +611,53 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   return DFWFM_OK;
 }
 
+int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, int64_t xi_stride,
+                          const float* const* xv, int64_t xv_stride, int64_t batch, float* const* out, void* stream) {
+  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  if (nb < 0) return fail(DFWFM_ERR_INVALID_ARG, "negative batch count");
+  if (nb == 0) return DFWFM_OK;
+  if (!xi || !xv || !out) return fail(DFWFM_ERR_INVALID_ARG, "null pointer array");
+  for (int32_t i = 0; i < nb; ++i) {
+    const int rc = check_inputs(m, xi[i], xi_stride, xv[i], xv_stride, batch, out[i]);
+    if (rc != DFWFM_OK) return rc;
+  }
+  if (batch == 0) return DFWFM_OK;
+  // the opt-in shallow_kernel (DFWFM_SHALLOW) has no batch-set form: one launch per batch
+  if ((m->shallow && !m->big_tables) || nb == 1) {
+    for (int32_t i = 0; i < nb; ++i) {
+      const int rc = dfwfm_forward(m, xi[i], xi_stride, xv[i], xv_stride, batch, out[i], stream);
+      if (rc != DFWFM_OK) return rc;
+    }
+    return DFWFM_OK;
+  }
+  if ((int64_t)nb * ((batch + kBM - 1) / kBM) > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "batch set too large");
+  const bool r32 = use_fwd32(m, (int64_t)nb * batch, stream);
+  const int rows = r32 ? 32 : kBM;
+  for (int32_t i0 = 0; i0 < nb; i0 += kMaxSet) {
+    const int32_t n = nb - i0 < kMaxSet ? nb - i0 : kMaxSet;
+    FwdArgs a;
+    fill_forward_args(m, a, xi[i0], xi_stride, xv[i0], xv_stride, batch, out[i0]);
+    if (const char* pr = getenv("DFWFM_PRIO"); !pr || atoi(pr) != 0) a.flags |= kPrio;
+    a.tail = m->tailI;
+    if (n > 1) {
+      a.nb = n;
+      a.tiles = (int32_t)((batch + rows - 1) / rows);
+      for (int32_t j = 0; j < n; ++j) {
+        a.set_xi[j] = xi[i0 + j];
+        a.set_xv[j] = xv[i0 + j];
+        a.set_out[j] = out[i0 + j];
+      }
+    }
+    int rc = diag_stamps_buffer(m, (int64_t)n * a.tiles * rows, 1, &a.stamps);
+    if (rc != DFWFM_OK) return rc;
+    const hipError_t e = r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
+                                              (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "batch-set forward launch");
+  }
+  return DFWFM_OK;
+}
+
 int dfwfm_forward_workspace_bytes(dfwfm_model* m, int64_t batch, size_t* bytes) {
   if (!m || !bytes || batch < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
   *bytes = (m->split || m->sp) ? split_ws_bytes(m, batch) : 0;

@@ -17,6 +17,23 @@ __device__ __forceinline__ void stamp(uint64_t* st, int slot, int tid) {
   if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
 }
 
+// the batch and first row of this workgroup's tile (ROWS samples per workgroup), and that batch's inputs and logits:
+// the batch set of dfwfm_forward_batches (p.nb > 1), else the one batch of the launch
+struct TileRef {
+  const int64_t* xi;
+  const float* xv;
+  float* out;
+  int64_t b0;
+};
+template <int ROWS>
+__device__ __forceinline__ TileRef tile_ref(const FwdArgs& p) {
+  if (p.nb > 1) {
+    const int bi = (int)blockIdx.x / p.tiles;  // wave-uniform
+    return TileRef{p.set_xi[bi], p.set_xv[bi], p.set_out[bi], (int64_t)((int)blockIdx.x - bi * p.tiles) * ROWS};
+  }
+  return TileRef{p.xi, p.xv, p.out, (int64_t)blockIdx.x * ROWS};
+}
+
 // sum over the 16 lanes of an aligned 16-lane group
 __device__ __forceinline__ float sum16(float v) {
   v += __shfl_xor(v, 8);

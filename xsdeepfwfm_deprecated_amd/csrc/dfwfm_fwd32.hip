@@ -161,7 +161,8 @@ fwd32_kernel(FwdArgs p) {
   float* part2 = smem + L.part2;
   float* tailr = smem + L.tailr;
   float* taild = smem + L.taild;
-  const int64_t b0 = (int64_t)blockIdx.x * kRows;
+  const TileRef tr = tile_ref<kRows>(p);  // batch set: this workgroup's batch
+  const int64_t b0 = tr.b0;
   stamp(p.stamps, 0, tid);
   stamp_start_rt(p.stamps, tid);
   if (flags & kPrio) __builtin_amdgcn_s_setprio(1);
@@ -216,9 +217,9 @@ fwd32_kernel(FwdArgs p) {
     key[k] = 0;
     if (f < F && gb < p.batch) {
       if (f < num)
-        key[k] = __float_as_int(p.xv[gb * p.xv_stride + f]);
+        key[k] = __float_as_int(tr.xv[gb * p.xv_stride + f]);
       else
-        key[k] = p.xi[gb * p.xi_stride + (f - num)];
+        key[k] = tr.xi[gb * p.xi_stride + (f - num)];
     }
   }
   f32x4 uw[kUpkPT];
@@ -583,7 +584,7 @@ fwd32_kernel(FwdArgs p) {
 #pragma unroll
     for (int w = 1; w < kNG; ++w) deepv += dsum[w * kRows + tid];
     deepv += ((taild[tid] + taild[kRows + tid]) + taild[2 * kRows + tid]) + taild[3 * kRows + tid];
-    p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
+    tr.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
   stamp(p.stamps, 8, tid);
   stamp_end_rt(p.stamps, tid);
@@ -602,7 +603,7 @@ hipError_t launch_fwd32(const FwdArgs& a, int D, size_t lds, hipStream_t s) {
   auto k = (a.flags & kHasQR) ? fwd32_kernel<10, true> : fwd32_kernel<10, false>;
   hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
   if (e != hipSuccess) return e;
-  const unsigned grid = (unsigned)((a.batch + kRows - 1) / kRows);
+  const unsigned grid = fwd_grid(a, kRows);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kNTH), lds, s, a);
   return hipGetLastError();
 }

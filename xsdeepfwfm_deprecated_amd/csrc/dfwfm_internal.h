@@ -30,6 +30,7 @@ constexpr int kPrio = 256;     // raise the wave priority for the phases before 
 constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables; shallow_kernel's QR loads)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kMaxH = 16;      // hidden layers
+constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)
 
 // Device copy of dfwfm_field_tables (same field order and sizes); for QR fields
 // n holds the accepted index bound ceil(n/c)*c.
@@ -93,7 +94,21 @@ struct FwdArgs {
   uint8_t fw_list8[kMaxPieces];
   uint8_t fw_off4[5];
   uint8_t fw_off8[9];
+  // batch set (dfwfm_forward_batches): nb > 1 -> workgroup w runs tile w % tiles of batch w / tiles, whose inputs
+  // and logits are set_xi / set_xv / set_out[w / tiles] (every batch `batch` rows, the strides above); nb <= 1:
+  // one batch at xi / xv / out
+  int32_t nb;
+  int32_t tiles;            // workgroups per batch
+  const int64_t* set_xi[kMaxSet];
+  const float* set_xv[kMaxSet];
+  float* set_out[kMaxSet];
 };
+
+// workgroups of a forward launch with `rows` samples per workgroup
+inline unsigned fwd_grid(const FwdArgs& a, int rows) {
+  const unsigned tiles = (unsigned)((a.batch + rows - 1) / rows);
+  return a.nb > 1 ? (unsigned)a.nb * tiles : tiles;
+}
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.
 struct LdsLayout {

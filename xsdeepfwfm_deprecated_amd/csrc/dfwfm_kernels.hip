@@ -105,7 +105,8 @@ fwd_kernel(FwdArgs p) {
   float* dsum = smem + L.dsum;
   float* fs = smem + L.fs;
 
-  const int64_t b0 = (int64_t)blockIdx.x * kBM;
+  const TileRef tr = tile_ref<kBM>(p);  // batch set: this workgroup's batch
+  const int64_t b0 = tr.b0;
   stamp(p.stamps, 0, tid);
   stamp_start_rt(p.stamps, tid);
   // gather / shallow phases at a raised priority: beside a co-resident workgroup's MLP they would otherwise
@@ -220,9 +221,9 @@ fwd_kernel(FwdArgs p) {
     key[k] = 0;
     if (f < F && gb < p.batch) {
       if (f < num)
-        key[k] = __float_as_int(p.xv[gb * p.xv_stride + f]);
+        key[k] = __float_as_int(tr.xv[gb * p.xv_stride + f]);
       else
-        key[k] = p.xi[gb * p.xi_stride + (f - num)];
+        key[k] = tr.xi[gb * p.xi_stride + (f - num)];
     }
   }
   f32x4 uw[kUpkPT];
@@ -606,7 +607,7 @@ fwd_kernel(FwdArgs p) {
     if constexpr (PART == 1) {
       if (tid < kBM && b0 + tid < p.batch) p.part_fs[b0 + tid] = fs[tid];
     } else {
-      if (tid < kBM && b0 + tid < p.batch) p.out[b0 + tid] = fs[tid] + p.bias[0];
+      if (tid < kBM && b0 + tid < p.batch) tr.out[b0 + tid] = fs[tid] + p.bias[0];
     }
     stamp(p.stamps, 8, tid);
     stamp_end_rt(p.stamps, tid);
@@ -800,7 +801,7 @@ fwd_kernel(FwdArgs p) {
     for (int w = 1; w < NG; ++w) deepv += dsum[w * kBM + tid];
     if (tail) deepv += ((tailr[NG * 64 * 4 + tid] + tailr[NG * 64 * 4 + kBM + tid]) +
                         tailr[NG * 64 * 4 + 2 * kBM + tid]) + tailr[NG * 64 * 4 + 3 * kBM + tid];
-    p.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
+    tr.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
   }
   stamp(p.stamps, 8, tid);
   stamp_end_rt(p.stamps, tid);
@@ -897,7 +898,7 @@ static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, hipStream_t s) {
     hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
     if (e != hipSuccess) return e;
   }
-  const unsigned grid = (unsigned)((a.batch + kBM - 1) / kBM);
+  const unsigned grid = fwd_grid(a, kBM);
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NG * KS), lds, s, a);
   return hipGetLastError();
 }
@@ -960,7 +961,7 @@ static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t
                                                             true, (a.flags & kFoFwlw) != 0).total;
     hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds3);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3((unsigned)((a.batch + kBM - 1) / kBM)), dim3(64 * ng), lds3, s, a);
+    hipLaunchKernelGGL(k, dim3(fwd_grid(a, kBM)), dim3(64 * ng), lds3, s, a);
     return hipGetLastError();
   }
   if (a.flags & kTrain) return ng == 8 ? launch_fwd_8<D, 0, true>(a, tpw, lds, s) : launch_fwd_k<D, 1, true>(a, tpw, lds, s);

@@ -160,6 +160,34 @@ class ForwardEngine:
         _lib.check(rc, "dfwfm_forward")
         return out
 
+    def forward_batches(self, batches, outs) -> list:
+        """dfwfm_forward_batches: the forward of every (xi, xv) in `batches` (same batch size and row strides),
+        all in one launch per 32 batches; logits into outs[i], bit-identical to forward() on each batch alone."""
+        nb = len(batches)
+        if nb == 0:
+            return outs
+        if len(outs) != nb:
+            raise ValueError("forward_batches: one output per batch")
+        ncat = self.cfg["field_size"] - self.cfg["numerical"]
+        num = self.cfg["numerical"]
+        xi0, xv0 = batches[0]
+        B = xi0.shape[0]
+        xs = xi0.stride(0) if ncat > 0 else 0
+        vs = xv0.stride(0) if num > 0 else 0
+        for xi, xv in batches:
+            if xi.shape[0] != B or (ncat > 0 and xi.stride(0) != xs) or (num > 0 and xv.stride(0) != vs):
+                raise ValueError("forward_batches: every batch needs the same size and row strides")
+        for o in outs:
+            if o.numel() < B:
+                raise ValueError("forward_batches: output smaller than the batch")
+        P = ctypes.c_void_p * nb
+        pxi = P(*[xi.data_ptr() for xi, _ in batches])
+        pxv = P(*[xv.data_ptr() for _, xv in batches])
+        pout = P(*[o.data_ptr() for o in outs])
+        rc = _lib.lib().dfwfm_forward_batches(self.handle, nb, pxi, xs, pxv, vs, B, pout, _stream_handle(self.device))
+        _lib.check(rc, "dfwfm_forward_batches")
+        return outs
+
     def _ws_bytes(self, B: int) -> int:
         cache = self.__dict__.setdefault("_ws_cache", {})
         if B not in cache:
