@@ -73,7 +73,7 @@ def parse():
                     help="give even-numbered streams one half of the CUs and odd-numbered streams the other (HIP CU "
                          "masks): with 32-sample workgroups a batch is 128 workgroups, one per CU of a half, so two "
                          "batches share each CU (default: even-odd with the 32-sample forward, else none)")
-    ap.add_argument("--batch-set", type=int, default=20,
+    ap.add_argument("--batch-set", type=int, default=32,
                     help="batches per forward launch (dfwfm_forward_batches: one grid over that many resident "
                          "batches, each batch its own inputs and logits); 1: one launch per batch (graph replay, "
                          "CU-masked stream pairs for the 32-sample forward)")
@@ -283,14 +283,16 @@ def main():
     # deep configs: four batches in flight on CU-masked stream pairs (even / odd CU ids): a 4096-row batch is 128
     # 32-sample workgroups, which cover a half, so the library runs fwd32_kernel and every CU holds two batches
     # (DESIGN.md section 3); DFWFM_R32=0: the 16-sample kernel on two plain streams
-    # batch sets (default): every launch is one grid over M resident batches on the whole chip (the 32-sample
-    # forward for the deep configs: a set's workgroups cover every CU twice over), two streams so that the next
-    # set's workgroups take the CU slots the current one frees while it drains.  --batch-set 1: one launch per
-    # batch from captured graphs; the deep configs then run four batches in flight on CU-masked stream pairs
+    # batch sets (default): every launch is one grid over up to M resident batches on the whole chip (the
+    # 32-sample forward for the deep configs: a set's workgroups cover every CU twice over); when the K steps
+    # fit one set they are ONE launch, else two streams, so that the next set's workgroups take the CU slots
+    # the current one frees while it drains.  --batch-set 1: one launch per batch from captured graphs; the deep
+    # configs then run four batches in flight on CU-masked stream pairs
     M = max(1, a.batch_set)
     r32_default = deep and os.environ.get("DFWFM_R32", "") != "0"
     cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32_default and M == 1 else "none")
-    S = max(1, a.streams if a.streams is not None else (2 if M > 1 else (3 if not deep else (4 if r32_default else 2))))
+    S = max(1, a.streams if a.streams is not None else
+            ((1 if a.steps <= M else 2) if M > 1 else (3 if not deep else (4 if r32_default else 2))))
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
     set_outs = [[torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(M)] for _ in range(S)] \
         if M > 1 else None
@@ -386,7 +388,7 @@ def main():
         # settle: untimed back-to-back forwards until the chip has run them for --settle-ms (its clock ramps
         # over the first few hundred forwards); then the W warmup steps, then the K timed steps
         settle_n, settle_t0 = 0, time.perf_counter()
-        chunk = max(S * G, 8)
+        chunk = S * min(M, max(per_stream(a.steps))) if M > 1 else max(S * G, 8)  # settle launches = timed ones
         while a.settle_ms > 0:
             run_n(chunk)
             settle_n += chunk

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over bench.py's own command (hipGraph replay, its streams; rocprofv3 --pmc serialises the dispatches
-# it counts), one counter group per pass, kernel-trace counters only (no sys / runtime trace).  80 steps after 40
-# warmup: with batch sets of M <= 20 on two streams every launch holds M batches.
+# it counts), one counter group per pass, kernel-trace counters only (no sys / runtime trace).  64 steps after 64
+# warmup: with the default batch sets (32) on two streams every launch holds 32 batches.
 #   TAG=r03e BENCH_ARGS="--config fwfm --table-scale 8" bash tools/pmc.sh
 # then: python tools/pmc_summary.py TAG gpurun_out profiles/pmc_traffic.json "$BENCH_ARGS"
 set -u
@@ -13,7 +13,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 -s KILL 150 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 80 --warmup 40 --settle-ms 0 --no-gate --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_${TAG}_$i.log 2>&1
+  timeout -k 10 -s KILL 150 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 64 --warmup 64 --settle-ms 0 --no-gate --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_${TAG}_$i.log 2>&1
   rc=$?
   echo "pass $i [$grp] rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi

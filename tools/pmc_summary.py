@@ -29,15 +29,15 @@ def workload_of(args):
 
     def opt(name, default):
         return a[a.index(name) + 1] if name in a else default
-    m = int(opt('--batch-set', '20'))
+    m = int(opt('--batch-set', '32'))
     return f"{opt('--config', 'deepfwfm')}/{opt('--first-order', 'lw')}/scale{opt('--table-scale', '1')}/" \
            f"{opt('--inputs', 'uniform')}" + ("/set" if m > 1 else "")
 
 
 def batches_per_launch(args):
-    """bench.py's batches per forward launch under tools/pmc.sh (80 steps, 40 warmup, two streams)."""
+    """bench.py's batches per forward launch under tools/pmc.sh (64 steps, 64 warmup, two streams)."""
     a = shlex.split(args)
-    return int(a[a.index('--batch-set') + 1]) if '--batch-set' in a else 20
+    return int(a[a.index('--batch-set') + 1]) if '--batch-set' in a else 32
 
 
 vals, durs = {}, {}
