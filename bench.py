@@ -182,7 +182,8 @@ def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
     if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
             return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
-        ng = 4 if os.environ.get("DFWFM_P3_NG") == "4" else 8
+        png = os.environ.get("DFWFM_P3_NG")
+        ng = 4 if png == "4" or (png is None and batch_set > 1) else 8  # batch sets: four waves
         return f"dfwfm::fwd_kernel<10,1,1,false,3,{ng},3,false>"  # MLP-free, 3 FwFM row tiles, no QR field
     ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
     tpw = 6 if ng == 4 else 3

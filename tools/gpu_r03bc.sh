@@ -13,6 +13,7 @@ run fwfm20 300 python bench.py --config fwfm --steps 20 --warmup 5 --no-cpu-base
 run fwfm2000 300 python bench.py --config fwfm --steps 2000 --warmup 400 --no-cpu-baseline || exit 1
 run qr20 300 python bench.py --config qr --steps 20 --warmup 5 --no-cpu-baseline || exit 1
 run pruned20 300 python bench.py --config pruned --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+run prof_fwfm20 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_proff -o run --output-format csv -- python3 bench.py --config fwfm --steps 20 --warmup 5 --no-cpu-baseline || exit 1
 run fwfm20s8 300 python bench.py --config fwfm --steps 20 --warmup 5 --table-scale 8 --no-cpu-baseline || exit 1
 run fwfm2000s8 300 python bench.py --config fwfm --steps 2000 --warmup 400 --table-scale 8 --no-cpu-baseline || exit 1
 TAG=${T}pmc BENCH_ARGS="" bash tools/pmc.sh || exit 1

@@ -74,7 +74,8 @@ __device__ __forceinline__ void mfma_chunk_rt(f32x4 (&acc)[RT][TPW], const float
 template <int TPW, int RT, int NG, int NS>
 __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __restrict__ act, int SA,
                                           const LayerStream<TPW, 1, NG>& ls, f32x4 (&b0)[TPW], f32x4 (&b1)[TPW],
-                                          f32x4 (&b2)[TPW], int lane, const TailStream<NG>& ts, f32x4 (&tp)[RT]) {
+                                          f32x4 (&b2)[TPW], int lane, const TailStream<NG>& ts, f32x4 (&tp)[RT],
+                                          bool mid_barrier) {
   const int voff = lane * 16;
   const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
   float4 a0[RT], a1[RT], a2[RT];
@@ -89,6 +90,7 @@ __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __
     f32x4 (&Z)[TPW] = (i % 3 == 0) ? b2 : ((i % 3 == 1) ? b0 : b1);
     float4 (&AX)[RT] = (i % 3 == 0) ? a0 : ((i % 3 == 1) ? a1 : a2);
     float4 (&AZ)[RT] = (i % 3 == 0) ? a2 : ((i % 3 == 1) ? a0 : a1);
+    if (i + 3 == NS && mid_barrier) __syncthreads();  // the previous layer's split tile (chunk NS - 1) is written
     if (i + 2 < NS) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) AZ[rt] = *reinterpret_cast<const float4*>(arow + rt * 16 * SA + 16 * (i + 2));
@@ -508,7 +510,10 @@ fwd32_kernel(FwdArgs p) {
       for (int j = 0; j < kTPW; ++j) acc[rt][j] = bq[j];
     ts.init(layer_off, NC, TT, g);
     f32x4 tp[kRT];
-    k_loop_rt<kTPW, kRT, kNG, kNS>(acc, buf, SX, ls, wb0, wb1, wb2, lane, ts, tp);
+    // kDeferTail: the barrier after the split tile's reduction waits inside this K loop, right before chunk NS - 1
+    // (the split tile's columns) is read -- until then the waves that did not reduce run their MFMAs
+    k_loop_rt<kTPW, kRT, kNG, kNS>(acc, buf, SX, ls, wb0, wb1, wb2, lane, ts, tp, h > 0 && (flags & kDeferTail));
+    if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(1);
     if (h == 0) stamp(p.stamps, 12, tid);
     __syncthreads();  // every wave has read the layer's input: the tile may be overwritten
 #pragma unroll
@@ -575,7 +580,8 @@ fwd32_kernel(FwdArgs p) {
         }
       }
     }
-    __syncthreads();
+    if (last || !(flags & kDeferTail)) __syncthreads();
+    if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(0);
     stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
   }
 

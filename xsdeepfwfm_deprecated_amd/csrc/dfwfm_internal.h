@@ -28,6 +28,8 @@ constexpr int kTrain = 64;     // save the activations the backward needs (FwdAr
 constexpr int kDrop = 128;     // dropout on the deep tower (train only)
 constexpr int kPrio = 256;     // raise the wave priority for the phases before the MLP (A/B: DFWFM_PRIO)
 constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables; shallow_kernel's QR loads)
+constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
+constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kMaxH = 16;      // hidden layers
 constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)

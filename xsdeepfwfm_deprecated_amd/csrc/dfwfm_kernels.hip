@@ -943,7 +943,9 @@ static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t
     // spill the QR rows' second operands)
     const char* png = getenv("DFWFM_P3_NG");
     const bool qr = (a.flags & kHasQR) != 0;
-    const bool w8 = qr || !png || atoi(png) != 4;
+    // batch sets (a.nb > 1): four waves -- with the CU slots refilled across batch boundaries, five four-wave
+    // workgroups per CU beat three eight-wave ones (2.52 vs 2.92 us per batch, profiles/r03/r03be_*)
+    const bool w8 = qr || (png ? atoi(png) != 4 : a.nb <= 1);
     auto pick = [&](auto ng_, auto qr_) {
       constexpr int NG = decltype(ng_)::value;
       constexpr bool Q = decltype(qr_)::value;
