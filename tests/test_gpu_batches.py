@@ -134,3 +134,26 @@ def test_batch_set_fwd32_schedule_variants_bit_identical(gpu, monkeypatch, env):
             eng.forward_batches(dev, outs)
         res[v] = torch.stack(outs).cpu().numpy()
     assert np.array_equal(res["0"], res["1"])
+
+
+@pytest.mark.parametrize("deep", [1, 0])
+def test_eval_by_batch_batch_sets_identical(gpu, deep):
+    """eval_by_batch's full 8192-row batches as batch sets give the same loss and metrics as one forward per batch
+    (reference model/DeepFMs.py:750-784), and an out-of-range index in one of them still raises IndexError."""
+    from xsdeepfwfm_deprecated_amd import synth
+    cfg, params, m = _criteo_model(gpu, deep, 0, seed=31)
+    n = 3 * 8192 + 100
+    xi, xv = synth.synth_inputs(cfg["feature_sizes"], 13, n, seed=8)
+    y = (np.random.default_rng(2).random(n) < 0.3).astype(np.float32)
+    res = {}
+    for on in (True, False):
+        m.eval_batch_sets = on
+        res[on] = m.eval_by_batch(xi.reshape(n, 26, 1), xv, y, n)
+    # loss and AUC exactly; PR-AUC / RCE up to the device metrics' own float64 summation order
+    assert res[True][:2] == res[False][:2]
+    assert np.allclose(res[True][2:], res[False][2:], rtol=1e-12, atol=0)
+    m.eval_batch_sets = True
+    bad = xi.copy()
+    bad[8192 + 5, 2] = -1
+    with pytest.raises(IndexError):
+        m.eval_by_batch(bad.reshape(n, 26, 1), xv, y, n)

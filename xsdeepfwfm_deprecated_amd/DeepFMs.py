@@ -95,6 +95,7 @@ class DeepFMs(nn.Module):
         self.md_flag = md_flag
         self.md_threshold = md_threshold
         self.strict_index_check = True  # raise IndexError for out-of-range Xi (the kernel's sticky flag)
+        self.eval_batch_sets = True  # eval_by_batch runs its full batches as batch sets (dfwfm_forward_batches)
         # inference over pruned hidden layers: the sparse MLP (dfwfm_spmlp.hip) when at most this fraction
         # of their weights is nonzero; 0 (default) keeps the dense MFMA kernel, which is faster at the
         # reference's 90 % masks (34.7 vs 100 us per batch)
@@ -412,7 +413,22 @@ class DeepFMs(nn.Module):
         logits = torch.empty(x_size, dtype=torch.float32, device=dev)
         total_loss = torch.zeros((), dtype=torch.float64, device=dev)
         with torch.no_grad(), self.deferred_index_check():
-            for off in range(0, x_size, bs):
+            off = 0
+            if dev.type == "cuda" and self.eval_batch_sets and x_size >= 2 * bs:
+                # the full batches as batch sets (dfwfm_forward_batches: up to 32 resident batches per launch, the
+                # same logits as one forward each); the sparse-MLP / pair-list variants keep one forward per batch
+                eng = self._sync_engine(dev)
+                alt = eng.sync_sparse(self.sparse_mlp_max_density) if self.use_deep else (
+                    eng.sync_pairs(self.fwfm_pair_max) if self.use_fwfm else False)
+                if not alt:
+                    nfull = x_size // bs
+                    eng.forward_batches([(Xi_d[i * bs:(i + 1) * bs], Xv_d[i * bs:(i + 1) * bs]) for i in range(nfull)],
+                                        [logits[i * bs:(i + 1) * bs] for i in range(nfull)])
+                    for i in range(nfull):
+                        sl = slice(i * bs, (i + 1) * bs)
+                        total_loss += F.binary_cross_entropy_with_logits(logits[sl], y_d[sl]).double() * bs
+                    off = nfull * bs
+            for off in range(off, x_size, bs):
                 end = min(x_size, off + bs)
                 out = self(Xi_d[off:end], Xv_d[off:end])
                 logits[off:end] = out
