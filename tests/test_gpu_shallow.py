@@ -1,7 +1,6 @@
 """GPU: the forward without a deep tower -- the FwFM-only config of BASELINE configs[0]: the default
-MLP-free fwd_kernel (PART 3, per-sample Gram FwFM) and the opt-in shallow_kernel (csrc/dfwfm_shallow.hip,
-DFWFM_SHALLOW=1 at model creation) against the oracle; shallow_kernel bit-identical to the generic fused
-kernel (DFWFM_NO_PART3=1)."""
+MLP-free fwd_kernel (PART 3, per-sample Gram FwFM) and the generic fused kernel (DFWFM_NO_PART3=1) against the
+oracle."""
 import numpy as np
 import pytest
 import torch
@@ -40,9 +39,8 @@ def _err(got, ref, cfg, params, xi, xv):
     return logit_close_scaled(got, ref, cfg, params, xi, xv)
 
 
-def _model(cfg, params, dev, monkeypatch, shallow):
+def _model(cfg, params, dev, monkeypatch, unused=False):
     from xsdeepfwfm_deprecated_amd import DeepFMs
-    monkeypatch.setenv("DFWFM_SHALLOW", "1" if shallow else "0")
     m = DeepFMs(**model_kwargs(cfg))
     m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     m = m.to(dev).eval()
@@ -77,48 +75,17 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
-def test_shallow_kernel_matches_oracle_and_fused(gpu, monkeypatch, case):
+def test_mlp_free_kernels_match_oracle(gpu, monkeypatch, case):
+    """The default MLP-free kernel (per-sample Gram FwFM) and the generic fused kernel (DFWFM_NO_PART3: the
+    piece-wise FwFM) against the oracle over the configs without a deep tower."""
     cfg, params, xi, xv = _case(**case, seed=len(str(case)))
-    got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
-    # bit-identical to the generic fused kernel (DFWFM_NO_PART3: the piece-wise FwFM, same arithmetic) ...
-    monkeypatch.setenv("DFWFM_NO_PART3", "1")
-    fused = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
-    monkeypatch.delenv("DFWFM_NO_PART3")
-    assert np.array_equal(got, fused)
-    # ... and the default MLP-free kernel (per-sample Gram FwFM, another summation order) within the bar
-    part3 = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
+    part3 = _run(_model(cfg, params, gpu, monkeypatch), xi, xv, gpu)
     assert _err(part3, ref, cfg, params, xi, xv) < 1e-5
-
-
-@pytest.mark.parametrize("B", [1, 15, 16, 17, 255, 4096 + 3])
-def test_shallow_kernel_ragged_batches(gpu, monkeypatch, B):
-    cfg, params, xi, xv = _case(39, 13, 10, B=B, seed=B)
-    got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
-    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
-    # a row's logit does not depend on its tile or slot
-    one = _run(_model(cfg, params, gpu, monkeypatch, True), xi[B - 1:], xv[B - 1:], gpu)
-    assert one[0] == got[B - 1]
-
-
-def test_shallow_kernel_full_size_tables(gpu, monkeypatch):
-    """Criteo-39 field sizes (1.33 M rows), B = 4096: the bench workload."""
-    cfg, params, xi, xv = _case(39, 13, 10, B=4096, big=True, seed=7)
-    got = _run(_model(cfg, params, gpu, monkeypatch, True), xi, xv, gpu)
-    ref = dfwfm_oracle.forward(cfg, params, xi, xv)
-    assert _err(got, ref, cfg, params, xi, xv) < 1e-5
-
-
-@pytest.mark.parametrize("bad", [-1, "n"])
-def test_shallow_kernel_index_out_of_range_raises(gpu, monkeypatch, bad):
-    cfg, params, xi, xv = _case(39, 13, 10, B=64, seed=3)
-    xi = xi.copy()
-    xi[37, 5] = -1 if bad == -1 else cfg["feature_sizes"][13 + 5]
-    m = _model(cfg, params, gpu, monkeypatch, True)
-    with pytest.raises(IndexError):
-        _run(m, xi, xv, gpu)
+    monkeypatch.setenv("DFWFM_NO_PART3", "1")
+    fused = _run(_model(cfg, params, gpu, monkeypatch), xi, xv, gpu)
+    monkeypatch.delenv("DFWFM_NO_PART3")
+    assert _err(fused, ref, cfg, params, xi, xv) < 1e-5
 
 
 @pytest.mark.parametrize("B", [1, 17, 4096 + 3])

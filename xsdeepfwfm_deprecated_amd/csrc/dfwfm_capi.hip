@@ -30,8 +30,6 @@ struct dfwfm_model {
   int cu_count[8], cu_n, cu_next;
   size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
   int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
-  int shallow;         // no deep tower: shallow_kernel (dfwfm_shallow.hip) runs the inference forward
-  int big_tables;      // some table has >= 2^31 rows (shallow_kernel then yields to fwd_kernel)
   // sparse deep tower (dfwfm_model_build_sparse_mlp): ELL of the pruned weights, used by dfwfm_forward_ws
   int sp;                          // enabled (cleared by set_dense: the ELL is then stale)
   const float* lin_w[kMaxH];       // the caller's weights from the last set_dense
@@ -282,11 +280,6 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   // fused launch (50.4 vs 43.0 us per batch alone, 43.4 vs 35.5 with two batches in flight): under a
   // co-resident MLP's weight stream the gather launch's dependent loads wait ~3x longer, and in the
   // fused kernel that wait is hidden behind the other workgroup's MLP instead of serialised
-  // no deep tower: fwd_kernel's four-wave shallow path; DFWFM_SHALLOW=1 selects shallow_kernel
-  // (dfwfm_shallow.hip, bit-identical; measured slower at three batches in flight: 6.8 vs 5.2 us per
-  // batch)
-  const char* sh = getenv("DFWFM_SHALLOW");
-  m->shallow = (!c.use_deep && sh && atoi(sh) != 0) ? 1 : 0;
   const char* sp = getenv("DFWFM_SPLIT");
   m->split = (c.use_deep && m->KS == 1 && sp && atoi(sp) != 0) ? 1 : 0;
   if (m->lds_bytes > 160 * 1024 || m->lds_inf > 160 * 1024) {
@@ -365,11 +358,8 @@ int dfwfm_model_set_tables(dfwfm_model* m, const dfwfm_field_tables* t, int32_t 
     if (host[f].c > 0) host[f].n = (host[f].n + host[f].c - 1) / host[f].c * host[f].c;
   memcpy(m->h_fields, host, sizeof(FieldDev) * n);
   m->flags &= ~kHasQR;
-  m->big_tables = 0;
-  for (int f = 0; f < n; ++f) {
+  for (int f = 0; f < n; ++f)
     if (host[f].c > 0) m->flags |= kHasQR;
-    if (host[f].n > 0x7fffffff) m->big_tables = 1;  // shallow_kernel indexes rows in 32 bits
-  }
   HIP_TRY(hipMemcpyAsync(m->d_fields, host, sizeof(FieldDev) * n, hipMemcpyHostToDevice, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // `host` is a stack buffer
   m->tables_set = true;
@@ -605,8 +595,7 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
-  hipError_t e = (m->shallow && !m->big_tables) ? launch_shallow(a, m->D, m->lds_gather, (hipStream_t)stream)
-                 : use_fwd32(m, batch, stream) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+  hipError_t e = use_fwd32(m, batch, stream) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
                                              (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
@@ -624,8 +613,7 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     if (rc != DFWFM_OK) return rc;
   }
   if (batch == 0) return DFWFM_OK;
-  // the opt-in shallow_kernel (DFWFM_SHALLOW) has no batch-set form: one launch per batch
-  if ((m->shallow && !m->big_tables) || nb == 1) {
+  if (nb == 1) {
     for (int32_t i = 0; i < nb; ++i) {
       const int rc = dfwfm_forward(m, xi[i], xi_stride, xv[i], xv_stride, batch, out[i], stream);
       if (rc != DFWFM_OK) return rc;

@@ -27,7 +27,7 @@ constexpr int kNeedE = 32;     // second-order / deep embeddings are gathered
 constexpr int kTrain = 64;     // save the activations the backward needs (FwdArgs::sv_*)
 constexpr int kDrop = 128;     // dropout on the deep tower (train only)
 constexpr int kPrio = 256;     // raise the wave priority for the phases before the MLP (A/B: DFWFM_PRIO)
-constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables; shallow_kernel's QR loads)
+constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables)
 constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
 constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
@@ -395,8 +395,6 @@ hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
 // the split forward's first launch alone (gather + shallow part -> a.part_e / a.part_fs)
 hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream_t s);
-// the forward without a deep tower (dfwfm_shallow.hip); lds: lds_layout(..., deep = false)
-hipError_t launch_shallow(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 // the fused inference forward on 32-sample workgroups (dfwfm_fwd32.hip): both 16-row tiles per wave in the MLP;
 // the static 3x400 form only (fwd32_supported), bit-identical logits to fwd_kernel's
