@@ -340,7 +340,7 @@ def _fit_small(batch_size):
 def test_data_parallel_fit_two_ranks(gpu):
     """config 5 semantics on one GPU: two gloo ranks (both on cuda:0) run fit with batch 256 each; every
     rank ends with bit-identical weights, and training matches one process on the global batch of 512
-    (same init and shuffles; float summation order differs)."""
+    (same init and shuffles; float summation order differs) to ~1e-6."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -358,10 +358,12 @@ def test_data_parallel_fit_two_ranks(gpu):
     (tr0, w0), (tr1, w1) = res[0], res[1]
     assert all(np.array_equal(w0[k], w1[k]) for k in w0)  # replicas stay identical
     tr_single, w_single = _fit_small(batch_size=512)
-    assert abs(tr0[-1] - tr_single[-1]) < 5e-3, (tr0, tr_single)
     num = sum(float(np.abs(w0[k] - w_single[k]).sum()) for k in w0)
     den = sum(float(np.abs(w_single[k]).sum()) for k in w0)
-    assert num / den < 1e-2, num / den
+    # measured on MI355X (profiles/r03/r03bj_dp_fit.log): final train loss 1.2e-7 apart, parameters 7.7e-8 relative
+    # L1 after 2 epochs (16 steps; only the fp32 summation order of the exchange differs) -- bars ~25-100x that
+    assert abs(tr0[-1] - tr_single[-1]) < 1e-5 * max(1.0, abs(tr_single[-1])), (tr0, tr_single)
+    assert num / den < 2e-6, num / den
 
 
 @pytest.mark.parametrize("D,N,H,fwlw", [(4, 256, 1, 0), (16, 512, 2, 0), (8, 96, 3, 1), (10, 144, 2, 1),
@@ -705,7 +707,10 @@ def test_data_parallel_step_equals_single_process_global_batch(gpu, name):
         sc = np.abs(gs[k]).max()
         assert np.abs(g0[k] - gs[k]).max() <= G_TOL * sc + 1e-12, k
     e = np.concatenate([np.abs(p0[k] - ps[k]).reshape(-1) / 1e-3 for k in ps])
-    assert np.median(e) < 1e-4 and np.quantile(e, 0.999) < 0.02, (np.median(e), np.quantile(e, 0.999))
+    # parameters after 3 steps in lr units (measured, profiles/r03/r03bk_dp_step.log: median 0, 99.9th percentile
+    # 7.5e-6, max 3.1e-4 -- Adam's m / sqrt(v) magnifies the exchange's fp32 reassociation on near-zero gradients)
+    assert np.median(e) < 1e-6 and np.quantile(e, 0.999) < 1e-4 and e.max() < 2e-3, \
+        (np.median(e), np.quantile(e, 0.999), e.max())
     resd = _run_dp(name, False, 1)  # dense exchange (all-reduce of the whole buffer)
     (gd, od), _ = resd[0]
     for k in gs:
