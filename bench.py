@@ -107,7 +107,9 @@ class _HostGate:
     the GPU runs): a gate held until an unbounded number of commands is queued could fill the hardware queue,
     and the host would then block inside a launch without ever reaching release()."""
 
-    def __init__(self, streams):
+    def __init__(self):
+        # allocated ahead of the warmup: the GPU idles from the warmup's end to release(), and an idle GPU lowers
+        # its clock within milliseconds (a 20 ms gap cost 13 % of a 20-step region, profiles/r03/r03bm_*)
         import ctypes
         self._hip = _hip_runtime()
         if self._hip is None:
@@ -118,6 +120,9 @@ class _HostGate:
             raise RuntimeError(f"hipHostMalloc: {rc}")
         self._word = ctypes.cast(self._p, ctypes.POINTER(ctypes.c_uint32))
         self._word[0] = 0
+
+    def arm(self, streams):
+        import ctypes
         for stream in streams:  # flags 0 = hipStreamWaitValueGte
             rc = self._hip.hipStreamWaitValue32(ctypes.c_void_p(stream.cuda_stream), self._p, ctypes.c_uint32(1),
                                                 ctypes.c_uint(0), ctypes.c_uint32(0xFFFFFFFF))
@@ -397,15 +402,12 @@ def main():
             if (time.perf_counter() - settle_t0) * 1e3 >= a.settle_ms:
                 break
         settle_ms = (time.perf_counter() - settle_t0) * 1e3
-        run_n(a.warmup)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize(dev)
-        # per-stream events: a launch's duration while S run side by side (what rocprofv3 reports)
+        # per-stream events: a launch's duration while S run side by side (what rocprofv3 reports); everything
+        # the timed region needs is created before the warmup, so that the GPU's idle gap between the warmup's end
+        # and the region's start is only the synchronisation and the enqueue (reported as idle_before_region_us)
         s0 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
         s1 = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
-        wall0 = time.perf_counter()
+        wend = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
         # the K steps are enqueued behind a device-side wait on a host flag (one wait per stream, one
         # flag), released once everything is queued: the timed region measures the GPU running K forwards,
         # not the host submitting graphs.  The region runs from the earliest stream's start event to the
@@ -414,9 +416,21 @@ def main():
         gate = None
         if not a.no_gate:
             try:
-                gate = _HostGate(streams)
+                gate = _HostGate()
             except (OSError, RuntimeError) as e:  # no gate on this runtime: time as --no-gate does
                 print(f"bench: host gate unavailable ({e}); timing without it", file=sys.stderr)
+        run_n(a.warmup)
+        for k, st in enumerate(streams):
+            wend[k].record(st)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        if os.environ.get("DFWFM_BENCH_IDLE_MS"):  # diagnostics: an idle gap before the timed region
+            time.sleep(float(os.environ["DFWFM_BENCH_IDLE_MS"]) / 1e3)
+        wall0 = time.perf_counter()
+        if gate is not None:
+            gate.arm(streams)
         for k, st in enumerate(streams):
             if k and gate is None:
                 st.wait_stream(streams[0])
@@ -440,6 +454,7 @@ def main():
     first = min(range(S), key=lambda k: s0[0].elapsed_time(s0[k]))
     last = max(range(S), key=lambda k: s0[0].elapsed_time(s1[k]))
     ms = s0[first].elapsed_time(s1[last])
+    idle_us = max(0.0, -max(s0[first].elapsed_time(w) for w in wend) * 1e3)  # last warmup end -> region start
     # per launch, S side by side (what rocprofv3 reports); a launch is one batch, or a set of up to M
     units = BATCH * (min(M, max(per_stream(a.steps))) if M > 1 else 1)
     n_launch = sum(-(-n // M) for n in per_stream(a.steps)) if M > 1 else a.steps
@@ -509,6 +524,7 @@ def main():
                    "what": "untimed back-to-back forwards before the warmup steps (clock ramp)"},
         "wall_s": round(wall, 4),
         "streams_in_region": skew,
+        "idle_before_region_us": round(idle_us, 1),
     }
     mfma = {"bound": mfma_bound, "achieved": round(achieved_tf, 3), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved_tf / PEAK_F32_MFMA_TFLOPS, 4), "flops_per_sample": flops}
