@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=20, help="forwards captured per hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-call", action="store_true",
+                    help="skip the per_call leg (one forward call per batch, sequential on one stream)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU sample per thread count")
     ap.add_argument("--inputs", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--table-scale", type=int, default=1,
@@ -275,15 +277,6 @@ def main():
         torch.cuda.synchronize(dev)
         params = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
 
-    n_bufs = 8  # distinct resident batches, rotated, so gathers are not L2-hot repeats
-    batches = []
-    for i in range(n_bufs):
-        seed = 1000 * rank + i
-        if a.inputs == "zipf":
-            xi, xv = synth.zipf_inputs(sizes, 13, BATCH, seed=seed)
-        else:
-            xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=seed)
-        batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
     # batches in flight: 2 fill the CUs' register files for the deep configs (two eight-wave workgroups per
     # CU); the FwFM-only forward is latency-bound and gains from a third (three eight-wave workgroups per CU)
     # deep configs: four batches in flight on CU-masked stream pairs (even / odd CU ids): a 4096-row batch is 128
@@ -299,6 +292,17 @@ def main():
     cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32_default and M == 1 else "none")
     S = max(1, a.streams if a.streams is not None else
             ((1 if a.steps <= M else 2) if M > 1 else (3 if not deep else (4 if r32_default else 2))))
+    # distinct resident batches, rotated: at least every batch of every launch in flight (S launches of up to M
+    # batches), so no input batch is read twice inside one launch or by two concurrent launches
+    n_bufs = max(8, S * M)
+    batches = []
+    for i in range(n_bufs):
+        seed = 1000 * rank + i
+        if a.inputs == "zipf":
+            xi, xv = synth.zipf_inputs(sizes, 13, BATCH, seed=seed)
+        else:
+            xi, xv = synth.synth_inputs(sizes, 13, BATCH, seed=seed)
+        batches.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
     outs = [torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(S)]
     set_outs = [[torch.empty(BATCH, dtype=torch.float32, device=dev) for _ in range(M)] for _ in range(S)] \
         if M > 1 else None
@@ -515,8 +519,10 @@ def main():
                    "workload_id": workload_id,
                    "global_batch": BATCH * world, "per_gpu_batch": BATCH,
                    "parallelism": f"dp{world} (independent batch shards, no collective)",
-                   "launch": (f"batch sets: {M} batches per launch (dfwfm_forward_batches, one grid; each batch its "
-                              "own resident inputs and logits)" if M > 1 else
+                   "launch": (f"batch sets: {units // BATCH} batches of {BATCH} per launch (dfwfm_forward_batches, "
+                              f"one grid; value = the aggregate over those batches; each batch its own resident inputs "
+                              f"and logits, {n_bufs} distinct resident batches, none read twice by the launches in "
+                              f"flight)" if M > 1 else
                               "eager" if a.no_graph else f"hipGraph replay, {G} forwards per graph")
                              + (f", {S} streams (batches in flight)" if S > 1 else "")
                              + (f", CU masks {cu_mask} (stream pairs on chip halves)" if cu_mask != "none" else "")},
@@ -547,12 +553,63 @@ def main():
                 "us_per_batch": floor_us, "frac": round(floor_us / (ms_per_step * 1e3), 4),
                 "source": "tools/ubench_gather.hip 3 (profiles/r02/r02q_ubench_gather_nb3.log)"}
         result["roofline_mfma"] = mfma
+    if not a.no_per_call and not (a.config == "pruned" and sparse_on):
+        pc = per_call_leg(eng, batches, dev, a.steps, flops, bytes_, a.config)
+        if world > 1:
+            t = torch.tensor([pc["us_per_batch"]], device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            pc["us_per_batch"] = round(float(t.item()), 3)
+            pc["samples_per_s"] = round(world * BATCH / (pc["us_per_batch"] / 1e6), 1)
+        result["per_call"] = pc
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(cfg, params, sizes, a.cpu_seconds, model, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def per_call_leg(eng, batches, dev, steps, flops, bytes_, config, settle_ms=150.0):
+    """The reference's call pattern beside the headline: one forward call per batch of 4096, the calls one after
+    the other on ONE plain stream (eval_by_batch / time_forward_pass, model/DeepFMs.py:750-780, :1012-1028), each
+    over its own resident batch; the library picks the kernel for a lone batch on the whole chip.  The forwards are
+    replayed from captured graphs of G calls (launch cost amortised as a serving loop would), after an untimed
+    settle, timed with HIP events on that stream."""
+    st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    out = torch.empty(BATCH, dtype=torch.float32, device=dev)
+    G = max(1, min(20, steps))
+    n = len(batches)
+    with torch.no_grad(), torch.cuda.stream(st):
+        eng.forward(*batches[0], out)
+        gs = []
+        for j in range(max(1, min(4, n // G))):  # graphs over different batches, replayed in turn
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                for i in range(G):
+                    eng.forward(*batches[(j * G + i) % n], out)
+            gs.append(g)
+        reps = -(-steps // G)
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < settle_ms:
+            for g in gs:
+                g.replay()
+            st.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for r in range(reps):
+            gs[r % len(gs)].replay()
+        e1.record(st)
+        st.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * G)
+    res = {"what": "one forward call per batch, sequential on one stream (the reference's per-batch call pattern)",
+           "batches": reps * G, "us_per_batch": round(us, 3), "samples_per_s": round(BATCH / (us / 1e6), 1),
+           "kernel": kernel_name(config, "none", 1)}
+    if config in ("fwfm", "fwfm_pruned"):
+        res["hbm_frac"] = round(bytes_ * BATCH / (us / 1e6) / 1e9 / PEAK_HBM_GBS, 4)
+    else:
+        res["mfma_frac"] = round(flops * BATCH / (us / 1e6) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)
+    return res
 
 
 def pmc_traffic(kname, workload_id, batches=1):

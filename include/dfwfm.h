@@ -280,23 +280,17 @@ typedef struct {
 } dfwfm_sparse_dest;
 
 /* Entries a batch of `batch` rows can produce (capacity = sum over the family's tables of min(batch, the
- * table's rows): one entry per distinct touched row), their row width and the device workspace
- * dfwfm_sparse_grads needs. */
+ * table's rows): one entry per distinct touched row) and their row width; *ws_bytes is always 0 (no workspace). */
 int dfwfm_sparse_grads_size(dfwfm_model* m, int32_t family, int64_t batch, int64_t* capacity, int32_t* width,
                             int64_t* ws_bytes);
-/* The list of the last training step: out_dest[e] (device int64) = float offset of entry e's row in the flat
- * buffer, out_rows[e * width ...] its summed gradient, *out_count (device int32) the number of entries; sorted
- * by (table, row), destinations unique.  Stream-ordered, no host synchronisation (graph-capturable). */
-int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, const dfwfm_sparse_dest* dest,
-                       int64_t capacity, int64_t* out_dest, float* out_rows, int32_t* out_count, void* ws,
-                       int64_t ws_bytes, void* stream);
-/* The same list, formed from the rank's OWN dense gradients of these tables instead of the saved activations: the
- * backward (DFWFM_BWD_TABLES) scattered them into `local` (local_floats floats, the tables at the `dest` offsets, zero
- * elsewhere); every touched row is claimed once through `stamp` (local_floats int32 of scratch, any contents: each
- * call writes the stamps of exactly the rows it reads back), copied to out_rows and cleared in `local` (zero
- * again afterwards).  Entries come unsorted (destinations unique), sums in atomic order: the replicas of a
- * data-parallel step stay identical because every rank applies the same bytes of every list.  No sort, no
- * workspace; stream-ordered, graph-capturable. */
+/* The list of the last training step, formed from the rank's OWN dense gradients of these tables: out_dest[e]
+ * (device int64) = float offset of entry e's row in the flat buffer, out_rows[e * width ...] its summed gradient,
+ * *out_count (device int32) the number of entries.  The backward (DFWFM_BWD_TABLES) scattered the tables into
+ * `local` (local_floats floats, the tables at the `dest` offsets, zero elsewhere); every touched row is claimed once
+ * through `stamp` (local_floats int32 of scratch, any contents: each call writes the stamps of exactly the rows it
+ * reads back), copied to out_rows and cleared in `local` (zero again afterwards).  Entries come unsorted
+ * (destinations unique), sums in atomic order: the replicas of a data-parallel step stay identical because every
+ * rank applies the same bytes of every list.  No sort, no workspace; stream-ordered, graph-capturable. */
 int dfwfm_sparse_grads_local(dfwfm_model* m, int32_t family, const dfwfm_sparse_dest* dest, int64_t capacity,
                              float* local, int32_t* stamp, int64_t local_floats, int64_t* out_dest, float* out_rows,
                              int32_t* out_count, void* stream);
@@ -307,8 +301,9 @@ int dfwfm_sparse_grads_apply(float* grad, int32_t width, const int64_t* dest, co
 
 /* ---- magnitude pruning (reference model/DeepFMs.py:647-673, binary_search_threshold :807-823) ----
  * The threshold whose fraction of |x| < threshold (compared in f32) hits `target`, found by the
- * reference's own bisection on (0, 100) -- same rounds, same result -- but from one radix sort of the
- * magnitudes instead of up to 101 passes with a host sync each.  Runs on `stream`; the threshold is
+ * reference's own bisection on (0, 100) -- same rounds, same result -- resolved 12 rounds per pass over
+ * the magnitudes (each pass histograms them against the 4095 mids the next 12 rounds can ask for)
+ * instead of up to 101 passes with a host sync each; no sort.  Runs on `stream`; the threshold is
  * written to device memory (`thr_dev`, one double) and never read back by the library. */
 typedef struct {
   const float* values;  /* device                                                                  */

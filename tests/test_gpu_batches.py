@@ -157,3 +157,52 @@ def test_eval_by_batch_batch_sets_identical(gpu, deep):
     bad[8192 + 5, 2] = -1
     with pytest.raises(IndexError):
         m.eval_by_batch(bad.reshape(n, 26, 1), xv, y, n)
+
+
+def test_batch_set_full_size_pruned_dense(gpu):
+    """BASELINE configs[3] on the path the bench runs: Criteo-39 tables, 3x400, the reference's magnitude masks
+    (prune_step(0.90, emb_r 0.444, prune_r 1), reference model/DeepFMs.py:647-673) applied on the device, the dense
+    32-sample forward (sparse tower off) over a set of 3 batches of 4096: every batch equals its own forward and the
+    float64 oracle at 1e-5 * max(1, |ref|)."""
+    from xsdeepfwfm_deprecated_amd.training import prune_step
+    cfg, _, m = _criteo_model(gpu, 1, 0, seed=1234)
+    m.sparse_mlp_max_density = 0.0
+    prune_step(m, 0.90, 1, 1, 1, 0.444, 1.0)
+    torch.cuda.synchronize()
+    params = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    # the masks are the reference's: ~90 % of every hidden layer and 44.4 % * 0.9 of the second-order rows zero
+    for h in (1, 2, 3):
+        z = float(np.mean(params[f"net_1_linear_{h}.weight"] == 0))
+        assert 0.89 < z < 0.91, (h, z)
+    eng = m._sync_engine(gpu)
+    assert not eng.sync_sparse(m.sparse_mlp_max_density)
+    _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], 3, 4096, seed=4242), sample=256)
+
+
+def test_forward_rejects_column_major_inputs(gpu):
+    """A column-major batch (np.asarray of a DataFrame keeps Fortran order through torch.as_tensor / .to()) must not
+    be read as row-major: the engine refuses it, and eval_by_batch / forward make their inputs row-major first."""
+    from xsdeepfwfm_deprecated_amd import synth
+    cfg, params, m = _criteo_model(gpu, 1, 0, seed=13)
+    n = 2 * 8192 + 50
+    xi, xv = synth.synth_inputs(cfg["feature_sizes"], 13, n, seed=21)
+    eng = m._sync_engine(gpu)
+    fi = torch.as_tensor(np.asfortranarray(xi)).to(gpu)
+    fv = torch.as_tensor(np.asfortranarray(xv)).to(gpu)
+    assert fi.stride(1) != 1 and fv.stride(1) != 1
+    with torch.no_grad():
+        with pytest.raises(ValueError):
+            eng.forward(fi, fv)
+        with pytest.raises(ValueError):
+            eng.forward_batches([(fi[:8192], fv[:8192]), (fi[8192:16384], fv[8192:16384])],
+                                [torch.empty(8192, device=gpu) for _ in range(2)])
+        with pytest.raises(ValueError):
+            eng.forward(torch.from_numpy(xi).to(gpu).to(torch.int32), torch.from_numpy(xv).to(gpu))
+        a = m(fi, fv).cpu().numpy()
+        b = m(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)).cpu().numpy()
+    assert np.array_equal(a, b)
+    y = (np.random.default_rng(3).random(n) < 0.3).astype(np.float32)
+    m.eval_batch_sets = True
+    rf = m.eval_by_batch(np.asfortranarray(xi), np.asfortranarray(xv), y, n)
+    rc = m.eval_by_batch(xi, xv, y, n)
+    assert rf[:2] == rc[:2]

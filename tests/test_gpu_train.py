@@ -513,7 +513,7 @@ def _kd_dp_worker(rank, world, port, q):
 # touched-row (sparse) gradients of the categorical tables: the data-parallel exchange
 def _sparse_setup(m, gpu):
     """FusedTrainStep-free driver of the C ABI: train forward + DFWFM_BWD_TABLES backward with the categorical
-    fields' grads NULL, then dfwfm_sparse_grads for both families into per-table dense buffers."""
+    fields' grads in a local buffer, then dfwfm_sparse_grads_local for both families (_local_lists_step)."""
     import ctypes
     from xsdeepfwfm_deprecated_amd import _lib
     fields, dense = m._param_layout()
@@ -527,8 +527,8 @@ def _sparse_setup(m, gpu):
 
 
 def _sparse_step(m, gpu, xi, xv, y, sparse, split=False):
-    """One backward of m on (xi, xv, y): dense scatter (sparse=False) or touched-row lists applied to a zero
-    buffer (sparse=True).  Returns {param name: grad}, the lists (for sparse) and the flat buffer."""
+    """One backward of m on (xi, xv, y) with the dense scatter (sparse=False; the touched-row lists are
+    _local_lists_step's).  Returns {param name: grad}, [] and the logits."""
     fields, dense, views, flat, _lib, ctypes = _sparse_setup(m, gpu)
     L, eng = _lib.lib(), m._sync_engine(gpu)
     st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
@@ -559,63 +559,15 @@ def _sparse_step(m, gpu, xi, xv, y, sparse, split=False):
     else:
         _lib.check(L.dfwfm_backward(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), st), "bwd")
     lists = []
-    if sparse:
-        for fam, (iq, ir) in ((0, (0, 1)), (1, (2, 3))):
-            o = lambda t: -1 if t is None else views[id(t)][0]  # noqa
-            dest = (_lib.dfwfm_sparse_dest * len(fields))(
-                *[_lib.dfwfm_sparse_dest(o(tup[iq]) if f >= m.num else -1, o(tup[ir]) if f >= m.num else -1)
-                  for f, tup in enumerate(fields)])
-            cap, w, wsb = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int64(0)
-            _lib.check(L.dfwfm_sparse_grads_size(eng.handle, fam, len(xi), ctypes.byref(cap), ctypes.byref(w),
-                                                 ctypes.byref(wsb)), "size")
-            if cap.value == 0:
-                continue
-            ws = torch.empty(wsb.value, dtype=torch.uint8, device=gpu)
-            od = torch.full((cap.value,), -7, dtype=torch.int64, device=gpu)
-            orow = torch.zeros(cap.value * w.value, device=gpu)
-            cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
-            _lib.check(L.dfwfm_sparse_grads(eng.handle, fam, ctypes.c_void_p(dl.data_ptr()), dest, cap.value,
-                                            ctypes.c_void_p(od.data_ptr()), ctypes.c_void_p(orow.data_ptr()),
-                                            ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                                            wsb.value, st), "sparse")
-            _lib.check(L.dfwfm_sparse_grads_apply(ctypes.c_void_p(flat.data_ptr()), w.value,
-                                                  ctypes.c_void_p(od.data_ptr()), ctypes.c_void_p(orow.data_ptr()),
-                                                  ctypes.c_void_p(cnt.data_ptr()), cap.value, st), "apply")
-            lists.append((fam, w.value, od, orow, cnt))
     torch.cuda.synchronize()
     names = {id(p): k for k, p in m.named_parameters()}
     g = {names[i]: v.detach().cpu().numpy().copy() for i, (o, v) in views.items()}
     return g, lists, out.detach().cpu().numpy()
 
 
-@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult", "train_deepfwfm_fwlw", "train_fwfm_nolw"])
-def test_sparse_row_lists_equal_dense_table_grads(gpu, name):
-    """dfwfm_sparse_grads + apply give the categorical tables' dense gradients (to fp32 reassociation: the
-    dense scatter adds atomically in any order), the lists are sorted, unique and exactly the touched rows,
-    and two runs give the same bits (fixed-order sums, no atomics)."""
-    cfg, params, xi, xv, y, *_ = load_train_golden(name)
-    m = build(cfg, params, gpu, is_deep_dropout=False)
-    gd, _, out_d = _sparse_step(m, gpu, xi, xv, y, sparse=False)
-    gs, lists, out_s = _sparse_step(m, gpu, xi, xv, y, sparse=True)
-    gs2, lists2, _ = _sparse_step(m, gpu, xi, xv, y, sparse=True)
-    assert np.array_equal(out_d, out_s)
-    for k in gd:
-        sc = np.abs(gd[k]).max()
-        assert np.abs(gs[k] - gd[k]).max() <= G_TOL * sc + 1e-12, k
-        assert np.array_equal(gs[k], gs2[k]), k  # deterministic
-    assert lists, "no list produced"
-    ncat = cfg["field_size"] - cfg["numerical"]
-    for (fam, w, od, orow, cnt), (_, _, od2, orow2, cnt2) in zip(lists, lists2):
-        n = int(cnt.item())
-        d = od[:n].cpu().numpy()
-        assert n > 0 and np.all(np.diff(d) > 0), "destinations ascending and unique"
-        assert np.array_equal(d, od2[:n].cpu().numpy()) and torch.equal(orow[:n * w], orow2[:n * w])
-        assert n <= len(xi) * ncat * 2
-
-
-def test_sparse_rows_hot_rows_cross_blocks(gpu):
-    """A field where every sample hits one of 3 rows (segments of ~B/3 positions, across many 64-position
-    blocks) and one with all-distinct rows: the carried block partials are summed right."""
+def test_local_lists_hot_rows(gpu):
+    """A field where every sample hits one of 3 rows (thousands of (table, sample) pairs race for one stamp) and one
+    with all-distinct rows: dfwfm_sparse_grads_local lists each touched row once, with the dense gradient's sum."""
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
     sizes = [1] * 13 + [3] + [5000] * 25
     B = 3000
@@ -626,10 +578,11 @@ def test_sparse_rows_hot_rows_cross_blocks(gpu):
                 deep_nodes=32, is_deep_dropout=False).to(gpu).train()
     m.init_weights()
     gd, _, _ = _sparse_step(m, gpu, xi, xv, y, sparse=False)
-    gs, lists, _ = _sparse_step(m, gpu, xi, xv, y, sparse=True)
+    gl, lists, local, _ = _local_lists_step(m, gpu, xi, xv, y)
+    assert float(local.abs().max()) == 0.0
     for k in gd:
         sc = np.abs(gd[k]).max()
-        assert np.abs(gs[k] - gd[k]).max() <= G_TOL * sc + 1e-12, k
+        assert np.abs(gl[k] - gd[k]).max() <= G_TOL * sc + 1e-12, k
     fam0 = lists[0]
     assert fam0[0] == 0 and int(fam0[4].item()) == sum(len(np.unique(xi[:, j])) for j in range(26))
 

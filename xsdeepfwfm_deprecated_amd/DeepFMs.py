@@ -406,8 +406,10 @@ class DeepFMs(nn.Module):
         self.eval()
         dev = self._device()
         ncat = self.field_size - self.num
-        Xi_d = torch.as_tensor(np.asarray(Xi)[:x_size]).reshape(x_size, ncat).to(dev, dtype=torch.int64)
-        Xv_d = torch.as_tensor(np.asarray(Xv)[:x_size], dtype=torch.float32).to(dev)
+        # row-major on the device: a column-major host array (np.asarray of a DataFrame) keeps its strides
+        # through as_tensor / .to(), and the C ABI reads a batch as base pointer + row stride
+        Xi_d = torch.as_tensor(np.asarray(Xi)[:x_size]).reshape(x_size, ncat).to(dev, dtype=torch.int64).contiguous()
+        Xv_d = torch.as_tensor(np.asarray(Xv)[:x_size], dtype=torch.float32).to(dev).contiguous()
         y_d = torch.as_tensor(np.asarray(y)[:x_size], dtype=torch.float32).to(dev)
         bs = 8192
         logits = torch.empty(x_size, dtype=torch.float32, device=dev)

@@ -50,7 +50,7 @@ DFWFM_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported", -3: "HIP error", -4: "bad state"}
 FLAG_INDEX_OUT_OF_RANGE = 1
 BWD_TABLES, BWD_MLP_WEIGHTS, BWD_TILES, BWD_SPREAD, BWD_REDUCE, BWD_SCATTER = 1, 2, 4, 8, 16, 32  # dfwfm_backward_phases
-FAMILY_SECOND, FAMILY_FIRST = 0, 1  # dfwfm_sparse_grads
+FAMILY_SECOND, FAMILY_FIRST = 0, 1  # dfwfm_sparse_grads_local
 ADAM_STATE_BYTES = 48
 
 
@@ -130,8 +130,6 @@ SIGNATURES = {
     "dfwfm_bce_grad": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_double, _P, _P, _P]),
     "dfwfm_sparse_grads_size": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
                                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]),
-    "dfwfm_sparse_grads": (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.POINTER(dfwfm_sparse_dest), ctypes.c_int64,
-                                          _P, _P, _P, _P, ctypes.c_int64, _P]),
     "dfwfm_sparse_grads_apply": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, _P, ctypes.c_int64, _P]),
     "dfwfm_sparse_grads_local": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(dfwfm_sparse_dest), ctypes.c_int64,
                                                 _P, _P, ctypes.c_int64, _P, _P, _P, _P]),

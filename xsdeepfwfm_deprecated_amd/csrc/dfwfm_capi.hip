@@ -1,5 +1,6 @@
 // dfwfm_capi.hip -- the extern "C" boundary (include/dfwfm.h) over the kernels.
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -546,9 +547,15 @@ int diag_stamps_buffer(dfwfm_model* m, int64_t batch, int which, uint64_t** out)
   return DFWFM_OK;
 }
 
-// CUs a stream may use (its CU mask; cached per stream handle)
+// CUs a stream may use (its CU mask; cached per stream handle).  The cache is shared by every host thread that
+// uses the model, so it is guarded; a handle the runtime reuses for a stream with another mask keeps the old count
+// until replaced, which only changes which (bit-identical) forward kernel runs.
+std::mutex g_cu_mu;
+
 int stream_cu_count(dfwfm_model* m, void* stream) {
-  for (int i = 0; i < m->cu_n; ++i)
+  std::lock_guard<std::mutex> lock(g_cu_mu);
+  const int cached = m->cu_n < 8 ? m->cu_n : 8;
+  for (int i = 0; i < cached; ++i)
     if (m->cu_stream[i] == stream) return m->cu_count[i];
   int n = 0;
   uint32_t mask[64] = {0};
@@ -1071,6 +1078,12 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       const int64_t max_splits = (batch + 127) / 128;
       if (splits > max_splits) splits = max_splits;
       if (splits < 1) splits = 1;
+      // a wave's raw-buffer range (a quarter of a split's rows x the widest row, in bytes) must fit 31 bits
+      int64_t wmax = m->N;
+      for (int l = 1; l <= H; ++l) wmax = d.ldx[l] > wmax ? d.ldx[l] : wmax;
+      const int64_t rows_cap = ((0x7fffffffLL / (wmax * 4)) * 4 - 4 * quantum) / quantum * quantum;
+      if (rows_cap < quantum) return fail(DFWFM_ERR_UNSUPPORTED, "MLP rows of %lld floats", (long long)wmax);
+      if ((batch + splits - 1) / splits > rows_cap) splits = (batch + rows_cap - 1) / rows_cap;
       int64_t rows = (batch + splits - 1) / splits;
       rows = (rows + quantum - 1) / quantum * quantum;  // whole k-step groups per wave
       splits = (batch + rows - 1) / rows;
@@ -1148,8 +1161,6 @@ int sparse_tasks(const dfwfm_model* m, int family, const dfwfm_sparse_dest* dest
   if (!has) return 0;
   for (int f = m->num; f < m->F; ++f) {
     const FieldDev& fd = m->h_fields[f];
-    const float* tq = family == DFWFM_FAMILY_SECOND ? fd.emb2 : fd.emb1;
-    const float* tr = family == DFWFM_FAMILY_SECOND ? fd.emb2_r : fd.emb1_r;
     for (int part = 0; part < (fd.c > 0 ? 2 : 1); ++part) {
       const int64_t off = dest ? (part == 0 ? dest[f].q : dest[f].r) : 0;
       if (off < 0) continue;
@@ -1159,7 +1170,6 @@ int sparse_tasks(const dfwfm_model* m, int family, const dfwfm_sparse_dest* dest
         t.field = (int16_t)f;
         t.c = (int32_t)fd.c;
         t.kind = (int8_t)(fd.c == 0 ? 0 : 1 + part);
-        t.other = (fd.c > 0 && fd.op == 0) ? (part == 0 ? tr : tq) : nullptr;
       }
       ++n;
     }
@@ -1199,49 +1209,8 @@ int dfwfm_sparse_grads_size(dfwfm_model* m, int32_t family, int64_t batch, int64
   *width = family == DFWFM_FAMILY_SECOND ? m->D : 1;
   if ((int64_t)nt * batch > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "more than 2^31 (table, sample) pairs");
   *capacity = sparse_capacity(m, family, nullptr, batch);
-  // the sort runs over every (table, sample) position; only the exchanged list is capped per table
-  *ws_bytes = nt ? (int64_t)sparse_workspace_bytes((int64_t)nt * batch, *width, nt) : 0;
+  *ws_bytes = 0;  // dfwfm_sparse_grads_local needs no workspace (kept in the signature: ABI version 2)
   return DFWFM_OK;
-}
-
-int dfwfm_sparse_grads(dfwfm_model* m, int32_t family, const float* dlogit, const dfwfm_sparse_dest* dest,
-                       int64_t capacity, int64_t* out_dest, float* out_rows, int32_t* out_count, void* ws,
-                       int64_t ws_bytes, void* stream) {
-  if (!m || !dest || !out_count) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
-  if (family != DFWFM_FAMILY_SECOND && family != DFWFM_FAMILY_FIRST) return fail(DFWFM_ERR_INVALID_ARG, "bad family");
-  if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_sparse_grads needs a preceding dfwfm_train_forward");
-  if (family == DFWFM_FAMILY_SECOND && m->t_batch > 0 && !m->bwd_tables)
-    return fail(DFWFM_ERR_STATE, "dfwfm_sparse_grads (second-order tables) needs the DFWFM_BWD_TABLES backward");
-  SparseArgs a;
-  memset(&a, 0, sizeof a);
-  a.ntasks = sparse_tasks(m, family, dest, &a);
-  a.D = m->D;
-  a.F = m->F;
-  a.num = m->num;
-  a.w = family == DFWFM_FAMILY_SECOND ? m->D : 1;
-  a.src = family == DFWFM_FAMILY_SECOND ? 0 : 1;
-  a.fields = m->d_fields;
-  a.xi = m->t_xi;
-  a.xi_stride = m->t_xs;
-  a.batch = m->t_batch;
-  a.sv_de = m->sv_de;
-  a.dlogit = dlogit;
-  a.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
-  const int64_t n = (int64_t)a.ntasks * a.batch;
-  const int64_t bound = sparse_capacity(m, family, dest, a.batch);
-  if (bound > capacity)
-    return fail(DFWFM_ERR_INVALID_ARG, "capacity %lld < %lld entries", (long long)capacity, (long long)bound);
-  if (n > 0 && (!dlogit || !out_dest || !out_rows || !ws)) return fail(DFWFM_ERR_INVALID_ARG, "null buffer");
-  hipStream_t s = (hipStream_t)stream;
-  if (n == 0) {
-    HIP_TRY(hipMemsetAsync(out_count, 0, sizeof(int32_t), s));
-    return DFWFM_OK;
-  }
-  const size_t need = sparse_workspace_bytes(n, a.w, a.ntasks);
-  if (ws_bytes < (int64_t)need)
-    return fail(DFWFM_ERR_INVALID_ARG, "workspace of %lld bytes < %zu", (long long)ws_bytes, need);
-  hipError_t e = launch_sparse_grads(a, out_dest, out_rows, out_count, ws, (size_t)ws_bytes, s);
-  return e == hipSuccess ? DFWFM_OK : hip_fail(e, "sparse grads");
 }
 
 int dfwfm_sparse_grads_local(dfwfm_model* m, int32_t family, const dfwfm_sparse_dest* dest, int64_t capacity,

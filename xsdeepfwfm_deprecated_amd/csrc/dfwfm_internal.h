@@ -240,7 +240,7 @@ struct ScatterArgs {
 
 // Touched-row gradients of one table family (dfwfm_sparse.hip): one task per categorical table.
 struct SparseTask {
-  const float* other;   // QR "mult": the partner table whose row multiplies the gradient (else null)
+  const float* other;   // unused (kept for the 24-byte layout)
   int64_t dest;         // float offset of this table's gradient in the caller's flat buffer
   int32_t c;            // QR collisions (kind 1, 2)
   int16_t field;        // model field index
@@ -254,18 +254,11 @@ struct SparseArgs {
   int32_t ntasks;
   int32_t D, F, num;
   int32_t w;            // row width of the family: D (second-order tables) or 1 (first-order tables)
-  int32_t src;          // 0: dE[b, f, :] (sv_de), 1: dfo[b, f] = dlogit * (lw[f] or 1)
   const FieldDev* fields;
   const int64_t* xi;
   int64_t xi_stride;
   int64_t batch;
-  const float* sv_de;
-  const float* dlogit;
-  const float* lw;
 };
-size_t sparse_workspace_bytes(int64_t n, int w, int ntasks);
-hipError_t launch_sparse_grads(const SparseArgs& a, int64_t* out_dest, float* out_rows, int32_t* out_count, void* ws,
-                               size_t ws_bytes, hipStream_t s);
 hipError_t launch_sparse_apply(float* grad, int w, const int64_t* dest, const float* rows, const int32_t* count,
                                int64_t cap, hipStream_t s);
 hipError_t launch_sparse_local(const SparseArgs& a, float* local, int32_t* stamp, int64_t cap, int64_t* out_dest,

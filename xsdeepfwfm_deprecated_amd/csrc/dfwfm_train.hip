@@ -1212,6 +1212,12 @@ hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream
 
 hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
   if (total_blocks <= 0) return hipSuccess;
+  // a wave's raw-buffer ranges and k-step offsets are 32-bit byte counts over its quarter of a split's rows
+  const int64_t q = a.rows_per_split / 4 + 4;
+  for (int l = 1; l <= a.H; ++l) {
+    const int64_t w = a.ldx[l] > a.N ? a.ldx[l] : a.N;
+    if (q * w * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(total_blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }

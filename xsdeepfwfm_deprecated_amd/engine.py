@@ -36,6 +36,23 @@ def _require_f32_cuda(t, name, device):
         raise RuntimeError(f"dfwfm: {name} must be contiguous")
 
 
+def _require_rows(t, name, dtype, device, width):
+    """The C ABI takes a batch as a base pointer + a row stride: each row's `width` entries must be contiguous
+    (a column-major array, e.g. np.asarray of a pandas DataFrame, would be read as the wrong entries)."""
+    if t.dtype != dtype or t.device != device:
+        raise ValueError(f"dfwfm: {name} must be a {dtype} tensor on {device}, got {t.dtype} on {t.device}")
+    if t.dim() < 1 or t.shape[0] == 0 or width == 0:
+        return
+    inner = 1
+    for d in range(t.dim() - 1, 0, -1):  # dims after the batch dim: row-major and dense
+        if t.shape[d] != 1 and t.stride(d) != inner:
+            raise ValueError(f"dfwfm: {name} rows must be contiguous (got strides {tuple(t.stride())}); "
+                             "pass .contiguous()")
+        inner *= t.shape[d]
+    if inner < width:
+        raise ValueError(f"dfwfm: {name} has {inner} entries per row, the model needs {width}")
+
+
 class ForwardEngine:
     """Binds one DeepFMs module to one device-resident dfwfm_model."""
 
@@ -145,6 +162,8 @@ class ForwardEngine:
         B = xi.shape[0]
         ncat = self.cfg["field_size"] - self.cfg["numerical"]
         num = self.cfg["numerical"]
+        _require_rows(xi, "Xi", torch.int64, self.device, ncat)
+        _require_rows(xv, "Xv", torch.float32, self.device, num)
         if out is None:
             out = torch.empty(B, dtype=torch.float32, device=self.device)
         xs = xi.stride(0) if ncat > 0 else 0
@@ -175,6 +194,8 @@ class ForwardEngine:
         xs = xi0.stride(0) if ncat > 0 else 0
         vs = xv0.stride(0) if num > 0 else 0
         for xi, xv in batches:
+            _require_rows(xi, "Xi", torch.int64, self.device, ncat)
+            _require_rows(xv, "Xv", torch.float32, self.device, num)
             if xi.shape[0] != B or (ncat > 0 and xi.stride(0) != xs) or (num > 0 and xv.stride(0) != vs):
                 raise ValueError("forward_batches: every batch needs the same size and row strides")
         for o in outs:
@@ -202,6 +223,8 @@ class ForwardEngine:
         """Forward of a training step; returns the token the matching backward must present."""
         B = xi.shape[0]
         ncat = self.cfg["field_size"] - self.cfg["numerical"]
+        _require_rows(xi, "Xi", torch.int64, self.device, ncat)
+        _require_rows(xv, "Xv", torch.float32, self.device, self.cfg["numerical"])
         xs = xi.stride(0) if ncat > 0 else 0
         vs = xv.stride(0) if self.cfg["numerical"] > 0 else 0
         rc = _lib.lib().dfwfm_train_forward(self.handle, ctypes.c_void_p(xi.data_ptr()), xs,

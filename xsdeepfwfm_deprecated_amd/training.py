@@ -160,7 +160,7 @@ class FusedTrainStep:
         # gradient buffer order: [categorical tables | the rest of what the backward's first part writes
         # (numerical-field tables, shallow dense, net_1_fc) | the MLP weights / biases the weight-gradient
         # GEMM writes last].  Under data parallelism the tables go over the sparse touched-row exchange
-        # (sparse_exchange, dfwfm_sparse_grads) and the two dense buckets over all-reduces, the first one
+        # (sparse_exchange, dfwfm_sparse_grads_local) and the two dense buckets over all-reduces, the first one
         # overlapping the GEMM; with sparse_exchange=False the tables join the first all-reduce (dense, like
         # the reference's nn.Embedding(sparse=False) gradients)
         mlp_ids = {id(t) for t in dense["lin_w"] + dense["lin_b"]}
@@ -246,7 +246,7 @@ class FusedTrainStep:
     # -- touched-row exchange of the categorical tables' gradients (data parallelism) ------------------
     def _setup_sparse(self, fields, views):
         """Per table family (second-order rows of width D, first-order rows of width 1) the list buffers of
-        dfwfm_sparse_grads, packed into ONE byte buffer per rank so the exchange is one all-gather:
+        dfwfm_sparse_grads_local, packed into ONE byte buffer per rank so the exchange is one all-gather:
         [dest int64 per family | rows f32 per family | counts int32]."""
         L, h = self.L, self.eng.handle
         base = self.grad.data_ptr()
@@ -643,9 +643,9 @@ def binary_search_threshold(param, target_percent, total_no):
 
 
 class DevicePruner:
-    """The reference's magnitude pruning on the device (C ABI dfwfm_prune_*): one radix sort per
-    threshold plus the reference's own bisection replayed on the sorted magnitudes -- the same
-    thresholds and masks as binary_search_threshold, without its up-to-101 host-synchronised passes."""
+    """The reference's magnitude pruning on the device (C ABI dfwfm_prune_*): the reference's own bisection,
+    12 rounds resolved per histogram pass over the magnitudes (dfwfm_prune.hip) -- the same thresholds and
+    masks as binary_search_threshold, without its up-to-101 host-synchronised passes."""
 
     def __init__(self, device):
         self.device = device
