@@ -62,7 +62,7 @@ def test_abi_version_and_error_string(built):
     assert L.dfwfm_set_step_source(None, None) == -1
     assert L.dfwfm_prune_threshold(None, 0, 0.5, None, None, 0, None) == -1
     assert L.dfwfm_prune_apply(None, 4, 0, None, None) == -1
-    assert L.dfwfm_prune_workspace_bytes(1000) >= 8000  # host-only query (hipcub sizing, no launch)
+    assert L.dfwfm_prune_workspace_bytes(1000) >= 8000  # host-only query (histogram-select sizing, no launch)
     assert ctypes.sizeof(built.dfwfm_prune_source) == 24
     assert L.dfwfm_eval_metrics(None, None, 4, None, None, 0, None) == -1
     assert L.dfwfm_metrics_workspace_bytes(1000) > 40 * 1000

@@ -114,64 +114,84 @@ def test_dp_grad_allreduce_gloo_world2():
 
 def _sparse_protocol_worker(rank, world, port, q):
     """One rank of the touched-row exchange at oracle level: its local table gradients (torch_port, loss
-    normalised by the global batch) -> (dest, row) list at fixed capacity packed into one byte buffer ->
-    training.gather_packed over gloo -> every rank's lists added in rank order."""
+    normalised by the global batch) -> (dest, row) lists of both table families (second-order rows of width D,
+    first-order rows of width 1) at the product's fixed capacity (sum over tables of min(rows per rank, table
+    rows)), packed with training.packed_layout into one byte buffer -> training.gather_packed over gloo -> every
+    rank's lists added in rank order (the order FusedTrainStep._apply_sparse uses)."""
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
-        from xsdeepfwfm_deprecated_amd.training import gather_packed
+        from xsdeepfwfm_deprecated_amd.training import gather_packed, packed_layout
         cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_lw")
         n = 64
         lo = rank * (n // world)
         hi = lo + n // world
         _, _, g, _ = torch_port.train_step(cfg, params, xi[lo:hi], xv[lo:hi], y[lo:hi], 1e-3, 0.0)
-        scale = (hi - lo) / n  # the rank's mean-loss gradient -> its share of the global mean
-        num, D = cfg["numerical"], cfg["embedding_size"]
-        names = [f"fm_2nd_embeddings.{f}.weight" for f in range(num, cfg["field_size"])]
-        offs = np.cumsum([0] + [params[k].shape[0] for k in names])
-        cap = len(names) * (n // world)
-        dest = np.full(cap, -1, np.int64)
-        rows = np.zeros((cap, D), np.float32)
-        c = 0
-        for j, k in enumerate(names):
-            touched = np.unique(xi[lo:hi, j])
-            dest[c:c + len(touched)] = offs[j] + touched
-            rows[c:c + len(touched)] = g[k][touched] * scale
-            c += len(touched)
-        send = torch.cat([torch.from_numpy(dest).view(torch.uint8), torch.from_numpy(rows).view(-1).view(torch.uint8),
-                          torch.tensor([c, 0], dtype=torch.int32).view(torch.uint8)])
-        recv = torch.zeros(world, send.numel(), dtype=torch.uint8)
+        scale = np.float32((hi - lo) / n)  # the rank's mean-loss gradient -> its share of the global mean
+        num, D, F = cfg["numerical"], cfg["embedding_size"], cfg["field_size"]
+        fams = []
+        for prefix, w in (("fm_2nd_embeddings", D), ("fm_1st_embeddings", 1)):
+            names = [f"{prefix}.{f}.weight" for f in range(num, F)]
+            if not all(k in params for k in names):
+                continue
+            offs = np.cumsum([0] + [params[k].shape[0] for k in names])
+            cap = sum(min(hi - lo, params[k].shape[0]) for k in names)
+            fams.append(dict(names=names, offs=offs, cap=cap, w=w))
+        nbytes = packed_layout(fams)
+        send = torch.zeros(nbytes, dtype=torch.uint8)
+        for f in fams:
+            dest = np.full(f["cap"], -1, np.int64)
+            rows = np.zeros((f["cap"], f["w"]), np.float32)
+            c = 0
+            for j, k in enumerate(f["names"]):
+                touched = np.unique(xi[lo:hi, j])
+                dest[c:c + len(touched)] = (f["offs"][j] + touched) * f["w"]
+                rows[c:c + len(touched)] = g[k].reshape(-1, f["w"])[touched] * scale
+                c += len(touched)
+            assert c <= f["cap"]
+            send[f["o_dest"]:f["o_dest"] + 8 * f["cap"]] = torch.from_numpy(dest).view(torch.uint8)
+            send[f["o_rows"]:f["o_rows"] + 4 * f["cap"] * f["w"]] = torch.from_numpy(rows).view(-1).view(torch.uint8)
+            send[f["o_cnt"]:f["o_cnt"] + 4] = torch.tensor([c], dtype=torch.int32).view(torch.uint8)
+        recv = torch.zeros(world, nbytes, dtype=torch.uint8)
         gather_packed(dist, send, recv, async_op=False)
-        flat = torch.zeros(int(offs[-1]), D)
-        for r in range(world):
-            b = recv[r]
-            cnt = int(b[-8:].view(torch.int32)[0])
-            d = b[:8 * cap].view(torch.int64)[:cnt]
-            v = b[8 * cap:8 * cap + 4 * cap * D].view(torch.float32).view(cap, D)[:cnt]
-            flat[d] += v  # destinations unique within one list
-        q.put((rank, flat.numpy()))
+        out = []
+        for f in fams:
+            flat = torch.zeros(int(f["offs"][-1]) * f["w"])
+            for r in range(world):  # rank order, one list after the other
+                b = recv[r]
+                cnt = int(b[f["o_cnt"]:f["o_cnt"] + 4].view(torch.int32)[0])
+                d = b[f["o_dest"]:f["o_dest"] + 8 * f["cap"]].view(torch.int64)[:cnt]
+                v = b[f["o_rows"]:f["o_rows"] + 4 * f["cap"] * f["w"]].view(torch.float32).view(f["cap"], f["w"])[:cnt]
+                for j in range(f["w"]):  # destinations unique within one list
+                    flat[d + j] += v[:, j]
+            out.append(flat.numpy())
+        q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
-def test_touched_row_exchange_protocol_gloo_world2():
-    """configs[4] exchange at oracle level on CPU: two gloo ranks' touched-row lists, all-gathered at fixed
-    capacity and added in rank order, equal the dense table gradients of one process on the global batch,
-    identically on both ranks."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_touched_row_exchange_protocol_gloo(world):
+    """configs[4] exchange at oracle level on CPU: `world` gloo ranks' touched-row lists of both table families,
+    all-gathered at fixed capacity in training.packed_layout's buffer and added in rank order, equal the dense
+    table gradients of one process on the global batch, and every rank's result is bit-identical."""
     import tempfile
     import torch.multiprocessing as mp
     port = os.path.join(tempfile.mkdtemp(), "store")  # a file rendezvous: no port to race for under pytest -n
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_sparse_protocol_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sparse_protocol_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert np.array_equal(res[0], res[1])
+    for r in range(1, world):
+        assert all(np.array_equal(a, b) for a, b in zip(res[0], res[r]))
     cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_lw")
     _, _, g, _ = torch_port.train_step(cfg, params, xi[:64], xv[:64], y[:64], 1e-3, 0.0)
-    dense = np.concatenate([g[f"fm_2nd_embeddings.{f}.weight"] for f in range(13, 39)])
-    assert np.abs(res[0] - dense).max() <= 2e-5 * np.abs(dense).max()
+    assert len(res[0]) == 2
+    for got, prefix in zip(res[0], ("fm_2nd_embeddings", "fm_1st_embeddings")):
+        dense = np.concatenate([g[f"{prefix}.{f}.weight"].reshape(-1) for f in range(13, 39)])
+        assert np.abs(got - dense).max() <= 2e-5 * np.abs(dense).max()

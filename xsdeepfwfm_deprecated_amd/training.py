@@ -119,6 +119,24 @@ def gather_packed(dist, send, recv, async_op=True):
     return dist.all_gather(list(recv.unbind(0)), send, async_op=async_op)
 
 
+def packed_layout(fams):
+    """Byte layout of one rank's touched-row lists in the exchanged buffer: [dest int64 per family | rows f32 per
+    family | counts int32], for fams = [{"cap": entries, "w": row width}, ...]; sets each family's o_dest / o_rows /
+    o_cnt and returns the buffer's size.  Every section starts 16-byte aligned and the size is a multiple of 16, so
+    each rank's slice of the all-gathered [world, nbytes] buffer keeps the int64 destination lists aligned."""
+    a16 = lambda x: (x + 15) & ~15  # noqa: E731
+    nbytes = 0
+    for f in fams:
+        f["o_dest"] = nbytes
+        nbytes = a16(nbytes + 8 * f["cap"])
+    for f in fams:
+        f["o_rows"] = nbytes
+        nbytes = a16(nbytes + 4 * f["cap"] * f["w"])
+    for i, f in enumerate(fams):
+        f["o_cnt"] = nbytes + 4 * i
+    return a16(nbytes + 4 * len(fams))
+
+
 class FusedTrainStep:
     """One reference training step -- fit()'s inner-loop body (:619-637): zero_grad, forward,
     BCE-with-logits, backward, Adam(lr, weight_decay) -- as HIP launches on pre-built pointers, captured
@@ -264,23 +282,10 @@ class FusedTrainStep:
                        "dfwfm_sparse_grads_size")
             if cap.value > 0:
                 fams.append(dict(fam=fam, dest=dest, cap=int(cap.value), w=int(w.value), ws_bytes=int(ws.value)))
-        # every section starts 16-byte aligned and the buffer is a multiple of 16 bytes, so each rank's slice of
-        # the all-gathered [world, nbytes] buffer keeps the int64 destination lists aligned
-        a16 = lambda x: (x + 15) & ~15  # noqa: E731
-        nbytes = 0
-        for f in fams:
-            f["o_dest"] = nbytes
-            nbytes = a16(nbytes + 8 * f["cap"])
-        for f in fams:
-            f["o_rows"] = nbytes
-            nbytes = a16(nbytes + 4 * f["cap"] * f["w"])
-        o_cnt = nbytes
-        nbytes = a16(nbytes + 4 * len(fams))
+        nbytes = packed_layout(fams)
         world = self.dist.get_world_size()
         self.sp_send = torch.zeros(nbytes, dtype=torch.uint8, device=self.dev)
         self.sp_recv = torch.zeros(world, nbytes, dtype=torch.uint8, device=self.dev)
-        for i, f in enumerate(fams):
-            f["o_cnt"] = o_cnt + 4 * i
         self.sp_fams = fams
         self.sp_bytes = nbytes
 
