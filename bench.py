@@ -146,12 +146,12 @@ class _HostGate:
 
 def r32_on(config="deepfwfm", cu_mask="even-odd", batch_set=1):
     """The library runs the 32-sample-workgroup forward (fwd32_kernel) for the bench's deep configs when the
-    launch's 32-sample workgroups cover every CU of its stream: a batch set (>= 2 batches of 4096 on the whole
-    chip), or one batch on a stream CU-masked to half of the chip; DFWFM_R32=1 forces it, DFWFM_R32=0 never."""
+    launch's 32-sample workgroups give every CU of its stream two (a batch set of >= 4 batches of 4096 on the whole
+    chip), or one on a CU-masked stream (one batch on half of the chip); DFWFM_R32=1 forces it, DFWFM_R32=0 never."""
     env = os.environ.get("DFWFM_R32", "")
     if config in ("fwfm", "fwfm_pruned") or env == "0":
         return False
-    return env not in ("",) or cu_mask not in (None, "none") or batch_set > 1
+    return env not in ("",) or cu_mask not in (None, "none") or batch_set >= 4
 
 
 def masked_streams(dev, S, how):
@@ -186,12 +186,18 @@ def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT / DFWFM_R32 select the A/B variants."""
     if r32_on(config, cu_mask, batch_set):
         return f"dfwfm::fwd32_kernel<10,{'true' if config == 'qr' else 'false'}>"
+    if config == "fwfm" and os.environ.get("DFWFM_FWFM_LANE", "1") != "0":
+        return "dfwfm::fwfm_lane_kernel<39,13,10>"  # MLP-free, a lane per (sample, column pair)
     if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
             return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
         png = os.environ.get("DFWFM_P3_NG")
         ng = 4 if png == "4" or (png is None and batch_set > 1) else 8  # batch sets: four waves (DESIGN.md 3.5)
         return f"dfwfm::fwd_kernel<10,1,1,false,3,{ng},3,false>"  # MLP-free, 3 FwFM row tiles, no QR field
+    if batch_set == 1 and cu_mask in (None, "none") and os.environ.get("DFWFM_WS", "1") != "0" \
+            and not os.environ.get("DFWFM_SPLIT") and config != "pruned_sparse":
+        # a lone 4096-row batch on the whole chip: one 16-sample tile per CU, the wave-specialised form
+        return f"dfwfm::fwd16ws_kernel<10,{'true' if config == 'qr' else 'false'}>"
     ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
     tpw = 6 if ng == 4 else 3
     if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):

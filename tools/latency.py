@@ -7,7 +7,7 @@ with HIP events around it (device time) and by the host clock around launch + sy
 batch's forward is also replayed from a one-forward hipGraph (launch overhead of a serving loop that captures).
 Prints one JSON line.
 
-  python tools/latency.py [--calls 1000] [--batches 1,16,64,256,1024,4096]
+  python tools/latency.py [--calls 1000] [--batches 1,16,64,256,1024,4096,8192]
 """
 import argparse
 import json
@@ -62,15 +62,31 @@ def measure(eng, xi, xv, out, calls, dev):
         g.replay()
         torch.cuda.synchronize(dev)
         ghost.append(time.perf_counter() - t0)
+    # back to back: 20 calls per graph, replayed without a host sync in between (a serving loop's steady state;
+    # the idle gap of a synchronised call lets the chip lower its clock)
+    g20 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g20):
+        for _ in range(20):
+            eng.forward(xi, xv, out)
+    reps = max(5, calls // 20)
+    for _ in range(reps):
+        g20.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        g20.replay()
+    e1.record(st)
+    e1.synchronize()
     return {"device_us_median": round(float(np.median(dev_us)), 2), "device_us_p99": round(float(np.percentile(dev_us, 99)), 2),
             "host_us_median": round(float(np.median(host)) * 1e6, 2),
-            "graph_host_us_median": round(float(np.median(ghost)) * 1e6, 2)}
+            "graph_host_us_median": round(float(np.median(ghost)) * 1e6, 2),
+            "back_to_back_us": round(e0.elapsed_time(e1) * 1e3 / (reps * 20), 2)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=1000)
-    ap.add_argument("--batches", default="1,16,64,256,1024,4096")
+    ap.add_argument("--batches", default="1,16,64,256,1024,4096,8192")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -89,6 +105,8 @@ def main():
                 out = torch.empty(b, dtype=torch.float32, device=dev)
                 r = measure(eng, xi, xv, out, a.calls if b <= 256 else max(100, a.calls // 10), dev)
                 r["samples_per_s_one_call_at_a_time"] = round(b / (r["device_us_median"] * 1e-6), 1)
+                if deep:  # f32 MFMA fraction of the back-to-back rate (967,620 FLOP per sample, 157.3 TF/s)
+                    r["mfma_frac_back_to_back"] = round(967620 * b / (r["back_to_back_us"] * 1e-6) / 157.3e12, 4)
                 rows[str(b)] = r
         res["models"][name] = rows
     print(json.dumps(res))

@@ -27,8 +27,11 @@ struct dfwfm_model {
   int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
   int r32;             // 32-sample workgroups (fwd32_kernel) usable: 0 no, 1 when the stream's CUs are covered, 2 forced
   size_t lds_r32;
+  int ws;              // fwd16ws_kernel usable (one 16-sample tile per CU or fewer)
+  size_t lds_ws;
   void* cu_stream[8];  // streams whose CU counts are cached (hipExtStreamGetCUMask), round-robin replaced
   int cu_count[8], cu_n, cu_next;
+  int dev_cus;         // CUs of the device (0 until the first stream_cu_count)
   size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
   int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
   // sparse deep tower (dfwfm_model_build_sparse_mlp): ELL of the pruned weights, used by dfwfm_forward_ws
@@ -45,6 +48,7 @@ struct dfwfm_model {
   // device state (owned)
   FieldDev* d_fields;
   float* d_upack;  // FwFM A-operand fragments [MT][S][64]
+  float* d_utri;   // the same U row-major [F][F] (MLP-free lane kernel)
   int2* d_pairs;   // build_fwfm_pairs: nonzero pairs of a pruned R (F (F - 1) / 2 capacity)
   int32_t npairs;
   int32_t* d_err;
@@ -126,7 +130,7 @@ int dev_alloc(T** p, size_t count) {
 
 void free_model(dfwfm_model* m) {
   if (!m) return;
-  void* ptrs[] = {m->d_fields, m->d_upack, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
+  void* ptrs[] = {m->d_fields, m->d_upack, m->d_utri, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
                   m->d_lw,     m->d_bias,  m->d_stamps,  m->d_wtpack, m->d_rsk,   m->d_ws,
                   m->d_ell,    m->d_cnt,   m->d_spstat, m->d_pairs};
   for (void* p : ptrs)
@@ -275,6 +279,11 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     // batches in flight on plain streams take disjoint halves of the chip; A/B against CU-masked streams)
     if (const char* pad = getenv("DFWFM_R32_LDS"))
       if (m->r32 && (size_t)atol(pad) > m->lds_r32 && atol(pad) <= 160 * 1024) m->lds_r32 = (size_t)atol(pad);
+    // the wave-specialised 16-sample form for a lone batch that gives each CU at most one 16-sample tile (same
+    // shapes as fwd32; DFWFM_WS=0 keeps fwd_kernel there, for A/B)
+    const char* ws = getenv("DFWFM_WS");
+    m->ws = (c.use_deep && fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG) && (!ws || atoi(ws) != 0)) ? 1 : 0;
+    m->lds_ws = m->ws ? fwd16ws_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
   }
   // split forward (opt-in, DFWFM_SPLIT=1): the gather / shallow part and the MLP as two launches, each
   // with its own roofline (HBM-bound gather, MFMA-bound MLP) for profiling.  Measured slower than the
@@ -296,7 +305,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     free_model(m);
     return rc;
   }
-  if ((rc = dev_alloc(&m->d_rsk, (size_t)m->MT * m->S * 64))) {
+  if ((rc = dev_alloc(&m->d_rsk, (size_t)m->MT * m->S * 64)) || (rc = dev_alloc(&m->d_utri, (size_t)F * F))) {
     free_model(m);
     return rc;
   }
@@ -318,6 +327,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   }
   e = hipMemset(m->d_err, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(m->d_upack, 0, sizeof(float) * (size_t)m->MT * m->S * 64);
+  if (e == hipSuccess) e = hipMemset(m->d_utri, 0, sizeof(float) * (size_t)F * F);
   if (e != hipSuccess) {
     free_model(m);
     return hip_fail(e, "hipMemset");
@@ -396,6 +406,7 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
     const int64_t tot = (int64_t)m->MT * m->S * 64;
     job(kPackFwfm, field_cov, m->d_upack, tot, m->F, c.use_fm ? 1 : 0, m->S);
     job(kPackFwfmSym, field_cov, m->d_rsk, tot, m->F, c.use_fm ? 1 : 0, m->S);
+    job(kPackFwfmTri, field_cov, m->d_utri, (int64_t)m->F * m->F, m->F, c.use_fm ? 1 : 0, 0);
   }
   if (m->flags & kFoFwlw) job(kPackPad, fwfm_lin, m->d_fwlw, m->F * m->D, m->F * m->D, 0, 0);
   if (m->flags & kFoLw) job(kPackPad, fm_1st, m->d_lw, m->F, m->F, 0, 0);
@@ -455,6 +466,7 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.out = out;
   a.err = m->d_err;
   a.upack = m->d_upack;
+  a.utri = m->d_utri;
   a.pairs = m->d_pairs;
   a.npairs = m->npairs;
   a.fwlw = m->d_fwlw;
@@ -554,6 +566,10 @@ std::mutex g_cu_mu;
 
 int stream_cu_count(dfwfm_model* m, void* stream) {
   std::lock_guard<std::mutex> lock(g_cu_mu);
+  if (m->dev_cus == 0) {
+    hipDeviceProp_t prop;
+    m->dev_cus = hipGetDeviceProperties(&prop, m->device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
   const int cached = m->cu_n < 8 ? m->cu_n : 8;
   for (int i = 0; i < cached; ++i)
     if (m->cu_stream[i] == stream) return m->cu_count[i];
@@ -572,10 +588,37 @@ int stream_cu_count(dfwfm_model* m, void* stream) {
   return m->cu_count[slot];
 }
 
+// the MLP-free forward on the lane-per-(sample, column pair) kernel (dfwfm_fwfm.hip): no deep tower, no QR field, no
+// pruned-pair list, a supported shape; DFWFM_FWFM_LANE=0 keeps fwd_kernel's MLP-free form (A/B)
+bool use_fwfm_lane(const dfwfm_model* m, int flags) {
+  if (flags & (kHasDeep | kTrain | kHasQR | kPairs)) return false;
+  if (!fwfm_lane_supported(m->F, m->num, m->D)) return false;
+  const char* v = getenv("DFWFM_FWFM_LANE");
+  return !v || atoi(v) != 0;
+}
+
+// fwd32 (32-sample workgroups) when its workgroups give every CU of the stream two of them (two per CU hide each
+// other's gather and shallow phases); on a CU-masked stream (the caller runs several batches side by side, one
+// stream per part of the chip) one per CU is enough.  Otherwise the 16-sample kernel: twice the workgroups for the
+// same rows -- a lone 8192-row batch is 512 of them, two per CU, where fwd32 would leave each CU one.
 bool use_fwd32(dfwfm_model* m, int64_t batch, void* stream) {
   if (m->r32 == 0) return false;
   if (m->r32 == 2) return true;
-  return (batch + 31) / 32 >= stream_cu_count(m, stream);
+  const int cus = stream_cu_count(m, stream);
+  const bool masked = cus < m->dev_cus;
+  return (batch + 31) / 32 >= (masked ? 1 : 2) * (int64_t)cus;
+}
+
+// fwd16ws when the launch's 16-sample tiles give no CU of the stream a second one (call after use_fwd32 said no)
+bool use_fwd16ws(dfwfm_model* m, int64_t batch, void* stream) {
+  if (m->ws == 0) return false;
+  return (batch + kBM - 1) / kBM <= (int64_t)stream_cu_count(m, stream);
+}
+
+// the deep forward's kernel for `rows` rows on `stream`: 2 fwd32, 1 fwd16ws, 0 fwd_kernel
+int deep_form(dfwfm_model* m, int64_t rows, void* stream) {
+  if (use_fwd32(m, rows, stream)) return 2;
+  return use_fwd16ws(m, rows, stream) ? 1 : 0;
 }
 
 }  // namespace
@@ -598,13 +641,17 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
     if (!pr || atoi(pr) != 0) a.flags |= kPrio;
     if (const char* pe = getenv("DFWFM_PRIO_EPI"); !pe || atoi(pe) != 0) a.flags |= kPrioEpi;
     if (const char* dt = getenv("DFWFM_DEFER_TAIL"); !dt || atoi(dt) != 0) a.flags |= kDeferTail;
+    if (const char* nt = getenv("DFWFM_NT_ROWS"); nt && atoi(nt) != 0) a.flags |= kNtRows;
   }
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
-  hipError_t e = use_fwd32(m, batch, stream) ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
-                            : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
-                                             (hipStream_t)stream);
+  const int form = use_fwfm_lane(m, a.flags) ? -1 : deep_form(m, batch, stream);
+  hipError_t e = form == -1 ? launch_fwfm_lane(a, (hipStream_t)stream)
+                 : form == 2 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                 : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
+                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
+                                              (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
 }
@@ -628,8 +675,17 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     return DFWFM_OK;
   }
   if ((int64_t)nb * ((batch + kBM - 1) / kBM) > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "batch set too large");
-  const bool r32 = use_fwd32(m, (int64_t)nb * batch, stream);
-  const int rows = r32 ? 32 : kBM;
+  bool lane = false;
+  {
+    FwdArgs probe;
+    fill_forward_args(m, probe, xi[0], xi_stride, xv[0], xv_stride, batch, out[0]);
+    lane = use_fwfm_lane(m, probe.flags);
+  }
+  // the kernel for the first launch's rows (a set of up to kMaxSet batches); later launches of a larger set use it too
+  const int64_t set_rows = (int64_t)(nb < kMaxSet ? nb : kMaxSet) * batch;
+  const int form = lane ? -1 : deep_form(m, set_rows, stream);
+  const bool r32 = form == 2;
+  const int rows = lane ? fwfm_lane_rows(m->D) : (r32 ? 32 : kBM);
   for (int32_t i0 = 0; i0 < nb; i0 += kMaxSet) {
     const int32_t n = nb - i0 < kMaxSet ? nb - i0 : kMaxSet;
     FwdArgs a;
@@ -639,6 +695,7 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     // the next K loop -- 30.33 -> 30.08 us per batch at 2000 steps, 31.3 -> 31.05 on a 20-batch set (r03be)
     if (const char* pe = getenv("DFWFM_PRIO_EPI"); !pe || atoi(pe) != 0) a.flags |= kPrioEpi;
     if (const char* dt = getenv("DFWFM_DEFER_TAIL"); !dt || atoi(dt) != 0) a.flags |= kDeferTail;
+    if (const char* nt = getenv("DFWFM_NT_ROWS"); nt && atoi(nt) != 0) a.flags |= kNtRows;
     a.tail = m->tailI;
     if (n > 1) {
       a.nb = n;
@@ -651,9 +708,11 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     }
     int rc = diag_stamps_buffer(m, (int64_t)n * a.tiles * rows, 1, &a.stamps);
     if (rc != DFWFM_OK) return rc;
-    const hipError_t e = r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
-                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
-                                              (hipStream_t)stream);
+    const hipError_t e = lane  ? launch_fwfm_lane(a, (hipStream_t)stream)
+                         : r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                         : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
+                                     : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
+                                                      (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "batch-set forward launch");
   }
   return DFWFM_OK;

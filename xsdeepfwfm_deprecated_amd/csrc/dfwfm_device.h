@@ -80,6 +80,30 @@ __device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict_
   }
 }
 
+// the same loads marked non-temporal (the nt cache policy): embedding rows are read once per sample, so they should
+// not push the MLP weights every workgroup re-reads out of the XCD's L2
+template <int D>
+__device__ __forceinline__ void load_row_nt(float (&v)[D], const float* __restrict__ src) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  if constexpr (D % 4 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 4) {
+      const f4 x = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + d));
+      v[d] = x.x; v[d + 1] = x.y; v[d + 2] = x.z; v[d + 3] = x.w;
+    }
+  } else if constexpr (D % 2 == 0) {
+#pragma unroll
+    for (int d = 0; d < D; d += 2) {
+      const f2 x = __builtin_nontemporal_load(reinterpret_cast<const f2*>(src + d));
+      v[d] = x.x; v[d + 1] = x.y;
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = __builtin_nontemporal_load(src + d);
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void store_row(float* dst, const float (&v)[D]) {
   if constexpr (D % 4 == 0) {

@@ -75,7 +75,7 @@ template <int TPW, int RT, int NG, int NS>
 __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __restrict__ act, int SA,
                                           const LayerStream<TPW, 1, NG>& ls, f32x4 (&b0)[TPW], f32x4 (&b1)[TPW],
                                           f32x4 (&b2)[TPW], int lane, const TailStream<NG>& ts, f32x4 (&tp)[RT],
-                                          bool mid_barrier) {
+                                          bool mid_barrier, int bar_at = -1) {
   const int voff = lane * 16;
   const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
   float4 a0[RT], a1[RT], a2[RT];
@@ -91,6 +91,7 @@ __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __
     float4 (&AX)[RT] = (i % 3 == 0) ? a0 : ((i % 3 == 1) ? a1 : a2);
     float4 (&AZ)[RT] = (i % 3 == 0) ? a2 : ((i % 3 == 1) ? a0 : a1);
     if (i + 3 == NS && mid_barrier) __syncthreads();  // the previous layer's split tile (chunk NS - 1) is written
+    if (i == bar_at) __syncthreads();                 // fwd16ws: the rest of the input tile is written (barrier B)
     if (i + 2 < NS) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) AZ[rt] = *reinterpret_cast<const float4*>(arow + rt * 16 * SA + 16 * (i + 2));
@@ -326,9 +327,15 @@ fwd32_kernel(FwdArgs p) {
         for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
       }
       if (live[k] && needE) {
-        load_row<D>(va[k], pa[k]);
-        if constexpr (QR)
-          if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
+        if (flags & kNtRows) {
+          load_row_nt<D>(va[k], pa[k]);
+          if constexpr (QR)
+            if (mode[k] != 0) load_row_nt<D>(vb[k], pb[k]);
+        } else {
+          load_row<D>(va[k], pa[k]);
+          if constexpr (QR)
+            if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
+        }
       }
       if (live[k] && fo_tab) {
         fa[k] = *qa[k];
@@ -594,6 +601,440 @@ fwd32_kernel(FwdArgs p) {
   }
   stamp(p.stamps, 8, tid);
   stamp_end_rt(p.stamps, tid);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// fwd16ws_kernel: ONE 16-sample tile per workgroup with its waves specialised -- the form for a lone batch on the whole
+// chip (the reference's call pattern: one forward per batch, model/DeepFMs.py:750-780, :1012-1028), where a 4096-row
+// batch is one 16-row tile per CU and no second workgroup shares the CU to hide the gather and the FwFM.
+//   waves 0-7 (MLP): load Xv and the numerical fields' rows, write those E columns, preload layer 1's weights, and
+//     start layer 1's K loop on the numerical chunks while the categorical rows are still in flight;
+//   waves 8-11 (shallow): load the keys and the categorical / QR rows, write the rest of E and the first order, then
+//     -- concurrently with layer 1's K loop -- the FwFM second order (fwd_kernel's pieces on four waves) and
+//     first + second per sample, and exit.
+// Barriers: A (numerical E written), B (all of E written; inside layer 1's K loop, before the first chunk with a
+// categorical column is read), C (the shallow sums written; the MLP waves' barrier after layer 1's K loop).  A wave
+// that has ended no longer takes part in a barrier (s_barrier waits on the surviving waves), so the MLP waves'
+// later barriers are theirs alone.  Per sample the arithmetic is fwd_kernel's static form (the same FwFM pieces, the
+// same sums, the same K order): the same logits bits as fwd_kernel and fwd32_kernel.
+namespace {
+constexpr int kWsRows = 16;
+constexpr int kWsSW = 4;                    // shallow waves
+constexpr int kWsNTH = 64 * (kNG + kWsSW);  // 768 threads
+constexpr int kWsRPTN = 2;                  // numerical rows per MLP thread (16 * F <= 768 at F <= 48)
+constexpr int kWsRPTC = 3;                  // categorical rows per shallow thread
+
+__host__ __device__ inline Lds32 ldsws_layout(int F, int D, int MT, int S, int SX) {
+  Lds32 L;
+  int o = 0;
+  L.buf = o;   o += kWsRows * SX;
+  L.fs = o;    o += kWsRows;
+  L.dsum = o;  o += kNG * kWsRows;
+  int s = o;
+  L.desc = s;  s += r4(14 * F);
+  L.lw = s;    s += r4(F);
+  L.fwlw = s;  s += r4(F * D);
+  L.upk = s;   s += MT * S * 64;
+  L.fo = s;    s += kWsRows * r4(F);
+  L.part2 = s; s += MT * D * 16;
+  int t = o;
+  L.tailr = t; t += kNG * 64 * 4;
+  L.taild = t; t += 4 * kWsRows;
+  L.total = r4(s > t ? s : t);
+  return L;
+}
+}  // namespace
+
+template <int D, bool QR>
+__global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool mlpw = wave < kNG;
+  const int F = p.F;
+  const int num = p.num;
+  const int SX = p.SX;
+  const int flags = p.flags;
+  const int Fp = r4(F);
+  const Lds32 L = ldsws_layout(F, D, p.MT, p.S, SX);
+  float* buf = smem + L.buf;
+  float* fs = smem + L.fs;
+  float* dsum = smem + L.dsum;
+  FieldDev* desc = reinterpret_cast<FieldDev*>(smem + L.desc);
+  float* lw_s = smem + L.lw;
+  float* fwlw_s = smem + L.fwlw;
+  float* upk = smem + L.upk;
+  float* fo = smem + L.fo;
+  float* part2 = smem + L.part2;
+  float* tailr = smem + L.tailr;
+  float* taild = smem + L.taild;
+  const TileRef tr = tile_ref<kWsRows>(p);
+  const int64_t b0 = tr.b0;
+  stamp(p.stamps, 0, tid);
+  stamp_start_rt(p.stamps, tid);
+  const int g = wave;
+  LayerStream<kTPW, 1, kNG> ls;
+  f32x4 wb0[kTPW], wb1[kTPW], wb2[kTPW];
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float4*>(p.wpack), (short)0, p.wpack_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.mlp_b), (short)0, p.H * p.NT * 16 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.fc), (short)0, p.NT * 16 * 4, 0x00020000);
+  TailStream<kNG> ts;
+  constexpr int TT = kNG * kTPW;  // the split tile
+  const bool needE = (flags & kNeedE) != 0;
+  const bool fo_tab = (flags & kFoTables) != 0;
+  const int nrows = kWsRows * num;               // numerical rows (MLP threads)
+  const int crows = kWsRows * (F - num);         // categorical rows (shallow threads)
+  __shared__ int ws_done;                        // shallow waves whose FwFM pieces are written
+  if (tid == 64 * kNG) ws_done = 0;              // before barrier A; counted after barrier B
+
+  if constexpr (QR) {  // descriptors staged in LDS by every thread
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    for (int i = tid; i < 7 * F; i += kWsNTH) reinterpret_cast<u32x2*>(desc)[i] = reinterpret_cast<const u32x2*>(p.fields)[i];
+    __syncthreads();
+  }
+  auto fdesc = [&](int f) -> FieldDev { if constexpr (QR) return desc[f]; else return p.fields[f]; };
+
+  if (mlpw) {
+    // ---- MLP waves: numerical rows (E = v_f * Xv, first order emb1[0] * Xv), the E padding, layer 1's weights ----
+    float va[kWsRPTN][D], fa[kWsRPTN], xs[kWsRPTN];
+    bool live[kWsRPTN];
+#pragma unroll
+    for (int k = 0; k < kWsRPTN; ++k) {
+      const int r = tid + k * 64 * kNG;
+      const int f = r >> 4;
+      const int64_t gb = b0 + (r & 15);
+      live[k] = r < nrows && gb < p.batch;
+      xs[k] = live[k] ? tr.xv[gb * p.xv_stride + f] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kWsRPTN; ++k) {
+      const int r = tid + k * 64 * kNG;
+      const int f = r >> 4;
+      fa[k] = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) va[k][d] = 0.f;
+      if (live[k]) {
+        const FieldDev fd = fdesc(f);
+        if (needE) load_row<D>(va[k], fd.emb2);
+        if (fo_tab) fa[k] = *fd.emb1;
+      }
+    }
+    ls.init(wrsrc, 0, p.NC0, p.NT, g, 0);
+    ls.preload(wb0, wb1, lane * 16);
+    const int w = p.W0 - F * D;
+    for (int i = tid; i < kWsRows * w; i += 64 * kNG) {
+      const int b = i / w;
+      buf[b * SX + F * D + (i - b * w)] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kWsRPTN; ++k) {
+      const int r = tid + k * 64 * kNG;
+      if (r < nrows) {
+        const int f = r >> 4, b = r & 15;
+        if (needE) {
+          float e[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(0, va[k][d], 0.f, xs[k]) : 0.f;
+          store_row<D>(buf + b * SX + f * D, e);
+        }
+        fo[b * Fp + f] = live[k] ? combine(0, fa[k], 0.f, xs[k]) : 0.f;
+      }
+    }
+    __syncthreads();  // A: the numerical E columns
+  } else {
+    // ---- shallow waves: keys, categorical / QR rows, the shallow parameters -------------------------------------
+    if (flags & kPrio) __builtin_amdgcn_s_setprio(1);
+    const int st = tid - 64 * kNG;
+    constexpr int RQ = QR ? kWsRPTC : 1;
+    const float* pa[kWsRPTC];
+    const float* qa[kWsRPTC];
+    const float* pb[RQ];
+    const float* qb[RQ];
+    int mode[kWsRPTC];
+    bool live[kWsRPTC];
+#pragma unroll
+    for (int k = 0; k < kWsRPTC; ++k) {
+      const int r = st + k * 64 * kWsSW;
+      const int f = num + (r >> 4);
+      const int64_t gb = b0 + (r & 15);
+      live[k] = r < crows && gb < p.batch;
+      pa[k] = qa[k] = nullptr;
+      if constexpr (QR) pb[k] = qb[k] = nullptr;
+      mode[k] = 0;
+      if (!live[k]) continue;
+      const FieldDev fd = fdesc(f);
+      int64_t idx = tr.xi[gb * p.xi_stride + (f - num)];
+      if (idx < 0 || idx >= fd.n) {
+        atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
+        idx = 0;
+      }
+      if (!QR || fd.c == 0) {
+        pa[k] = fd.emb2 + idx * D;
+        if (fo_tab) qa[k] = fd.emb1 + idx;
+      } else if constexpr (QR) {
+        const int64_t q = idx / fd.c;
+        const int64_t rr = idx - q * fd.c;
+        mode[k] = fd.op == 0 ? 1 : 2;
+        pa[k] = fd.emb2 + q * D;
+        pb[k] = fd.emb2_r + rr * D;
+        if (fo_tab) {
+          qa[k] = fd.emb1 + q;
+          qb[k] = fd.emb1_r + rr;
+        }
+      }
+    }
+    float va[kWsRPTC][D], vb[RQ][D], fa[kWsRPTC], fb[RQ];
+#pragma unroll
+    for (int k = 0; k < kWsRPTC; ++k) {
+      fa[k] = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) va[k][d] = 0.f;
+      if constexpr (QR) {
+        fb[k] = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
+      }
+      if (live[k] && needE) {
+        load_row<D>(va[k], pa[k]);
+        if constexpr (QR)
+          if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
+      }
+      if (live[k] && fo_tab) {
+        fa[k] = *qa[k];
+        if constexpr (QR)
+          if (mode[k] != 0) fb[k] = *qb[k];
+      }
+    }
+    // the shallow parameters to LDS while the rows are in flight
+    const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
+    for (int i = st; i < n_upk; i += 64 * kWsSW) reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(p.upack)[i];
+    if (flags & kFoFwlw)
+      for (int i = st; i < F * D; i += 64 * kWsSW) fwlw_s[i] = p.fwlw[i];
+    if (flags & kFoLw)
+      for (int i = st; i < F; i += 64 * kWsSW) lw_s[i] = p.lw[i];
+    __syncthreads();  // A
+#pragma unroll
+    for (int k = 0; k < kWsRPTC; ++k) {
+      const int r = st + k * 64 * kWsSW;
+      if (r < crows) {
+        const int f = num + (r >> 4), b = r & 15;
+        if (needE) {
+          float e[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(mode[k], va[k][d], QR ? vb[k][d] : 0.f, 1.f) : 0.f;
+          store_row<D>(buf + b * SX + f * D, e);
+        }
+        fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], QR ? fb[k] : 0.f, 1.f) : 0.f;
+      }
+    }
+    __syncthreads();  // B: all of E
+    // ---- first order (fwlw) and the FwFM second order: fwd_kernel's pieces over the four shallow waves ----------
+    const int sw = wave - kNG;
+    if (flags & kFoFwlw) {
+      for (int r = st; r < kWsRows * F; r += 64 * kWsSW) {
+        const int f = r >> 4;
+        const int b = r & 15;
+        const float* e = buf + b * SX + f * D;
+        const float* wv = fwlw_s + f * D;
+        float sacc = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) sacc += e[d] * wv[d];
+        fo[b * Fp + f] = sacc;
+      }
+    }
+    if (flags & kHasSecond) {
+      const int S = p.S;
+      const int p_lo = p.fw_off4[sw], p_hi = p.fw_off4[sw + 1];
+      for (int pi = p_lo; pi < p_hi; ++pi) {
+        const int pc = p.fw_list4[pi];
+        const int m = pc / D;
+        const int nt = pc - m * D;
+        const int n = nt * 16 + (lane & 15);
+        const int b = n / D;
+        const float* ecol = buf + b * SX + (n - b * D);
+        const float* ua = upk + m * S * 64 + lane;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto group = [&](int s0, auto U_) {
+          constexpr int U = decltype(U_)::value;
+          float av[U], bv[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            av[u] = ua[(s0 + u) * 64];
+            bv[u] = ecol[(4 * (s0 + u) + (lane >> 4)) * D];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+        };
+        int s0 = 4 * m;
+        for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
+        const int rem = S - s0;
+        if (rem == 3) group(s0, std::integral_constant<int, 3>{});
+        else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
+        else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * m + 4 * (lane >> 4) + r;
+          const int kk = (k < F ? k : 0) * D;
+          v = fmaf(k < F ? ecol[kk] : 0.f, acc[r], v);
+        }
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 16) part2[pc * 16 + lane] = v;
+      }
+    }
+    // the pieces reach the per-sample sums of every shallow wave through LDS; the MLP waves are inside layer 1's K
+    // loop, so instead of a workgroup barrier the four shallow waves count in on an LDS word (all four arrive:
+    // no shallow wave leaves before this point)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) atomicAdd(&ws_done, 1);
+    while (__hip_atomic_load(&ws_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWsSW) __builtin_amdgcn_s_sleep(1);
+    {
+      const int b = sw * 4 + (lane >> 4);
+      const int q = lane & 15;
+      float first = 0.f, second = 0.f;
+      for (int f = q; f < F; f += 16) {
+        const float x = fo[b * Fp + f];
+        first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
+      }
+      if (flags & kHasSecond) {
+        for (int d = q; d < D; d += 16) {
+          const int n = b * D + d;
+          for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
+        }
+      }
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) {
+        first += __shfl_xor(first, o);
+        second += __shfl_xor(second, o);
+      }
+      if (q == 0) fs[b] = first + second;
+    }
+    __syncthreads();  // C: the MLP waves' barrier after layer 1's K loop
+    return;
+  }
+
+  // ---- phase M (MLP waves): layer 1 starts on the numerical chunks; barrier B before the first categorical one ----
+  const int cB = (num * D) / 16;  // first K chunk with a categorical column
+  if (cB < 2) __syncthreads();    // B (the loop's first two activation reads would need it)
+  auto load_bias = [&](f32x4 (&bq)[kTPW], int h, int nq) {
+#pragma unroll
+    for (int j = 0; j < kTPW; ++j) {
+      int t = g + kNG * j;
+      t = t < p.NT ? t : p.NT - 1;
+      bq[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            brsrc, nq * 4, __builtin_amdgcn_readfirstlane((h * p.NT + t) * 64), 0));
+    }
+  };
+  f32x4 bq[kTPW];
+  load_bias(bq, 0, 4 * (lane >> 4));
+  int layer_off = 0;
+  for (int h = 0; h < p.H; ++h) {
+    int lv = lane;
+    asm volatile("" : "+v"(lv));
+    const int rowl = lv & 15;
+    const int nq = 4 * (lv >> 4);
+    const int NC = h == 0 ? p.NC0 : p.NT;
+    const bool last = h == p.H - 1;
+    const int boff = __builtin_amdgcn_readfirstlane((h * p.NT + TT) * 64 + (g & 3) * 4);
+    const int ntail = TT * 16 + nq + (g & 3);
+    const float bn_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, nq * 4, boff, 0));
+    f32x4 acc[1][kTPW];
+#pragma unroll
+    for (int j = 0; j < kTPW; ++j) acc[0][j] = bq[j];
+    ts.init(layer_off, NC, TT, g);
+    f32x4 tp[1];
+    k_loop_rt<kTPW, 1, kNG, kNS>(acc, buf, SX, ls, wb0, wb1, wb2, lane, ts, tp, h > 0 && (flags & kDeferTail),
+                                 h == 0 && cB >= 2 ? cB - 2 : -1);
+    if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(1);
+    if (h == 0) stamp(p.stamps, 12, tid);
+    __syncthreads();  // every wave has read the layer's input (h == 0: C, the shallow sums are in fs)
+    reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = tp[0];
+    float dpart = 0.f;
+    {
+      float* orow = buf + rowl * SX + nq;
+#pragma unroll
+      for (int j = 0; j < kTPW; ++j) {
+        const int t = g + kNG * j;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = relu_keep_nan(acc[0][j][r]);
+        if (!last) {
+          *reinterpret_cast<f32x4*>(orow + t * 16) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          const f32x4 wf = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(frsrc, nq * 4, t * 64, 0));
+          dpart = fmaf(v[0], wf[0], dpart);
+          dpart = fmaf(v[1], wf[1], dpart);
+          dpart = fmaf(v[2], wf[2], dpart);
+          dpart = fmaf(v[3], wf[3], dpart);
+        }
+      }
+    }
+    if (last) {
+      float d = dpart;
+      d += __shfl_xor(d, 16);
+      d += __shfl_xor(d, 32);
+      if (lane < 16) dsum[g * kWsRows + rowl] = d;
+    }
+    layer_off += p.NT * NC * 64;
+    if (!last) {
+      ls.init(wrsrc, layer_off, p.NT, p.NT, g, 0);
+      ls.preload(wb0, wb1, lane * 16);
+      load_bias(bq, h + 1, nq);
+    }
+    if (h == 0) stamp(p.stamps, 13, tid);
+    __syncthreads();
+    if (g < 4) {
+      const bool valid = ntail < p.N;
+      float wf_t = 0.f;
+      if (last)
+        wf_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             frsrc, nq * 4, __builtin_amdgcn_readfirstlane(TT * 64 + g * 4), 0));
+      const float* tpp = tailr + lane * 4 + g;
+      float sum = tpp[0];
+#pragma unroll
+      for (int w = 1; w < kNG; ++w) sum += tpp[w * 256];
+      const float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
+      if (!last) {
+        buf[rowl * SX + TT * 16 + nq + g] = v;
+      } else {
+        float c = v * wf_t;
+        c += __shfl_xor(c, 16);
+        c += __shfl_xor(c, 32);
+        if (lane < 16) taild[g * kWsRows + rowl] = c;
+      }
+    }
+    if (last || !(flags & kDeferTail)) __syncthreads();
+    if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(0);
+    stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
+  }
+  if (tid < kWsRows && b0 + tid < p.batch) {
+    float deepv = dsum[tid];
+#pragma unroll
+    for (int w = 1; w < kNG; ++w) deepv += dsum[w * kWsRows + tid];
+    deepv += ((taild[tid] + taild[kWsRows + tid]) + taild[2 * kWsRows + tid]) + taild[3 * kWsRows + tid];
+    tr.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
+  }
+  stamp(p.stamps, 8, tid);
+  stamp_end_rt(p.stamps, tid);
+}
+
+size_t fwd16ws_lds_bytes(int F, int D, int MT, int S, int SX) {
+  return sizeof(float) * (size_t)ldsws_layout(F, D, MT, S, SX).total;
+}
+
+hipError_t launch_fwd16ws(const FwdArgs& a, int D, size_t lds, hipStream_t s) {
+  if (D != 10) return hipErrorInvalidValue;
+  auto k = (a.flags & kHasQR) ? fwd16ws_kernel<10, true> : fwd16ws_kernel<10, false>;
+  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3(fwd_grid(a, kWsRows)), dim3(kWsNTH), lds, s, a);
+  return hipGetLastError();
 }
 
 size_t fwd32_lds_bytes(int F, int D, int MT, int S, int SX) {

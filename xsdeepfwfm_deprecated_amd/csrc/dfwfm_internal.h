@@ -30,6 +30,7 @@ constexpr int kPrio = 256;     // raise the wave priority for the phases before 
 constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables)
 constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
 constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
+constexpr int kNtRows = 8192;  // embedding-row loads with the non-temporal cache policy (A/B: DFWFM_NT_ROWS)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kMaxH = 16;      // hidden layers
 constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)
@@ -59,6 +60,7 @@ struct FwdArgs {
   float* out;
   int32_t* err;
   const float* upack;  // FwFM A-operand fragments [MT][S][64]: strictly-upper (R + R^T)/2
+  const float* utri;   // the same U row-major [F][F] (zero on and below the diagonal): the MLP-free lane kernel
   const int2* pairs;   // kPairs: the nonzero strictly-upper entries of (R + R^T)/2, (k | l << 16, w bits), k-major
   int32_t npairs;
   const float* fwlw;   // [F*D]
@@ -345,7 +347,7 @@ inline hipError_t ensure_lds_limit(const void* fn, size_t lds) {
 }
 
 // One packing job of set_dense (see pack_dense_kernel).
-enum PackType : int32_t { kPackPad = 0, kPackLinear = 1, kPackLinearT = 2, kPackFwfm = 3, kPackFwfmSym = 4 };
+enum PackType : int32_t { kPackPad = 0, kPackLinear = 1, kPackLinearT = 2, kPackFwfm = 3, kPackFwfmSym = 4, kPackFwfmTri = 5 };
 struct PackJob {
   const float* src;
   float* dst;
@@ -394,6 +396,14 @@ hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 bool fwd32_supported(int F, int D, int H, int NT, int NC0, int tailI, int NG);
 size_t fwd32_lds_bytes(int F, int D, int MT, int S, int SX);
 hipError_t launch_fwd32(const FwdArgs& a, int D, size_t lds, hipStream_t s);
+// one 16-sample tile per workgroup with specialised waves (MLP / gather + FwFM): a lone batch on the whole chip;
+// the same shapes as fwd32 (fwd32_supported), bit-identical logits
+size_t fwd16ws_lds_bytes(int F, int D, int MT, int S, int SX);
+hipError_t launch_fwd16ws(const FwdArgs& a, int D, size_t lds, hipStream_t s);
+// the MLP-free forward with a lane per (sample, column pair) (dfwfm_fwfm.hip): fwfm_lane_rows samples per workgroup
+bool fwfm_lane_supported(int F, int num, int D);
+int fwfm_lane_rows(int D);
+hipError_t launch_fwfm_lane(const FwdArgs& a, hipStream_t s);
 // per-embedding-size launchers, each compiled in its own translation unit (-DDFWFM_KD=<D>)
 #define DFWFM_PER_D_CAT2(a, b) a##b
 #define DFWFM_PER_D_CAT(a, b) DFWFM_PER_D_CAT2(a, b)

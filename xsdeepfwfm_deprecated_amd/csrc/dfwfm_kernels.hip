@@ -823,6 +823,7 @@ fwd_kernel(FwdArgs p) {
 //                  the diagonal is removed by :366-367); FM: 1 above the diagonal.  Fragment order
 //                  out[(m*S + s)*64 + lane] = U[16m + (lane&15)][4s + (lane>>4)]
 //   kPackFwfmSym   the backward's symmetric off-diagonal (R + R^T)/2 (FM: ones), same order
+//   kPackFwfmTri   U row-major [F][F], zero on and below the diagonal (the MLP-free lane kernel's scalar reads)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void pack_elem(const PackJob& j, int64_t i) {
   switch (j.type) {
@@ -845,6 +846,12 @@ __device__ __forceinline__ void pack_elem(const PackJob& j, int64_t i) {
         v[s] = (n < N && k < K) ? j.src[(int64_t)n * K + k] : 0.f;
       }
       reinterpret_cast<float4*>(j.dst)[i] = make_float4(v[0], v[1], v[2], v[3]);
+      break;
+    }
+    case kPackFwfmTri: {
+      const int F = j.a, mode = j.b;
+      const int k = (int)(i / F), l = (int)(i - (int64_t)k * F);
+      j.dst[i] = l > k ? ((mode == 1) ? 1.f : (j.src[l * F + k] + j.src[k * F + l]) * 0.5f) : 0.f;
       break;
     }
     case kPackFwfm:

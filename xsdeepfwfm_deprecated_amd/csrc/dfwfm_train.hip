@@ -638,8 +638,9 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
 }
 
 // Sum of the per-block partials, added into the grads (accumulate, like autograd): 64 outputs per
-// workgroup, each wave sums a quarter of the blocks (8 loads in flight per lane), then the four
-// quarters are combined in a fixed order (deterministic).
+// workgroup, each wave sums a quarter of the blocks in block order (32 loads in flight per lane: the sum is a
+// chain of dependent L2 round trips otherwise -- 8 in flight made it 6 us alone and ~39 us beside the weight
+// GEMM), then the four quarters are combined in a fixed order (deterministic).
 __global__ void __launch_bounds__(256) reduce_final_kernel(RedArgs a, int nblk) {
   __shared__ float q4[4][64];
   const int F = a.F, D = a.D, N = a.N, num = a.num, FD = F * D, numD = num * D;
@@ -651,6 +652,13 @@ __global__ void __launch_bounds__(256) reduce_final_kernel(RedArgs a, int nblk) 
   float s = 0.f;
   if (o < P) {
     int b = b0;
+    for (; b + 32 <= b1; b += 32) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = a.part[(size_t)(b + u) * P + o];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += v[u];
+    }
     for (; b + 8 <= b1; b += 8) {
       float v[8];
 #pragma unroll
