@@ -185,7 +185,10 @@ def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT / DFWFM_R32 select the A/B variants."""
     if r32_on(config, cu_mask, batch_set):
-        return f"dfwfm::fwd32_kernel<10,{'true' if config == 'qr' else 'false'}>"
+        qr = 'true' if config == 'qr' else 'false'
+        if cu_mask in (None, "none") and os.environ.get("DFWFM_PERSIST", "1") != "0":
+            return f"dfwfm::fwdp_kernel<10,{qr}>"  # persistent, gather waves a tile ahead (DESIGN.md 3.6)
+        return f"dfwfm::fwd32_kernel<10,{qr}>"
     if config == "fwfm" and os.environ.get("DFWFM_FWFM_LANE", "1") != "0":
         return "dfwfm::fwfm_lane_kernel<39,13,10>"  # MLP-free, a lane per (sample, column pair)
     if config in ("fwfm", "fwfm_pruned"):

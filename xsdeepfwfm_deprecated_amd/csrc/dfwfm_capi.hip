@@ -29,6 +29,8 @@ struct dfwfm_model {
   size_t lds_r32;
   int ws;              // fwd16ws_kernel usable (one 16-sample tile per CU or fewer)
   size_t lds_ws;
+  int persist;         // fwd32's launches as the persistent fwdp_kernel (DFWFM_PERSIST=0: plain fwd32, A/B)
+  size_t lds_p;
   void* cu_stream[8];  // streams whose CU counts are cached (hipExtStreamGetCUMask), round-robin replaced
   int cu_count[8], cu_n, cu_next;
   int dev_cus;         // CUs of the device (0 until the first stream_cu_count)
@@ -284,6 +286,10 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     const char* ws = getenv("DFWFM_WS");
     m->ws = (c.use_deep && fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG) && (!ws || atoi(ws) != 0)) ? 1 : 0;
     m->lds_ws = m->ws ? fwd16ws_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
+    const char* pe = getenv("DFWFM_PERSIST");
+    m->persist = (m->r32 && (!pe || atoi(pe) != 0)) ? 1 : 0;
+    m->lds_p = m->persist ? fwdp_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
+    if (m->lds_p > 160 * 1024) m->persist = 0;
   }
   // split forward (opt-in, DFWFM_SPLIT=1): the gather / shallow part and the MLP as two launches, each
   // with its own roofline (HBM-bound gather, MFMA-bound MLP) for profiling.  Measured slower than the
@@ -615,9 +621,11 @@ bool use_fwd16ws(dfwfm_model* m, int64_t batch, void* stream) {
   return (batch + kBM - 1) / kBM <= (int64_t)stream_cu_count(m, stream);
 }
 
-// the deep forward's kernel for `rows` rows on `stream`: 2 fwd32, 1 fwd16ws, 0 fwd_kernel
+// the deep forward's kernel for `rows` rows on `stream`: 3 fwdp (fwd32's rows on an unmasked stream: persistent,
+// one workgroup per CU), 2 fwd32 (a CU-masked stream shares its CUs with another stream's launches, two workgroups
+// per CU), 1 fwd16ws, 0 fwd_kernel
 int deep_form(dfwfm_model* m, int64_t rows, void* stream) {
-  if (use_fwd32(m, rows, stream)) return 2;
+  if (use_fwd32(m, rows, stream)) return (m->persist && stream_cu_count(m, stream) >= m->dev_cus) ? 3 : 2;
   return use_fwd16ws(m, rows, stream) ? 1 : 0;
 }
 
@@ -647,7 +655,9 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
   const int form = use_fwfm_lane(m, a.flags) ? -1 : deep_form(m, batch, stream);
+  if (form == 3) a.tiles = (int32_t)((batch + 31) / 32);
   hipError_t e = form == -1 ? launch_fwfm_lane(a, (hipStream_t)stream)
+                 : form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
                  : form == 2 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                  : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
                              : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
@@ -684,7 +694,7 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
   // the kernel for the first launch's rows (a set of up to kMaxSet batches); later launches of a larger set use it too
   const int64_t set_rows = (int64_t)(nb < kMaxSet ? nb : kMaxSet) * batch;
   const int form = lane ? -1 : deep_form(m, set_rows, stream);
-  const bool r32 = form == 2;
+  const bool r32 = form >= 2;
   const int rows = lane ? fwfm_lane_rows(m->D) : (r32 ? 32 : kBM);
   for (int32_t i0 = 0; i0 < nb; i0 += kMaxSet) {
     const int32_t n = nb - i0 < kMaxSet ? nb - i0 : kMaxSet;
@@ -708,7 +718,9 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     }
     int rc = diag_stamps_buffer(m, (int64_t)n * a.tiles * rows, 1, &a.stamps);
     if (rc != DFWFM_OK) return rc;
+    if (form == 3) a.tiles = (int32_t)((batch + 31) / 32);
     const hipError_t e = lane  ? launch_fwfm_lane(a, (hipStream_t)stream)
+                         : form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
                          : r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                          : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
                                      : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,

@@ -80,7 +80,16 @@ __global__ void __launch_bounds__(64) fwfm_lane_kernel(FwdArgs p) {
   const bool fo_tab = (flags & kFoTables) != 0;
   const bool lw = (flags & kFoLw) != 0;
   f2 x[F];
-  float first = 0.f;
+  // the first order's terms (numerical weights times Xv up to 63) cancel to a logit of ~1e2 in the FwFM-only models:
+  // the lane's sum carries its rounding errors along (two-sum), which keeps the logits inside the north-star bar of
+  // the reference's own fp32 result (golden fwfm_nolw: 1.15e-5 plain, 7.6e-6 compensated, the reference 6.3e-6)
+  float first = 0.f, fcomp = 0.f;
+  auto add_first = [&](float v) {
+    const float s = first + v;
+    const float bb = s - first;
+    fcomp += (first - (s - bb)) + (v - bb);
+    first = s;
+  };
 #pragma unroll
   for (int f = 0; f < F; ++f) {
     const float* e2 = fd[f].emb2;
@@ -99,7 +108,7 @@ __global__ void __launch_bounds__(64) fwfm_lane_kernel(FwdArgs p) {
       if (live && need_e) x[f] = *reinterpret_cast<const f2*>(e2 + r * D + 2 * j);
       if (live && fo_tab && j == f % LPS) fo = e1[r];
     }
-    if (fo_tab && j == f % LPS) first = lw ? fmaf(fo, ((cf_t)p.lw)[f], first) : first + fo;
+    if (fo_tab && j == f % LPS) add_first(lw ? fo * ((cf_t)p.lw)[f] : fo);
   }
 
   // ---- fwlw first order: sum_d fwlw[f][d] e[f][d] over this lane's d (lw-projected when use_lw) -------------------
@@ -108,9 +117,10 @@ __global__ void __launch_bounds__(64) fwfm_lane_kernel(FwdArgs p) {
     for (int f = 0; f < F; ++f) {
       const f2 w = *reinterpret_cast<const f2*>(p.fwlw + f * D + 2 * j);
       const float v = fmaf(x[f].y, w.y, x[f].x * w.x);
-      first = lw ? fmaf(v, ((cf_t)p.lw)[f], first) : first + v;
+      add_first(lw ? v * ((cf_t)p.lw)[f] : v);
     }
   }
+  first += fcomp;
 
   // ---- second order: sum_k x_k . (sum_{l>k} U[k][l] x_l), U wave-uniform ------------------------------------------
   float second = 0.f;

@@ -399,6 +399,10 @@ hipError_t launch_fwd32(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 // one 16-sample tile per workgroup with specialised waves (MLP / gather + FwFM): a lone batch on the whole chip;
 // the same shapes as fwd32 (fwd32_supported), bit-identical logits
 size_t fwd16ws_lds_bytes(int F, int D, int MT, int S, int SX);
+// persistent batch-set form of fwd32 (one workgroup per CU walking 32-sample tiles, gather waves a tile ahead of
+// the MLP waves): a.tiles must hold the 32-sample tiles per batch; bit-identical logits
+size_t fwdp_lds_bytes(int F, int D, int MT, int S, int SX);
+hipError_t launch_fwdp(const FwdArgs& a, int D, size_t lds, int cus, hipStream_t s);
 hipError_t launch_fwd16ws(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 // the MLP-free forward with a lane per (sample, column pair) (dfwfm_fwfm.hip): fwfm_lane_rows samples per workgroup
 bool fwfm_lane_supported(int F, int num, int D);
