@@ -50,7 +50,7 @@ struct dfwfm_model {
   // device state (owned)
   FieldDev* d_fields;
   float* d_upack;  // FwFM A-operand fragments [MT][S][64]
-  float* d_utri;   // the same U row-major [F][F] (MLP-free lane kernel)
+  float* d_utri;   // the same U row-major [F][r4(F)] (MLP-free lane kernel)
   int2* d_pairs;   // build_fwfm_pairs: nonzero pairs of a pruned R (F (F - 1) / 2 capacity)
   int32_t npairs;
   int32_t* d_err;
@@ -311,7 +311,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     free_model(m);
     return rc;
   }
-  if ((rc = dev_alloc(&m->d_rsk, (size_t)m->MT * m->S * 64)) || (rc = dev_alloc(&m->d_utri, (size_t)F * F))) {
+  if ((rc = dev_alloc(&m->d_rsk, (size_t)m->MT * m->S * 64)) || (rc = dev_alloc(&m->d_utri, (size_t)F * r4(F)))) {
     free_model(m);
     return rc;
   }
@@ -333,7 +333,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   }
   e = hipMemset(m->d_err, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(m->d_upack, 0, sizeof(float) * (size_t)m->MT * m->S * 64);
-  if (e == hipSuccess) e = hipMemset(m->d_utri, 0, sizeof(float) * (size_t)F * F);
+  if (e == hipSuccess) e = hipMemset(m->d_utri, 0, sizeof(float) * (size_t)F * r4(F));
   if (e != hipSuccess) {
     free_model(m);
     return hip_fail(e, "hipMemset");
@@ -412,7 +412,7 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
     const int64_t tot = (int64_t)m->MT * m->S * 64;
     job(kPackFwfm, field_cov, m->d_upack, tot, m->F, c.use_fm ? 1 : 0, m->S);
     job(kPackFwfmSym, field_cov, m->d_rsk, tot, m->F, c.use_fm ? 1 : 0, m->S);
-    job(kPackFwfmTri, field_cov, m->d_utri, (int64_t)m->F * m->F, m->F, c.use_fm ? 1 : 0, 0);
+    job(kPackFwfmTri, field_cov, m->d_utri, (int64_t)m->F * r4(m->F), m->F, c.use_fm ? 1 : 0, r4(m->F));
   }
   if (m->flags & kFoFwlw) job(kPackPad, fwfm_lin, m->d_fwlw, m->F * m->D, m->F * m->D, 0, 0);
   if (m->flags & kFoLw) job(kPackPad, fm_1st, m->d_lw, m->F, m->F, 0, 0);

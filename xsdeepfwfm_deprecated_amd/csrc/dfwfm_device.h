@@ -16,6 +16,10 @@ __device__ __forceinline__ float relu_keep_nan(float v) { return v < 0.f ? 0.f :
 __device__ __forceinline__ void stamp(uint64_t* st, int slot, int tid) {
   if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
 }
+// the same, recorded by thread `who` (a wave-specialised kernel's other wave group)
+__device__ __forceinline__ void stamp_by(uint64_t* st, int slot, int tid, int who) {
+  if (st != nullptr && tid == who) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
+}
 
 // the batch and first row of this workgroup's tile (ROWS samples per workgroup), and that batch's inputs and logits:
 // the batch set of dfwfm_forward_batches (p.nb > 1), else the one batch of the launch

@@ -745,6 +745,7 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
       }
     }
     __syncthreads();  // A: the numerical E columns
+    stamp(p.stamps, 1, tid);
   } else {
     // ---- shallow waves: keys, categorical / QR rows, the shallow parameters -------------------------------------
     if (flags & kPrio) __builtin_amdgcn_s_setprio(1);
@@ -817,6 +818,7 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
     if (flags & kFoLw)
       for (int i = st; i < F; i += 64 * kWsSW) lw_s[i] = p.lw[i];
     __syncthreads();  // A
+    stamp_by(p.stamps, 2, tid, 64 * kNG);
 #pragma unroll
     for (int k = 0; k < kWsRPTC; ++k) {
       const int r = st + k * 64 * kWsSW;
@@ -831,7 +833,9 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
         fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], QR ? fb[k] : 0.f, 1.f) : 0.f;
       }
     }
+    stamp_by(p.stamps, 9, tid, 64 * kNG);
     __syncthreads();  // B: all of E
+    stamp_by(p.stamps, 3, tid, 64 * kNG);
     // ---- first order (fwlw) and the FwFM second order: fwd_kernel's pieces over the four shallow waves ----------
     const int sw = wave - kNG;
     if (flags & kFoFwlw) {
@@ -891,6 +895,7 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
     // the pieces reach the per-sample sums of every shallow wave through LDS; the MLP waves are inside layer 1's K
     // loop, so instead of a workgroup barrier the four shallow waves count in on an LDS word (all four arrive:
     // no shallow wave leaves before this point)
+    stamp_by(p.stamps, 10, tid, 64 * kNG);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) atomicAdd(&ws_done, 1);
     while (__hip_atomic_load(&ws_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWsSW) __builtin_amdgcn_s_sleep(1);
@@ -915,6 +920,7 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
       }
       if (q == 0) fs[b] = first + second;
     }
+    stamp_by(p.stamps, 11, tid, 64 * kNG);
     __syncthreads();  // C: the MLP waves' barrier after layer 1's K loop
     return;
   }
@@ -1118,7 +1124,7 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
   const int mine = (ntiles - t0 + G - 1) / G;     // tiles of this workgroup: t0, t0 + G, ...
   const bool needE = (flags & kNeedE) != 0;
   const bool fo_tab = (flags & kFoTables) != 0;
-  stamp_start_rt(p.stamps, tid);
+  stamp(p.stamps, 0, tid);
 
   if constexpr (QR) {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -1332,23 +1338,29 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
     };
     // tile 0 before the MLP starts (three barriers)
     gather(t0, bufs[0]);
+    stamp_by(p.stamps, 1, tid, 64 * kNG);
     __syncthreads();  // P1
     fwfm(bufs[0]);
+    stamp_by(p.stamps, 2, tid, 64 * kNG);
     __syncthreads();  // P2
     sums(fsb);
+    stamp_by(p.stamps, 3, tid, 64 * kNG);
     __syncthreads();  // P3
     // during tile i: tile i + 1, in the long intervals of the MLP waves' 9 barriers
     for (int i = 0; i + 1 < mine; ++i) {
       const int tn = t0 + (i + 1) * G;
       float* bn = bufs[(i + 1) & 1];
       gather(tn, bn);
+      if (i == 1) stamp_by(p.stamps, 11, tid, 64 * kNG);
       __syncthreads();  // 1: after layer 1's K loop
       __syncthreads();  // 2: after layer 1's epilogue
       fwfm(bn);
+      if (i == 1) stamp_by(p.stamps, 12, tid, 64 * kNG);
       __syncthreads();  // 3: the split tile's barrier inside layer 2's K loop
       __syncthreads();  // 4: after layer 2's K loop
       __syncthreads();  // 5: after layer 2's epilogue
       sums(fsb + ((i + 1) & 1) * kRows);
+      if (i == 1) stamp_by(p.stamps, 13, tid, 64 * kNG);
       __syncthreads();  // 6: inside layer 3's K loop
       __syncthreads();  // 7
       __syncthreads();  // 8
@@ -1385,7 +1397,9 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
   __syncthreads();  // P1
   __syncthreads();  // P2
   __syncthreads();  // P3
+  stamp(p.stamps, 9, tid);
   for (int i = 0; i < mine; ++i) {
+    if (i == 1) stamp(p.stamps, 4, tid);
     const TileRef tr = ptile(p, t0 + i * G);
     const int64_t b0 = tr.b0;
     float* buf = bufs[i & 1];
@@ -1410,6 +1424,7 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
       f32x4 tp[kRT];
       k_loop_rt<kTPW, kRT, kNG, kNS>(acc, buf, SX, ls, wb0, wb1, wb2, lane, ts, tp, h > 0);
       if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(1);
+      if (i == 1) stamp(p.stamps, 5 + h, tid);  // layer h's K loop done (before its barrier)
       __syncthreads();  // every wave has read the layer's input: the tile may be overwritten
 #pragma unroll
       for (int rt = 0; rt < kRT; ++rt) reinterpret_cast<f32x4*>(tailr)[(g * kRT + rt) * 64 + lane] = tp[rt];
@@ -1487,8 +1502,8 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
       deepv += ((taild[tid] + taild[kRows + tid]) + taild[2 * kRows + tid]) + taild[3 * kRows + tid];
       tr.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
     }
+    if (i == 1) stamp(p.stamps, 8, tid);
   }
-  stamp_end_rt(p.stamps, tid);
 }
 
 size_t fwdp_lds_bytes(int F, int D, int MT, int S, int SX) {

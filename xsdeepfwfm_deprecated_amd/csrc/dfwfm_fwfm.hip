@@ -6,14 +6,16 @@
 // bound a CU to three to five 16-sample workgroups.  Here a wave owns 12 samples, five lanes per sample, lane j holding
 // columns (2j, 2j+1) of every field's embedding row in registers (78 VGPRs at Criteo-39):
 //   second[b] = sum_d sum_{k<l} U[k][l] e[k][d] e[l][d],  U = strictly upper (R + R^T) / 2 (FM: ones),
-// as t_k = sum_{l>k} U[k][l] x_l, acc += x_k . t_k per lane -- exactly the 741 x 10 useful FMAs, U wave-uniform (scalar
-// loads of a row-major pack).  No LDS, no barrier: every wave runs alone, so a CU holds as many waves as registers
-// allow and one wave's dependent gather (index -> row) overlaps the others' FMAs.  Each field's row is one 8-byte load
+// as t_k = sum_{l>k} U[k][l] x_l, acc += x_k . t_k per lane -- the 741 x 10 useful FMAs (plus the few zeros of U's
+// aligned chunks), U wave-uniform: each one-wave workgroup stages it in 6 KB of LDS (scalar loads of it missed the
+// scalar cache on every first touch of a CU: 23 us per lone batch).  Every wave runs alone, so a CU holds as many
+// waves as registers allow and one wave's dependent gather (index -> row) overlaps the others' FMAs.  Each field's row is one 8-byte load
 // per lane (five lanes read the 40-byte row), the index / Xv of a field is loaded once per sample and passed to the
 // sample's other lanes by a cross-lane read, and the table first order of field f is read by lane f % 5.
 // The five lanes' partial sums are added by cross-lane reads; out[b] = (first + second) + bias as the reference.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dfwfm_device.h"
 #include "dfwfm_internal.h"
@@ -33,8 +35,9 @@ struct LaneShape {
 
 }  // namespace
 
-template <int F, int NUM, int D>
-__global__ void __launch_bounds__(64) fwfm_lane_kernel(FwdArgs p) {
+// WPE4: capped at 128 registers (four waves per SIMD, a few spilled) instead of ~166 (three); A/B DFWFM_LANE_WPE=4
+template <int F, int NUM, int D, bool WPE4>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE4 ? 4 : 1))) fwfm_lane_kernel(FwdArgs p) {
   using S = LaneShape<F, NUM, D>;
   constexpr int LPS = S::LPS, SPW = S::SPW;
   static_assert(D % 2 == 0 && SPW * LPS <= 64, "lane layout");
@@ -52,6 +55,13 @@ __global__ void __launch_bounds__(64) fwfm_lane_kernel(FwdArgs p) {
   typedef const __attribute__((address_space(4))) FieldDev* cfd_t;
   typedef const __attribute__((address_space(4))) float* cf_t;
   const cfd_t fd = (cfd_t)p.fields;
+
+  constexpr int FP = (F + 3) & ~3;
+  __shared__ float4 us[F * FP / 4];
+  if (flags & kHasSecond) {  // U [F][FP] -> LDS, behind which the index loads go out
+    const float4* ug = reinterpret_cast<const float4*>(p.utri);
+    for (int i = lane; i < F * FP / 4; i += 64) us[i] = ug[i];
+  }
 
   // ---- indices and Xv: lane j loads the entries of columns j, j + LPS, ... of its sample -----------------------
   int32_t idx[S::PI];
@@ -122,19 +132,29 @@ __global__ void __launch_bounds__(64) fwfm_lane_kernel(FwdArgs p) {
   }
   first += fcomp;
 
-  // ---- second order: sum_k x_k . (sum_{l>k} U[k][l] x_l), U wave-uniform ------------------------------------------
+  __syncthreads();  // the wave's U stores are visible (the workgroup is this one wave)
+  // ---- second order: sum_k x_k . (sum_{l>k} U[k][l] x_l) ----------------------------------------------------------
+  // U (rows padded to FP floats, zero on and below the diagonal) is staged in this wave's LDS at the kernel's start
+  // and read as wave-uniform 16-byte broadcasts from the first aligned chunk of each row's l > k part (the one to
+  // three entries l <= k read with it are zeros: fmaf(0, x, t) == t)
   float second = 0.f;
   if (flags & kHasSecond) {
-    const cf_t U = (cf_t)p.utri;
     float ax = 0.f, ay = 0.f;
 #pragma unroll
     for (int k = 0; k < F - 1; ++k) {
       float tx = 0.f, ty = 0.f;
 #pragma unroll
-      for (int l = k + 1; l < F; ++l) {
-        const float u = U[k * F + l];
-        tx = fmaf(u, x[l].x, tx);
-        ty = fmaf(u, x[l].y, ty);
+      for (int c = (k + 1) / 4; c < FP / 4; ++c) {
+        const float4 u4 = us[k * (FP / 4) + c];
+        const float uu[4] = {u4.x, u4.y, u4.z, u4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int l = 4 * c + e;
+          if (l < F) {
+            tx = fmaf(uu[e], x[l].x, tx);
+            ty = fmaf(uu[e], x[l].y, ty);
+          }
+        }
       }
       ax = fmaf(x[k].x, tx, ax);
       ay = fmaf(x[k].y, ty, ay);
@@ -159,7 +179,9 @@ int fwfm_lane_rows(int D) { return 64 / (D / 2); }
 
 hipError_t launch_fwfm_lane(const FwdArgs& a, hipStream_t s) {
   if (!fwfm_lane_supported(a.F, a.num, 10)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((fwfm_lane_kernel<39, 13, 10>), dim3(fwd_grid(a, fwfm_lane_rows(10))), dim3(64), 0, s, a);
+  const char* w = getenv("DFWFM_LANE_WPE");
+  auto k = (w && atoi(w) == 4) ? fwfm_lane_kernel<39, 13, 10, true> : fwfm_lane_kernel<39, 13, 10, false>;
+  hipLaunchKernelGGL(k, dim3(fwd_grid(a, fwfm_lane_rows(10))), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -60,7 +60,7 @@ struct FwdArgs {
   float* out;
   int32_t* err;
   const float* upack;  // FwFM A-operand fragments [MT][S][64]: strictly-upper (R + R^T)/2
-  const float* utri;   // the same U row-major [F][F] (zero on and below the diagonal): the MLP-free lane kernel
+  const float* utri;   // the same U row-major [F][r4(F)] (zero on and below the diagonal): the MLP-free lane kernel
   const int2* pairs;   // kPairs: the nonzero strictly-upper entries of (R + R^T)/2, (k | l << 16, w bits), k-major
   int32_t npairs;
   const float* fwlw;   // [F*D]

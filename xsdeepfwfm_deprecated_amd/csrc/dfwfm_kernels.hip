@@ -823,7 +823,7 @@ fwd_kernel(FwdArgs p) {
 //                  the diagonal is removed by :366-367); FM: 1 above the diagonal.  Fragment order
 //                  out[(m*S + s)*64 + lane] = U[16m + (lane&15)][4s + (lane>>4)]
 //   kPackFwfmSym   the backward's symmetric off-diagonal (R + R^T)/2 (FM: ones), same order
-//   kPackFwfmTri   U row-major [F][F], zero on and below the diagonal (the MLP-free lane kernel's scalar reads)
+//   kPackFwfmTri   U row-major [F][r4(F)], zero on and below the diagonal and in the padding (the lane kernel)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void pack_elem(const PackJob& j, int64_t i) {
   switch (j.type) {
@@ -849,9 +849,9 @@ __device__ __forceinline__ void pack_elem(const PackJob& j, int64_t i) {
       break;
     }
     case kPackFwfmTri: {
-      const int F = j.a, mode = j.b;
-      const int k = (int)(i / F), l = (int)(i - (int64_t)k * F);
-      j.dst[i] = l > k ? ((mode == 1) ? 1.f : (j.src[l * F + k] + j.src[k * F + l]) * 0.5f) : 0.f;
+      const int F = j.a, mode = j.b, FP = j.d;
+      const int k = (int)(i / FP), l = (int)(i - (int64_t)k * FP);
+      j.dst[i] = (l > k && l < F) ? ((mode == 1) ? 1.f : (j.src[l * F + k] + j.src[k * F + l]) * 0.5f) : 0.f;
       break;
     }
     case kPackFwfm:
