@@ -495,6 +495,12 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
+  // the deep forwards' FwFM on the VALU for the Criteo shape (every deep kernel alike: same bits across forms);
+  // DFWFM_VALU_FWFM=0 keeps the MFMA pieces (A/B)
+  if (m->F == 39 && m->D == 10 && (a.flags & kHasSecond) && (a.flags & kHasDeep)) {
+    const char* v = getenv("DFWFM_VALU_FWFM");
+    if (!v || atoi(v) != 0) a.flags |= kValuFwfm;
+  }
   // the static K loop (fwd_kernel NS = 25) when every layer is 25 chunks deep and 25 tiles wide
   a.ns = (m->NC0 == 25 && m->NT == 25 && !getenv("DFWFM_NO_STATIC_K")) ? 25 : 0;
   memcpy(a.fw_list4, m->fw_list4, sizeof a.fw_list4);

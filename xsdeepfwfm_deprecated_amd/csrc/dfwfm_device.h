@@ -64,6 +64,48 @@ __device__ __forceinline__ void stamp_end_rt(uint64_t* st, int tid) {
   }
 }
 
+// FwFM second order on the vector ALUs for the Criteo shape (kValuFwfm: F = 39 fields, D = 10): lane (sample s, column
+// d), six samples per wave, x_k = E[s][k][d] from the LDS tile (rows at stride SX), t_k = sum_{l>k} U[k][l] x_l with
+// U [F][FP] (zero on and below the diagonal) read as wave-uniform 16-byte LDS broadcasts from the first aligned chunk of
+// row k's l > k part, a = sum_k x_k t_k; the sample's D lanes added in d order -> sec[s].  Waves w, w + nw, ... take
+// the groups of six samples.  Beside another wave's MFMA K loop these VALU instructions take the issue slots the
+// MFMAs leave free (the same work as MFMA Gram pieces waited on the saturated matrix pipe: 24k cycles in fwd16ws).
+template <int F, int D, int ROWS>
+__device__ __forceinline__ void fwfm_valu(const float* __restrict__ E, int SX, const float4* __restrict__ us,
+                                          float* __restrict__ sec, int w, int nw, int lane) {
+  constexpr int SPW = 64 / D;
+  constexpr int FP = (F + 3) & ~3;
+  const int sl = lane / D, d = lane - sl * D;
+  for (int s0 = w * SPW; s0 < ROWS; s0 += nw * SPW) {
+    asm volatile("" ::: "memory");  // U's LDS reads stay in the loop (hoisted they would take ~680 registers)
+    const int s = s0 + sl;
+    const bool act = sl < SPW && s < ROWS;
+    const float* e = E + (act ? s : 0) * SX + d;
+    float x[F];
+#pragma unroll
+    for (int k = 0; k < F; ++k) x[k] = act ? e[k * D] : 0.f;
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < F - 1; ++k) {
+      float t = 0.f;
+#pragma unroll
+      for (int c = (k + 1) / 4; c < FP / 4; ++c) {
+        const float4 u4 = us[k * (FP / 4) + c];
+        const float uu[4] = {u4.x, u4.y, u4.z, u4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * c + q < F) t = fmaf(uu[q], x[4 * c + q], t);
+      }
+      a = fmaf(x[k], t, a);
+    }
+    const int base = (sl < SPW ? sl : 0) * D;
+    float tot = __shfl(a, base);
+#pragma unroll
+    for (int o = 1; o < D; ++o) tot += __shfl(a, base + o);
+    if (act && d == 0) sec[s] = tot;
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict__ src) {
   if constexpr (D % 4 == 0) {

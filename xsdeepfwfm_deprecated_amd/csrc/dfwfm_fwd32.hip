@@ -226,11 +226,12 @@ fwd32_kernel(FwdArgs p) {
     }
   }
   f32x4 uw[kUpkPT];
-  const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
+  const bool valu = (flags & kValuFwfm) != 0;  // fwfm_valu: the row-major U instead of the MFMA fragments
+  const int n_upk = (flags & kHasSecond) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
 #pragma unroll
   for (int k = 0; k < kUpkPT; ++k) {
     const int i = tid + k * kNTH;
-    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(p.upack)[i];
+    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
   }
   float fw[kFwlwPT];
   const int n_fwlw = (flags & kFoFwlw) ? F * D : 0;
@@ -397,7 +398,9 @@ fwd32_kernel(FwdArgs p) {
     }
   }
   stamp(p.stamps, 9, tid);
-  if (flags & kHasSecond) {
+  if ((flags & kHasSecond) && valu) {
+    fwfm_valu<39, 10, kRows>(buf, SX, reinterpret_cast<const float4*>(upk), part2, wave, kNG, lane);
+  } else if (flags & kHasSecond) {
     // both 16-row halves of a piece at once: one U fragment read feeds two independent MFMA chains (each chain's
     // order is fwd_kernel's, so the sums are the same bits), which halves this phase's dependent latency
     const int S = p.S;
@@ -469,7 +472,9 @@ fwd32_kernel(FwdArgs p) {
       const float x = fo[b * Fp + f];
       first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
     }
-    if (flags & kHasSecond) {
+    if ((flags & kHasSecond) && valu) {
+      second = q == 0 ? part2[b] : 0.f;
+    } else if (flags & kHasSecond) {
       const int MTD = p.MT * D;
       for (int d = q; d < D; d += 16) {
         const int n = bl * D + d;
@@ -811,8 +816,10 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
       }
     }
     // the shallow parameters to LDS while the rows are in flight
-    const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
-    for (int i = st; i < n_upk; i += 64 * kWsSW) reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(p.upack)[i];
+    const bool valu = (flags & kValuFwfm) != 0;
+    const int n_upk = (flags & kHasSecond) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
+    for (int i = st; i < n_upk; i += 64 * kWsSW)
+      reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
     if (flags & kFoFwlw)
       for (int i = st; i < F * D; i += 64 * kWsSW) fwlw_s[i] = p.fwlw[i];
     if (flags & kFoLw)
@@ -850,7 +857,9 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
         fo[b * Fp + f] = sacc;
       }
     }
-    if (flags & kHasSecond) {
+    if ((flags & kHasSecond) && valu) {
+      fwfm_valu<39, 10, kWsRows>(buf, SX, reinterpret_cast<const float4*>(upk), part2, sw, kWsSW, lane);
+    } else if (flags & kHasSecond) {
       const int S = p.S;
       const int p_lo = p.fw_off4[sw], p_hi = p.fw_off4[sw + 1];
       for (int pi = p_lo; pi < p_hi; ++pi) {
@@ -907,7 +916,9 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
         const float x = fo[b * Fp + f];
         first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
       }
-      if (flags & kHasSecond) {
+      if ((flags & kHasSecond) && valu) {
+        second = q == 0 ? part2[b] : 0.f;
+      } else if (flags & kHasSecond) {
         for (int d = q; d < D; d += 16) {
           const int n = b * D + d;
           for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
@@ -1136,8 +1147,10 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
     // ================================ gather waves =====================================================================
     const int st = tid - 64 * kNG;
     const int sw = wave - kNG;
-    const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
-    for (int i = st; i < n_upk; i += 64 * kPSW) reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(p.upack)[i];
+    const bool valu = (flags & kValuFwfm) != 0;
+    const int n_upk = (flags & kHasSecond) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
+    for (int i = st; i < n_upk; i += 64 * kPSW)
+      reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
     if (flags & kFoFwlw)
       for (int i = st; i < F * D; i += 64 * kPSW) fwlw_s[i] = p.fwlw[i];
     if (flags & kFoLw)
@@ -1253,7 +1266,9 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
           fo[b * Fp + f] = sacc;
         }
       }
-      if (flags & kHasSecond) {
+      if ((flags & kHasSecond) && valu) {
+        fwfm_valu<39, 10, kRows>(buf, SX, reinterpret_cast<const float4*>(upk), part2, sw, kPSW, lane);
+      } else if (flags & kHasSecond) {
         const int S = p.S;
         const int MTD = p.MT * D;
         const int p_lo = p.fw_off4[sw], p_hi = p.fw_off4[sw + 1];
@@ -1321,7 +1336,9 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
           const float x = fo[b * Fp + f];
           first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
         }
-        if (flags & kHasSecond) {
+        if ((flags & kHasSecond) && valu) {
+          second = q == 0 ? part2[b] : 0.f;
+        } else if (flags & kHasSecond) {
           const int MTD = p.MT * D;
           for (int d = q; d < D; d += 16) {
             const int n = bl * D + d;

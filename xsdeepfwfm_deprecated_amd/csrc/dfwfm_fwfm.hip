@@ -50,11 +50,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE4 ? 
   const int64_t b = tr.b0 + s;
   const bool live = s < SPW && b < p.batch;
   const int flags = p.flags;
-  // wave-uniform tables through the constant address space: scalar loads into SGPRs (the kernel writes only out and
-  // the error word, neither of which aliases them)
-  typedef const __attribute__((address_space(4))) FieldDev* cfd_t;
   typedef const __attribute__((address_space(4))) float* cf_t;
-  const cfd_t fd = (cfd_t)p.fields;
+  // the field descriptors in ONE round trip: lane f < F loads field f's table bases and row count, the loops below
+  // take them with v_readlane (scalar loads of them, one field at a time, put a cold scalar-cache miss in front of
+  // every row load: 23 us for a lone batch)
+  uint32_t d_e2lo = 0, d_e2hi = 0, d_e1lo = 0, d_e1hi = 0, d_nlo = 0, d_nhi = 0;
+  const float d_lw = ((flags & kFoLw) && lane < F) ? p.lw[lane] : 0.f;  // lw[f] the same way
+  if (lane < F) {
+    const FieldDev fdl = p.fields[lane];
+    const uint64_t e2 = reinterpret_cast<uint64_t>(fdl.emb2), e1 = reinterpret_cast<uint64_t>(fdl.emb1);
+    d_e2lo = (uint32_t)e2; d_e2hi = (uint32_t)(e2 >> 32);
+    d_e1lo = (uint32_t)e1; d_e1hi = (uint32_t)(e1 >> 32);
+    d_nlo = (uint32_t)fdl.n; d_nhi = (uint32_t)((uint64_t)fdl.n >> 32);
+  }
+  auto ptr_of = [](uint32_t lo, uint32_t hi, int f) {
+    return reinterpret_cast<const float*>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, f) << 32) |
+                                          (uint32_t)__builtin_amdgcn_readlane((int)lo, f));
+  };
 
   constexpr int FP = (F + 3) & ~3;
   __shared__ float4 us[F * FP / 4];
@@ -64,18 +76,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE4 ? 
   }
 
   // ---- indices and Xv: lane j loads the entries of columns j, j + LPS, ... of its sample -----------------------
-  int32_t idx[S::PI];
+  int64_t kv[S::PI];
   float xvv[S::PV];
 #pragma unroll
   for (int q = 0; q < S::PI; ++q) {
     const int c = j + q * LPS;
-    int64_t v = 0;
-    if (live && c < S::NCAT) {
-      v = tr.xi[b * p.xi_stride + c];
-      if (v < 0 || v >= fd[NUM + c].n) {
-        atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
-        v = 0;
-      }
+    kv[q] = (live && c < S::NCAT) ? tr.xi[b * p.xi_stride + c] : 0;
+  }
+  int32_t idx[S::PI];
+#pragma unroll
+  for (int q = 0; q < S::PI; ++q) {
+    const int c = j + q * LPS;
+    // field NUM + c's row count from the lane that loaded its descriptor (c differs by lane: a cross-lane read)
+    const int src = NUM + (c < S::NCAT ? c : 0);
+    const int64_t n = (int64_t)(((uint64_t)(uint32_t)__shfl((int)d_nhi, src) << 32) | (uint32_t)__shfl((int)d_nlo, src));
+    int64_t v = kv[q];
+    if (live && c < S::NCAT && (v < 0 || v >= n)) {
+      atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
+      v = 0;
     }
     idx[q] = (int32_t)v;
   }
@@ -102,8 +120,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE4 ? 
   };
 #pragma unroll
   for (int f = 0; f < F; ++f) {
-    const float* e2 = fd[f].emb2;
-    const float* e1 = fd[f].emb1;
+    const float* e2 = ptr_of(d_e2lo, d_e2hi, f);
+    const float* e1 = ptr_of(d_e1lo, d_e1hi, f);
     x[f] = f2{0.f, 0.f};
     float fo = 0.f;
     if (f < NUM) {
@@ -118,7 +136,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE4 ? 
       if (live && need_e) x[f] = *reinterpret_cast<const f2*>(e2 + r * D + 2 * j);
       if (live && fo_tab && j == f % LPS) fo = e1[r];
     }
-    if (fo_tab && j == f % LPS) add_first(lw ? fo * ((cf_t)p.lw)[f] : fo);
+    if (fo_tab && j == f % LPS) add_first(lw ? fo * __shfl(d_lw, f) : fo);
   }
 
   // ---- fwlw first order: sum_d fwlw[f][d] e[f][d] over this lane's d (lw-projected when use_lw) -------------------
@@ -127,7 +145,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE4 ? 
     for (int f = 0; f < F; ++f) {
       const f2 w = *reinterpret_cast<const f2*>(p.fwlw + f * D + 2 * j);
       const float v = fmaf(x[f].y, w.y, x[f].x * w.x);
-      add_first(lw ? v * ((cf_t)p.lw)[f] : v);
+      add_first(lw ? v * __shfl(d_lw, f) : v);
     }
   }
   first += fcomp;

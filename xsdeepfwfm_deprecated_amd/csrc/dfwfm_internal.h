@@ -31,6 +31,7 @@ constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_table
 constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
 constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
 constexpr int kNtRows = 8192;  // embedding-row loads with the non-temporal cache policy (A/B: DFWFM_NT_ROWS)
+constexpr int kValuFwfm = 16384; // deep forwards: the FwFM of the Criteo shape (F 39, D 10) on the VALU (fwfm_valu)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kMaxH = 16;      // hidden layers
 constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)

@@ -227,11 +227,13 @@ fwd_kernel(FwdArgs p) {
     }
   }
   f32x4 uw[kUpkPT];
-  const int n_upk = (PART != 3 && (flags & kHasSecond)) ? p.MT * p.S * 16 : 0;  // PART 3 reads them from global
+  // kValuFwfm: the row-major U [F][r4(F)] for fwfm_valu instead of the MFMA fragments (same LDS region)
+  const bool valu = D == 10 && (flags & kValuFwfm) != 0;
+  const int n_upk = (PART != 3 && (flags & kHasSecond)) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
 #pragma unroll
   for (int k = 0; k < kUpkPT; ++k) {
     const int i = tid + k * NTH;
-    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(p.upack)[i];
+    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
   }
   float fw[kFwlwPT];
   const int n_fwlw = (flags & kFoFwlw) ? F * D : 0;
@@ -498,6 +500,8 @@ fwd_kernel(FwdArgs p) {
         if (lane == 0) part2[b] = part;
       }
     }
+  } else if ((flags & kHasSecond) && valu) {
+    if constexpr (D == 10) fwfm_valu<39, 10, kBM>(bufX, SX, reinterpret_cast<const float4*>(upk), part2, wave, NW, lane);
   } else if (flags & kHasSecond) {
     // Y = U * E_b on MFMA: rows k (fields, MT tiles of 16), columns n = b*D + d (D tiles of 16), contraction
     // over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].  The work is cut into
@@ -587,6 +591,8 @@ fwd_kernel(FwdArgs p) {
     if (flags & kHasSecond) {
       if constexpr (PART == 3) {
         second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
+      } else if (valu) {
+        second = q == 0 ? part2[b] : 0.f;  // fwfm_valu's sum
       } else {
         for (int d = q; d < D; d += 16) {  // D = 32: two terms per lane
           const int n = b * D + d;

@@ -472,8 +472,12 @@ class FusedTrainStep:
             # one process: a single graph that forks after the per-tile backward -- the weight-gradient GEMM
             # and the MLP's Adam on a side stream; the reductions, the table scatter and the other tensors' Adam
             # (the 58 MB of tables) beside them
-            # (A/B only, DFWFM_TRAIN_FORK: spread = fork after the scatter, none = one stream)
-            fork = os.environ.get("DFWFM_TRAIN_FORK", "tiles")
+            # (A/B only, DFWFM_TRAIN_FORK: spread = fork after the scatter, none = one stream, tiles = fork right after
+            # the per-tile backward with the reductions' final sums beside the GEMM)
+            # default (reduce): the reductions' final sums (39 small workgroups) run BEFORE the fork -- launched
+            # beside the weight-gradient GEMM they waited for its 225 workgroups to leave the CUs and took 38 us
+            # instead of ~6, holding the scatter and the main Adam behind them (profiles/r04/r04c_proftrain)
+            fork = os.environ.get("DFWFM_TRAIN_FORK", "reduce")
             if fork == "none":
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g1, stream=s):
@@ -482,16 +486,19 @@ class FusedTrainStep:
                 torch.cuda.current_stream(self.dev).wait_stream(s)
                 return g1, None, None, None, None
             late = fork == "spread"
+            first = fork == "reduce"
             s1 = torch.cuda.Stream(self.dev)
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g1, stream=s):
                     self._part1(self.B, denom, phases=_lib.BWD_TABLES if late else _lib.BWD_TILES)
+                    if first:
+                        self._backward_phase(_lib.BWD_REDUCE)
                     s1.wait_stream(s)
                     with torch.cuda.stream(s1):
                         self._part1b()
                         self._adam_mlp()
                     if not late:
-                        self._backward_phase(_lib.BWD_SPREAD)
+                        self._backward_phase(_lib.BWD_SCATTER if first else _lib.BWD_SPREAD)
                     self._adam_main()
                     s.wait_stream(s1)
             torch.cuda.current_stream(self.dev).wait_stream(s)
