@@ -6,9 +6,9 @@
 // bound a CU to three to five 16-sample workgroups.  Here a wave owns 12 samples, five lanes per sample, lane j holding
 // columns (2j, 2j+1) of every field's embedding row in registers (78 VGPRs at Criteo-39):
 //   second[b] = sum_d sum_{k<l} U[k][l] e[k][d] e[l][d],  U = strictly upper (R + R^T) / 2 (FM: ones),
-// as t_k = sum_{l>k} U[k][l] x_l, acc += x_k . t_k per lane -- the 741 x 10 useful FMAs (plus the few zeros of U's
-// aligned chunks), U wave-uniform: each one-wave workgroup stages it in 6 KB of LDS (scalar loads of it missed the
-// scalar cache on every first touch of a CU: 23 us per lone batch).  Every wave runs alone, so a CU holds as many
+// as t_k = sum_{l>k} U[k][l] x_l, acc += x_k . t_k per lane -- exactly the 741 x 10 useful FMAs, U wave-uniform:
+// staged through 6 KB of LDS into 25 registers spread over the wave and taken entry by entry with v_readlane (scalar
+// loads of it missed the scalar cache on every first touch of a CU; LDS reads in the loop waited every few FMAs).  Every wave runs alone, so a CU holds as many
 // waves as registers allow and one wave's dependent gather (index -> row) overlaps the others' FMAs.  Each field's row is one 8-byte load
 // per lane (five lanes read the 40-byte row), the index / Xv of a field is loaded once per sample and passed to the
 // sample's other lanes by a cross-lane read, and the table first order of field f is read by lane f % 5.
@@ -151,28 +151,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE4 ? 
   first += fcomp;
 
   __syncthreads();  // the wave's U stores are visible (the workgroup is this one wave)
-  // ---- second order: sum_k x_k . (sum_{l>k} U[k][l] x_l) ----------------------------------------------------------
-  // U (rows padded to FP floats, zero on and below the diagonal) is staged in this wave's LDS at the kernel's start
-  // and read as wave-uniform 16-byte broadcasts from the first aligned chunk of each row's l > k part (the one to
-  // three entries l <= k read with it are zeros: fmaf(0, x, t) == t)
+  // ---- second order: sum_k x_k . (sum_{l>k} U[k][l] x_l), U in the wave's registers (UReg: readlane -> SGPR) -------
   float second = 0.f;
   if (flags & kHasSecond) {
+    UReg<F> U;
+    U.load(reinterpret_cast<const float*>(us), lane);
     float ax = 0.f, ay = 0.f;
 #pragma unroll
     for (int k = 0; k < F - 1; ++k) {
       float tx = 0.f, ty = 0.f;
 #pragma unroll
-      for (int c = (k + 1) / 4; c < FP / 4; ++c) {
-        const float4 u4 = us[k * (FP / 4) + c];
-        const float uu[4] = {u4.x, u4.y, u4.z, u4.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int l = 4 * c + e;
-          if (l < F) {
-            tx = fmaf(uu[e], x[l].x, tx);
-            ty = fmaf(uu[e], x[l].y, ty);
-          }
-        }
+      for (int l = k + 1; l < F; ++l) {
+        const float u = U.at(k, l);
+        tx = fmaf(u, x[l].x, tx);
+        ty = fmaf(u, x[l].y, ty);
       }
       ax = fmaf(x[k].x, tx, ax);
       ay = fmaf(x[k].y, ty, ay);
