@@ -189,9 +189,6 @@ def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
         if cu_mask in (None, "none") and os.environ.get("DFWFM_PERSIST", "1") != "0":
             return f"dfwfm::fwdp_kernel<10,{qr}>"  # persistent, gather waves a tile ahead
         return f"dfwfm::fwd32_kernel<10,{qr}>"
-    if config == "fwfm" and os.environ.get("DFWFM_FWFM_LANE", "1") != "0":
-        wpe4 = "true" if os.environ.get("DFWFM_LANE_WPE") == "4" else "false"
-        return f"dfwfm::fwfm_lane_kernel<39,13,10,{wpe4}>"  # MLP-free, a lane per (sample, column pair)
     if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
             return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"

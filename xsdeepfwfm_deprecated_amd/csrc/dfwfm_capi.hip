@@ -50,7 +50,6 @@ struct dfwfm_model {
   // device state (owned)
   FieldDev* d_fields;
   float* d_upack;  // FwFM A-operand fragments [MT][S][64]
-  float* d_utri;   // the same U row-major [F][r4(F)] (MLP-free lane kernel)
   int2* d_pairs;   // build_fwfm_pairs: nonzero pairs of a pruned R (F (F - 1) / 2 capacity)
   int32_t npairs;
   int32_t* d_err;
@@ -132,7 +131,7 @@ int dev_alloc(T** p, size_t count) {
 
 void free_model(dfwfm_model* m) {
   if (!m) return;
-  void* ptrs[] = {m->d_fields, m->d_upack, m->d_utri, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
+  void* ptrs[] = {m->d_fields, m->d_upack, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
                   m->d_lw,     m->d_bias,  m->d_stamps,  m->d_wtpack, m->d_rsk,   m->d_ws,
                   m->d_ell,    m->d_cnt,   m->d_spstat, m->d_pairs};
   for (void* p : ptrs)
@@ -311,7 +310,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     free_model(m);
     return rc;
   }
-  if ((rc = dev_alloc(&m->d_rsk, (size_t)m->MT * m->S * 64)) || (rc = dev_alloc(&m->d_utri, (size_t)F * r4(F)))) {
+  if ((rc = dev_alloc(&m->d_rsk, (size_t)m->MT * m->S * 64))) {
     free_model(m);
     return rc;
   }
@@ -333,7 +332,6 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   }
   e = hipMemset(m->d_err, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(m->d_upack, 0, sizeof(float) * (size_t)m->MT * m->S * 64);
-  if (e == hipSuccess) e = hipMemset(m->d_utri, 0, sizeof(float) * (size_t)F * r4(F));
   if (e != hipSuccess) {
     free_model(m);
     return hip_fail(e, "hipMemset");
@@ -412,7 +410,6 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
     const int64_t tot = (int64_t)m->MT * m->S * 64;
     job(kPackFwfm, field_cov, m->d_upack, tot, m->F, c.use_fm ? 1 : 0, m->S);
     job(kPackFwfmSym, field_cov, m->d_rsk, tot, m->F, c.use_fm ? 1 : 0, m->S);
-    job(kPackFwfmTri, field_cov, m->d_utri, (int64_t)m->F * r4(m->F), m->F, c.use_fm ? 1 : 0, r4(m->F));
   }
   if (m->flags & kFoFwlw) job(kPackPad, fwfm_lin, m->d_fwlw, m->F * m->D, m->F * m->D, 0, 0);
   if (m->flags & kFoLw) job(kPackPad, fm_1st, m->d_lw, m->F, m->F, 0, 0);
@@ -472,7 +469,6 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.out = out;
   a.err = m->d_err;
   a.upack = m->d_upack;
-  a.utri = m->d_utri;
   a.pairs = m->d_pairs;
   a.npairs = m->npairs;
   a.fwlw = m->d_fwlw;
@@ -495,12 +491,7 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
-  // the deep forwards' FwFM on the VALU for the Criteo shape (every deep kernel alike: same bits across forms);
-  // DFWFM_VALU_FWFM=0 keeps the MFMA pieces (A/B)
-  if (m->F == 39 && m->D == 10 && (a.flags & kHasSecond) && (a.flags & kHasDeep)) {
-    const char* v = getenv("DFWFM_VALU_FWFM");
-    if (!v || atoi(v) != 0) a.flags |= kValuFwfm;
-  }
+
   // the static K loop (fwd_kernel NS = 25) when every layer is 25 chunks deep and 25 tiles wide
   a.ns = (m->NC0 == 25 && m->NT == 25 && !getenv("DFWFM_NO_STATIC_K")) ? 25 : 0;
   memcpy(a.fw_list4, m->fw_list4, sizeof a.fw_list4);
@@ -600,15 +591,6 @@ int stream_cu_count(dfwfm_model* m, void* stream) {
   return m->cu_count[slot];
 }
 
-// the MLP-free forward on the lane-per-(sample, column pair) kernel (dfwfm_fwfm.hip): no deep tower, no QR field, no
-// pruned-pair list, a supported shape; DFWFM_FWFM_LANE=0 keeps fwd_kernel's MLP-free form (A/B)
-bool use_fwfm_lane(const dfwfm_model* m, int flags) {
-  if (flags & (kHasDeep | kTrain | kHasQR | kPairs)) return false;
-  if (!fwfm_lane_supported(m->F, m->num, m->D)) return false;
-  const char* v = getenv("DFWFM_FWFM_LANE");
-  return !v || atoi(v) != 0;
-}
-
 // fwd32 (32-sample workgroups) when its workgroups give every CU of the stream two of them (two per CU hide each
 // other's gather and shallow phases); on a CU-masked stream (the caller runs several batches side by side, one
 // stream per part of the chip) one per CU is enough.  Otherwise the 16-sample kernel: twice the workgroups for the
@@ -660,10 +642,9 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
-  const int form = use_fwfm_lane(m, a.flags) ? -1 : deep_form(m, batch, stream);
+  const int form = (a.flags & kHasDeep) ? deep_form(m, batch, stream) : 0;
   if (form == 3) a.tiles = (int32_t)((batch + 31) / 32);
-  hipError_t e = form == -1 ? launch_fwfm_lane(a, (hipStream_t)stream)
-                 : form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
+  hipError_t e = form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
                  : form == 2 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                  : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
                              : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
@@ -691,17 +672,11 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     return DFWFM_OK;
   }
   if ((int64_t)nb * ((batch + kBM - 1) / kBM) > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "batch set too large");
-  bool lane = false;
-  {
-    FwdArgs probe;
-    fill_forward_args(m, probe, xi[0], xi_stride, xv[0], xv_stride, batch, out[0]);
-    lane = use_fwfm_lane(m, probe.flags);
-  }
   // the kernel for the first launch's rows (a set of up to kMaxSet batches); later launches of a larger set use it too
   const int64_t set_rows = (int64_t)(nb < kMaxSet ? nb : kMaxSet) * batch;
-  const int form = lane ? -1 : deep_form(m, set_rows, stream);
+  const int form = m->cfg.use_deep ? deep_form(m, set_rows, stream) : 0;
   const bool r32 = form >= 2;
-  const int rows = lane ? fwfm_lane_rows(m->D) : (r32 ? 32 : kBM);
+  const int rows = r32 ? 32 : kBM;
   for (int32_t i0 = 0; i0 < nb; i0 += kMaxSet) {
     const int32_t n = nb - i0 < kMaxSet ? nb - i0 : kMaxSet;
     FwdArgs a;
@@ -725,8 +700,7 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     int rc = diag_stamps_buffer(m, (int64_t)n * a.tiles * rows, 1, &a.stamps);
     if (rc != DFWFM_OK) return rc;
     if (form == 3) a.tiles = (int32_t)((batch + 31) / 32);
-    const hipError_t e = lane  ? launch_fwfm_lane(a, (hipStream_t)stream)
-                         : form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
+    const hipError_t e = form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
                          : r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
                          : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
                                      : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,

@@ -64,60 +64,6 @@ __device__ __forceinline__ void stamp_end_rt(uint64_t* st, int tid) {
   }
 }
 
-// U spread over a wave's registers: lane i holds U_flat[i + 64 j] of the padded [F][FP] U (UJ registers); an entry is
-// then a v_readlane into an SGPR, the FMA's scalar operand -- no memory access in the loop (LDS reads of U, a few in
-// flight at a time, waited ~100 cycles every few FMAs: 40k+ cycles for one wave's 741 FMAs)
-template <int F>
-struct UReg {
-  static constexpr int FP = (F + 3) & ~3;
-  static constexpr int UJ = (F * FP + 63) / 64;
-  float r[UJ];
-  __device__ __forceinline__ void load(const float* __restrict__ us_flat, int lane) {
-#pragma unroll
-    for (int j = 0; j < UJ; ++j) r[j] = (j * 64 + lane < F * FP) ? us_flat[j * 64 + lane] : 0.f;
-  }
-  __device__ __forceinline__ float at(int k, int l) const {  // k, l compile-time after unrolling
-    const int e = k * FP + l;
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[e / 64]), e % 64));
-  }
-};
-
-// FwFM second order on the vector ALUs for the Criteo shape (kValuFwfm: F = 39 fields, D = 10): lane (sample s, column
-// d), six samples per wave, x_k = E[s][k][d] from the LDS tile (rows at stride SX), t_k = sum_{l>k} U[k][l] x_l, a =
-// sum_k x_k t_k; the sample's D lanes added in d order -> sec[s].  Waves w, w + nw, ... take the groups of six samples.
-// U comes from the padded [F][FP] copy in LDS (us) into the wave's registers (UReg).  Beside another wave's MFMA K
-// loop these VALU instructions take the issue slots the MFMAs leave free.
-template <int F, int D, int ROWS>
-__device__ __forceinline__ void fwfm_valu(const float* __restrict__ E, int SX, const float4* __restrict__ us,
-                                          float* __restrict__ sec, int w, int nw, int lane) {
-  constexpr int SPW = 64 / D;
-  const int sl = lane / D, d = lane - sl * D;
-  if (w * SPW >= ROWS) return;
-  UReg<F> U;
-  U.load(reinterpret_cast<const float*>(us), lane);
-  for (int s0 = w * SPW; s0 < ROWS; s0 += nw * SPW) {
-    const int s = s0 + sl;
-    const bool act = sl < SPW && s < ROWS;
-    const float* e = E + (act ? s : 0) * SX + d;
-    float x[F];
-#pragma unroll
-    for (int k = 0; k < F; ++k) x[k] = act ? e[k * D] : 0.f;
-    float a = 0.f;
-#pragma unroll
-    for (int k = 0; k < F - 1; ++k) {
-      float t = 0.f;
-#pragma unroll
-      for (int l = k + 1; l < F; ++l) t = fmaf(U.at(k, l), x[l], t);
-      a = fmaf(x[k], t, a);
-    }
-    const int base = (sl < SPW ? sl : 0) * D;
-    float tot = __shfl(a, base);
-#pragma unroll
-    for (int o = 1; o < D; ++o) tot += __shfl(a, base + o);
-    if (act && d == 0) sec[s] = tot;
-  }
-}
-
 template <int D>
 __device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict__ src) {
   if constexpr (D % 4 == 0) {

@@ -136,6 +136,71 @@ __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __
   for (int rt = 0; rt < RT; ++rt) tp[rt] = c0[rt] + c1[rt];
 }
 
+// FwFM pieces (fwd_kernel's (row tile m, column tile nt) work units, fw_list order) NP at a time with their MFMA
+// chains interleaved -- and both 16-row halves of each (RT = 2) -- for waves that run them beside another wave group's
+// MFMA K loop: one piece's 10-deep dependent chain at a time left them latency-bound.  Every chain is one piece's
+// steps in order from 4m, so the sums are fwd_kernel's bits.
+template <int NP, int RT, int D>
+__device__ __forceinline__ void fwfm_pieces(const uint8_t* __restrict__ list, int lo, int hi, const float* buf, int SX,
+                                            const float* upk, int S, int F, int MTD, float* part2, int lane) {
+  for (int pi = lo; pi < hi; pi += NP) {
+    int pc[NP], m[NP];
+    bool on[NP];
+    const float* ecol[NP];
+    const float* ua[NP];
+    int smin = S;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      on[q] = pi + q < hi;
+      pc[q] = list[on[q] ? pi + q : pi];
+      m[q] = pc[q] / D;
+      const int nt = pc[q] - m[q] * D;
+      const int n = nt * 16 + (lane & 15);
+      const int b = n / D;
+      ecol[q] = buf + b * SX + (n - b * D);
+      ua[q] = upk + m[q] * S * 64 + lane;
+      if (on[q]) smin = 4 * m[q] < smin ? 4 * m[q] : smin;
+    }
+    f32x4 acc[NP][RT];
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[q][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = smin; s < S; ++s) {
+      float av[NP], bv[NP][RT];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        av[q] = ua[q][s * 64];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) bv[q][rt] = ecol[q][rt * 16 * SX + (4 * s + (lane >> 4)) * D];
+      }
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        if (on[q] && s >= 4 * m[q])
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q][rt], acc[q][rt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      if (!on[q]) continue;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const float* ec = ecol[q] + rt * 16 * SX;
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * m[q] + 4 * (lane >> 4) + r;
+          const int kk = (k < F ? k : 0) * D;
+          v = fmaf(k < F ? ec[kk] : 0.f, acc[q][rt][r], v);
+        }
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 16) part2[(rt * MTD + pc[q]) * 16 + lane] = v;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // QR: some field may be a QR embedding (false: no second operand, row descriptors loaded directly with the keys)
@@ -226,12 +291,11 @@ fwd32_kernel(FwdArgs p) {
     }
   }
   f32x4 uw[kUpkPT];
-  const bool valu = (flags & kValuFwfm) != 0;  // fwfm_valu: the row-major U instead of the MFMA fragments
-  const int n_upk = (flags & kHasSecond) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
+  const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
 #pragma unroll
   for (int k = 0; k < kUpkPT; ++k) {
     const int i = tid + k * kNTH;
-    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
+    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(p.upack)[i];
   }
   float fw[kFwlwPT];
   const int n_fwlw = (flags & kFoFwlw) ? F * D : 0;
@@ -398,9 +462,7 @@ fwd32_kernel(FwdArgs p) {
     }
   }
   stamp(p.stamps, 9, tid);
-  if ((flags & kHasSecond) && valu) {
-    fwfm_valu<39, 10, kRows>(buf, SX, reinterpret_cast<const float4*>(upk), part2, wave, kNG, lane);
-  } else if (flags & kHasSecond) {
+  if (flags & kHasSecond) {
     // both 16-row halves of a piece at once: one U fragment read feeds two independent MFMA chains (each chain's
     // order is fwd_kernel's, so the sums are the same bits), which halves this phase's dependent latency
     const int S = p.S;
@@ -472,9 +534,7 @@ fwd32_kernel(FwdArgs p) {
       const float x = fo[b * Fp + f];
       first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
     }
-    if ((flags & kHasSecond) && valu) {
-      second = q == 0 ? part2[b] : 0.f;
-    } else if (flags & kHasSecond) {
+    if (flags & kHasSecond) {
       const int MTD = p.MT * D;
       for (int d = q; d < D; d += 16) {
         const int n = bl * D + d;
@@ -816,10 +876,8 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
       }
     }
     // the shallow parameters to LDS while the rows are in flight
-    const bool valu = (flags & kValuFwfm) != 0;
-    const int n_upk = (flags & kHasSecond) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
-    for (int i = st; i < n_upk; i += 64 * kWsSW)
-      reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
+    const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
+    for (int i = st; i < n_upk; i += 64 * kWsSW) reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(p.upack)[i];
     if (flags & kFoFwlw)
       for (int i = st; i < F * D; i += 64 * kWsSW) fwlw_s[i] = p.fwlw[i];
     if (flags & kFoLw)
@@ -857,49 +915,9 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
         fo[b * Fp + f] = sacc;
       }
     }
-    if ((flags & kHasSecond) && valu) {
-      fwfm_valu<39, 10, kWsRows>(buf, SX, reinterpret_cast<const float4*>(upk), part2, sw, kWsSW, lane);
-    } else if (flags & kHasSecond) {
+    if (flags & kHasSecond) {
       const int S = p.S;
-      const int p_lo = p.fw_off4[sw], p_hi = p.fw_off4[sw + 1];
-      for (int pi = p_lo; pi < p_hi; ++pi) {
-        const int pc = p.fw_list4[pi];
-        const int m = pc / D;
-        const int nt = pc - m * D;
-        const int n = nt * 16 + (lane & 15);
-        const int b = n / D;
-        const float* ecol = buf + b * SX + (n - b * D);
-        const float* ua = upk + m * S * 64 + lane;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        auto group = [&](int s0, auto U_) {
-          constexpr int U = decltype(U_)::value;
-          float av[U], bv[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            av[u] = ua[(s0 + u) * 64];
-            bv[u] = ecol[(4 * (s0 + u) + (lane >> 4)) * D];
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
-        };
-        int s0 = 4 * m;
-        for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
-        const int rem = S - s0;
-        if (rem == 3) group(s0, std::integral_constant<int, 3>{});
-        else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
-        else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
-        float v = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * m + 4 * (lane >> 4) + r;
-          const int kk = (k < F ? k : 0) * D;
-          v = fmaf(k < F ? ecol[kk] : 0.f, acc[r], v);
-        }
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if (lane < 16) part2[pc * 16 + lane] = v;
-      }
+      fwfm_pieces<3, 1, D>(p.fw_list4, p.fw_off4[sw], p.fw_off4[sw + 1], buf, SX, upk, S, F, p.MT * D, part2, lane);
     }
     // the pieces reach the per-sample sums of every shallow wave through LDS; the MLP waves are inside layer 1's K
     // loop, so instead of a workgroup barrier the four shallow waves count in on an LDS word (all four arrive:
@@ -916,9 +934,7 @@ __global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
         const float x = fo[b * Fp + f];
         first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
       }
-      if ((flags & kHasSecond) && valu) {
-        second = q == 0 ? part2[b] : 0.f;
-      } else if (flags & kHasSecond) {
+      if (flags & kHasSecond) {
         for (int d = q; d < D; d += 16) {
           const int n = b * D + d;
           for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
@@ -1147,10 +1163,8 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
     // ================================ gather waves =====================================================================
     const int st = tid - 64 * kNG;
     const int sw = wave - kNG;
-    const bool valu = (flags & kValuFwfm) != 0;
-    const int n_upk = (flags & kHasSecond) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
-    for (int i = st; i < n_upk; i += 64 * kPSW)
-      reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
+    const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
+    for (int i = st; i < n_upk; i += 64 * kPSW) reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(p.upack)[i];
     if (flags & kFoFwlw)
       for (int i = st; i < F * D; i += 64 * kPSW) fwlw_s[i] = p.fwlw[i];
     if (flags & kFoLw)
@@ -1250,7 +1264,6 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
           }
         }
       }
-      if (flags & kPrio) __builtin_amdgcn_s_setprio(0);
     };
     // fwlw first order and the FwFM pieces of the tile in `buf` (every gather wave's rows are written)
     auto fwfm = [&](const float* buf) {
@@ -1266,62 +1279,10 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
           fo[b * Fp + f] = sacc;
         }
       }
-      if ((flags & kHasSecond) && valu) {
-        fwfm_valu<39, 10, kRows>(buf, SX, reinterpret_cast<const float4*>(upk), part2, sw, kPSW, lane);
-      } else if (flags & kHasSecond) {
+      if (flags & kHasSecond) {
         const int S = p.S;
         const int MTD = p.MT * D;
-        const int p_lo = p.fw_off4[sw], p_hi = p.fw_off4[sw + 1];
-        for (int pi = p_lo; pi < p_hi; ++pi) {
-          const int pc = p.fw_list4[pi];
-          const int m = pc / D;
-          const int nt = pc - m * D;
-          const int n = nt * 16 + (lane & 15);
-          const int b = n / D;
-          const float* ecol0 = buf + b * SX + (n - b * D);
-          const float* ecol1 = ecol0 + 16 * SX;
-          const float* ua = upk + m * S * 64 + lane;
-          f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-          auto group = [&](int s0, auto U_) {
-            constexpr int U = decltype(U_)::value;
-            float av[U], bv0[U], bv1[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const int l = (4 * (s0 + u) + (lane >> 4)) * D;
-              av[u] = ua[(s0 + u) * 64];
-              bv0[u] = ecol0[l];
-              bv1[u] = ecol1[l];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv0[u], acc0, 0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv1[u], acc1, 0, 0, 0);
-            }
-          };
-          int s0 = 4 * m;
-          for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
-          const int rem = S - s0;
-          if (rem == 3) group(s0, std::integral_constant<int, 3>{});
-          else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
-          else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
-          float v0 = 0.f, v1 = 0.f;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int k = 16 * m + 4 * (lane >> 4) + r;
-            const int kk = (k < F ? k : 0) * D;
-            v0 = fmaf(k < F ? ecol0[kk] : 0.f, acc0[r], v0);
-            v1 = fmaf(k < F ? ecol1[kk] : 0.f, acc1[r], v1);
-          }
-          v0 += __shfl_xor(v0, 16);
-          v1 += __shfl_xor(v1, 16);
-          v0 += __shfl_xor(v0, 32);
-          v1 += __shfl_xor(v1, 32);
-          if (lane < 16) {
-            part2[pc * 16 + lane] = v0;
-            part2[(MTD + pc) * 16 + lane] = v1;
-          }
-        }
+        fwfm_pieces<2, kRT, D>(p.fw_list4, p.fw_off4[sw], p.fw_off4[sw + 1], buf, SX, upk, S, F, MTD, part2, lane);
       }
     };
     // first[b] + second[b] of the 32 rows -> fs (fwd32's 16-lane sums; each gather wave two groups of four rows)
@@ -1336,9 +1297,7 @@ __global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
           const float x = fo[b * Fp + f];
           first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
         }
-        if ((flags & kHasSecond) && valu) {
-          second = q == 0 ? part2[b] : 0.f;
-        } else if (flags & kHasSecond) {
+        if (flags & kHasSecond) {
           const int MTD = p.MT * D;
           for (int d = q; d < D; d += 16) {
             const int n = bl * D + d;

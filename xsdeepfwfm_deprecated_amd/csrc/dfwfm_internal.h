@@ -31,7 +31,6 @@ constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_table
 constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
 constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
 constexpr int kNtRows = 8192;  // embedding-row loads with the non-temporal cache policy (A/B: DFWFM_NT_ROWS)
-constexpr int kValuFwfm = 16384; // deep forwards: the FwFM of the Criteo shape (F 39, D 10) on the VALU (fwfm_valu)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kMaxH = 16;      // hidden layers
 constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)
@@ -61,7 +60,6 @@ struct FwdArgs {
   float* out;
   int32_t* err;
   const float* upack;  // FwFM A-operand fragments [MT][S][64]: strictly-upper (R + R^T)/2
-  const float* utri;   // the same U row-major [F][r4(F)] (zero on and below the diagonal): the MLP-free lane kernel
   const int2* pairs;   // kPairs: the nonzero strictly-upper entries of (R + R^T)/2, (k | l << 16, w bits), k-major
   int32_t npairs;
   const float* fwlw;   // [F*D]
@@ -348,7 +346,7 @@ inline hipError_t ensure_lds_limit(const void* fn, size_t lds) {
 }
 
 // One packing job of set_dense (see pack_dense_kernel).
-enum PackType : int32_t { kPackPad = 0, kPackLinear = 1, kPackLinearT = 2, kPackFwfm = 3, kPackFwfmSym = 4, kPackFwfmTri = 5 };
+enum PackType : int32_t { kPackPad = 0, kPackLinear = 1, kPackLinearT = 2, kPackFwfm = 3, kPackFwfmSym = 4 };
 struct PackJob {
   const float* src;
   float* dst;
@@ -405,10 +403,6 @@ size_t fwd16ws_lds_bytes(int F, int D, int MT, int S, int SX);
 size_t fwdp_lds_bytes(int F, int D, int MT, int S, int SX);
 hipError_t launch_fwdp(const FwdArgs& a, int D, size_t lds, int cus, hipStream_t s);
 hipError_t launch_fwd16ws(const FwdArgs& a, int D, size_t lds, hipStream_t s);
-// the MLP-free forward with a lane per (sample, column pair) (dfwfm_fwfm.hip): fwfm_lane_rows samples per workgroup
-bool fwfm_lane_supported(int F, int num, int D);
-int fwfm_lane_rows(int D);
-hipError_t launch_fwfm_lane(const FwdArgs& a, hipStream_t s);
 // per-embedding-size launchers, each compiled in its own translation unit (-DDFWFM_KD=<D>)
 #define DFWFM_PER_D_CAT2(a, b) a##b
 #define DFWFM_PER_D_CAT(a, b) DFWFM_PER_D_CAT2(a, b)

@@ -227,13 +227,11 @@ fwd_kernel(FwdArgs p) {
     }
   }
   f32x4 uw[kUpkPT];
-  // kValuFwfm: the row-major U [F][r4(F)] for fwfm_valu instead of the MFMA fragments (same LDS region)
-  const bool valu = D == 10 && (flags & kValuFwfm) != 0;
-  const int n_upk = (PART != 3 && (flags & kHasSecond)) ? (valu ? F * r4(F) / 4 : p.MT * p.S * 16) : 0;
+  const int n_upk = (PART != 3 && (flags & kHasSecond)) ? p.MT * p.S * 16 : 0;  // PART 3 reads them from global
 #pragma unroll
   for (int k = 0; k < kUpkPT; ++k) {
     const int i = tid + k * NTH;
-    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(valu ? p.utri : p.upack)[i];
+    if (i < n_upk) uw[k] = reinterpret_cast<const f32x4*>(p.upack)[i];
   }
   float fw[kFwlwPT];
   const int n_fwlw = (flags & kFoFwlw) ? F * D : 0;
@@ -500,8 +498,6 @@ fwd_kernel(FwdArgs p) {
         if (lane == 0) part2[b] = part;
       }
     }
-  } else if ((flags & kHasSecond) && valu) {
-    if constexpr (D == 10) fwfm_valu<39, 10, kBM>(bufX, SX, reinterpret_cast<const float4*>(upk), part2, wave, NW, lane);
   } else if (flags & kHasSecond) {
     // Y = U * E_b on MFMA: rows k (fields, MT tiles of 16), columns n = b*D + d (D tiles of 16), contraction
     // over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].  The work is cut into
@@ -591,8 +587,6 @@ fwd_kernel(FwdArgs p) {
     if (flags & kHasSecond) {
       if constexpr (PART == 3) {
         second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
-      } else if (valu) {
-        second = q == 0 ? part2[b] : 0.f;  // fwfm_valu's sum
       } else {
         for (int d = q; d < D; d += 16) {  // D = 32: two terms per lane
           const int n = b * D + d;
@@ -829,7 +823,6 @@ fwd_kernel(FwdArgs p) {
 //                  the diagonal is removed by :366-367); FM: 1 above the diagonal.  Fragment order
 //                  out[(m*S + s)*64 + lane] = U[16m + (lane&15)][4s + (lane>>4)]
 //   kPackFwfmSym   the backward's symmetric off-diagonal (R + R^T)/2 (FM: ones), same order
-//   kPackFwfmTri   U row-major [F][r4(F)], zero on and below the diagonal and in the padding (the lane kernel)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void pack_elem(const PackJob& j, int64_t i) {
   switch (j.type) {
@@ -852,12 +845,6 @@ __device__ __forceinline__ void pack_elem(const PackJob& j, int64_t i) {
         v[s] = (n < N && k < K) ? j.src[(int64_t)n * K + k] : 0.f;
       }
       reinterpret_cast<float4*>(j.dst)[i] = make_float4(v[0], v[1], v[2], v[3]);
-      break;
-    }
-    case kPackFwfmTri: {
-      const int F = j.a, mode = j.b, FP = j.d;
-      const int k = (int)(i / FP), l = (int)(i - (int64_t)k * FP);
-      j.dst[i] = (l > k && l < F) ? ((mode == 1) ? 1.f : (j.src[l * F + k] + j.src[k * F + l]) * 0.5f) : 0.f;
       break;
     }
     case kPackFwfm:
