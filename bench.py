@@ -186,8 +186,6 @@ def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
     train, part, tile groups); DFWFM_NG / DFWFM_SPLIT / DFWFM_R32 select the A/B variants."""
     if r32_on(config, cu_mask, batch_set):
         qr = 'true' if config == 'qr' else 'false'
-        if cu_mask in (None, "none") and os.environ.get("DFWFM_PERSIST", "1") != "0":
-            return f"dfwfm::fwdp_kernel<10,{qr}>"  # persistent, gather waves a tile ahead (DESIGN.md 3.6)
         return f"dfwfm::fwd32_kernel<10,{qr}>"
     if config in ("fwfm", "fwfm_pruned"):
         if os.environ.get("DFWFM_NO_PART3"):
@@ -195,10 +193,6 @@ def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
         png = os.environ.get("DFWFM_P3_NG")
         ng = 4 if png == "4" or (png is None and batch_set > 1) else 8  # batch sets: four waves
         return f"dfwfm::fwd_kernel<10,1,1,false,3,{ng},3,false>"  # MLP-free, 3 FwFM row tiles, no QR field
-    if batch_set == 1 and cu_mask in (None, "none") and os.environ.get("DFWFM_WS", "1") != "0" \
-            and not os.environ.get("DFWFM_SPLIT") and config != "pruned_sparse":
-        # a lone 4096-row batch on the whole chip: one 16-sample tile per CU, the wave-specialised form
-        return f"dfwfm::fwd16ws_kernel<10,{'true' if config == 'qr' else 'false'}>"
     ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
     tpw = 6 if ng == 4 else 3
     if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):

@@ -206,38 +206,3 @@ def test_forward_rejects_column_major_inputs(gpu):
     rf = m.eval_by_batch(np.asfortranarray(xi), np.asfortranarray(xv), y, n)
     rc = m.eval_by_batch(xi, xv, y, n)
     assert rf[:2] == rc[:2]
-
-
-@pytest.mark.parametrize("qr", [0, 1])
-@pytest.mark.parametrize("nb,B", [(4, 4096), (9, 4096 + 31), (33, 1024), (1, 20000)])
-def test_persistent_set_bit_identical_to_fwd32(gpu, monkeypatch, qr, nb, B):
-    """The persistent batch-set forward (fwdp_kernel: one workgroup per CU walking 32-sample tiles, gather waves
-    preparing tile j+1 while the MLP waves run tile j) gives fwd32's bits (DFWFM_PERSIST=0) on every batch of the set
-    -- sets that fill the chip, ragged batches, more batches than one launch holds, one large batch -- and the
-    oracle's logits at the north-star bar."""
-    cfg, params, _ = _criteo_model(gpu, 1, qr, seed=303 + qr)
-    host = _inputs(cfg["feature_sizes"], nb, B, seed=17 * nb + B)
-    res = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("DFWFM_PERSIST", v)
-        from xsdeepfwfm_deprecated_amd import DeepFMs
-        m = DeepFMs(**model_kwargs(cfg))
-        m.load_state_dict({k: torch.from_numpy(x) for k, x in params.items()})
-        m = m.to(gpu).eval()
-        eng = m._sync_engine(gpu)
-        dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
-        outs = [torch.full((B,), float("nan"), device=gpu) for _ in dev]
-        with torch.no_grad():
-            if nb > 1:
-                eng.forward_batches(dev, outs)
-            else:
-                eng.forward(dev[0][0], dev[0][1], outs[0])
-        torch.cuda.synchronize()
-        res[v] = [o.cpu().numpy() for o in outs]
-    for a, b in zip(res["0"], res["1"]):
-        assert np.array_equal(a, b)
-    rng = np.random.default_rng(nb)
-    for i in (0, nb - 1):
-        rows = rng.choice(B, 48, replace=False)
-        xi, xv = host[i]
-        assert logit_close(res["1"][i][rows], dfwfm_oracle.forward(cfg, params, xi[rows], xv[rows])) < 1e-5

@@ -405,44 +405,6 @@ def test_fwd32_bit_identical_to_fwd_kernel(gpu, monkeypatch, qr, B):
     assert logit_close(outs["1"][rows], dfwfm_oracle.forward(cfg, params, xi[rows], xv[rows])) < 1e-5
 
 
-@pytest.mark.parametrize("qr", [0, 1])
-@pytest.mark.parametrize("fwlw", [0, 1])
-@pytest.mark.parametrize("B", [1, 33, 4096])
-def test_fwd16ws_bit_identical_to_fwd_kernel(gpu, monkeypatch, qr, fwlw, B):
-    """The wave-specialised one-tile-per-CU forward (fwd16ws_kernel: MLP waves start layer 1 on the numerical columns
-    while gather waves load the categorical rows and run the FwFM; a lone batch of <= 16 x CUs rows) gives the same
-    bits as fwd_kernel's static form (DFWFM_WS=0) and the oracle's logits at the north-star bar."""
-    from xsdeepfwfm_deprecated_amd import synth
-    sizes = synth.CRITEO_FEATURE_SIZES
-    cfg = dict(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_logit=0,
-               use_deep=1, use_lw=1, use_fwlw=fwlw, h_depth=3, deep_nodes=400, numerical=13, embedding_bag=qr,
-               qr_flag=qr, qr_operation="mult", qr_collisions=4, qr_threshold=200)
-    from xsdeepfwfm_deprecated_amd import DeepFMs
-    m = DeepFMs(**model_kwargs(cfg))
-    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
-    params = synth.synth_state(shapes, 39, 10, 400, True, True, seed=71 + qr + 2 * fwlw)
-    xi, xv = synth.synth_inputs(sizes, 13, B, seed=B + 5)
-    outs = {}
-    for ws in ("0", "1"):
-        monkeypatch.setenv("DFWFM_WS", ws)
-        mm = make_model(cfg, params, gpu)
-        outs[ws] = run(mm, xi, xv, gpu)
-    assert np.array_equal(outs["0"], outs["1"])
-    rows = np.arange(B) if B < 200 else np.random.default_rng(5).choice(B, 128, replace=False)
-    assert logit_close(outs["1"][rows], dfwfm_oracle.forward(cfg, params, xi[rows], xv[rows])) < 1e-5
-
-
-@pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_fwlw_lw", "deepfwfm_qr_mult", "deepfwfm_qr_add_fwlw",
-                                  "deepfwfm_embbag", "deepfwfm_pruned", "fm_deep"])
-def test_fwd16ws_matches_reference_goldens(gpu, monkeypatch, name):
-    """Every deep golden through the wave-specialised forward in 16-row launches of one tile per CU or fewer."""
-    monkeypatch.setenv("DFWFM_WS", "1")
-    cfg, params, xi, xv, y, l32, l64, auc = load_golden(name)
-    m = make_model(cfg, params, gpu)
-    got = np.concatenate([run(m, xi[i:i + 1024], xv[i:i + 1024], gpu) for i in range(0, len(xi), 1024)])
-    assert logit_close(got, l32) < 1e-5 and logit_close(got, l64) < 1e-5
-
-
 @pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_fwlw_lw", "deepfwfm_qr_mult", "deepfwfm_qr_add_fwlw",
                                   "deepfwfm_embbag", "deepfwfm_pruned", "fm_deep"])
 def test_fwd32_matches_reference_goldens(gpu, monkeypatch, name):

@@ -44,7 +44,7 @@ vals, durs = {}, {}
 for path in glob.glob(os.path.join(root, f"pmc_{tag}_*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
-        if not any(n in k for n in ("fwd_kernel", "fwd32_kernel", "fwd16ws_kernel", "fwfm_lane_kernel")):
+        if not any(n in k for n in ("fwd_kernel", "fwd32_kernel")):
             continue
         k = k.replace("void ", "").replace(" ", "").split("(")[0]  # bench.py's kernel_name form
         vals.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))

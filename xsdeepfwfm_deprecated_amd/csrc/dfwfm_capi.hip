@@ -27,10 +27,6 @@ struct dfwfm_model {
   int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
   int r32;             // 32-sample workgroups (fwd32_kernel) usable: 0 no, 1 when the stream's CUs are covered, 2 forced
   size_t lds_r32;
-  int ws;              // fwd16ws_kernel usable (one 16-sample tile per CU or fewer)
-  size_t lds_ws;
-  int persist;         // fwd32's launches as the persistent fwdp_kernel (DFWFM_PERSIST=0: plain fwd32, A/B)
-  size_t lds_p;
   void* cu_stream[8];  // streams whose CU counts are cached (hipExtStreamGetCUMask), round-robin replaced
   int cu_count[8], cu_n, cu_next;
   int dev_cus;         // CUs of the device (0 until the first stream_cu_count)
@@ -280,15 +276,6 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     // batches in flight on plain streams take disjoint halves of the chip; A/B against CU-masked streams)
     if (const char* pad = getenv("DFWFM_R32_LDS"))
       if (m->r32 && (size_t)atol(pad) > m->lds_r32 && atol(pad) <= 160 * 1024) m->lds_r32 = (size_t)atol(pad);
-    // the wave-specialised 16-sample form for a lone batch that gives each CU at most one 16-sample tile (same
-    // shapes as fwd32; DFWFM_WS=0 keeps fwd_kernel there, for A/B)
-    const char* ws = getenv("DFWFM_WS");
-    m->ws = (c.use_deep && fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG) && (!ws || atoi(ws) != 0)) ? 1 : 0;
-    m->lds_ws = m->ws ? fwd16ws_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
-    const char* pe = getenv("DFWFM_PERSIST");
-    m->persist = (m->r32 && (!pe || atoi(pe) != 0)) ? 1 : 0;
-    m->lds_p = m->persist ? fwdp_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
-    if (m->lds_p > 160 * 1024) m->persist = 0;
   }
   // split forward (opt-in, DFWFM_SPLIT=1): the gather / shallow part and the MLP as two launches, each
   // with its own roofline (HBM-bound gather, MFMA-bound MLP) for profiling.  Measured slower than the
@@ -491,7 +478,6 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
-
   // the static K loop (fwd_kernel NS = 25) when every layer is 25 chunks deep and 25 tiles wide
   a.ns = (m->NC0 == 25 && m->NT == 25 && !getenv("DFWFM_NO_STATIC_K")) ? 25 : 0;
   memcpy(a.fw_list4, m->fw_list4, sizeof a.fw_list4);
@@ -603,20 +589,6 @@ bool use_fwd32(dfwfm_model* m, int64_t batch, void* stream) {
   return (batch + 31) / 32 >= (masked ? 1 : 2) * (int64_t)cus;
 }
 
-// fwd16ws when the launch's 16-sample tiles give no CU of the stream a second one (call after use_fwd32 said no)
-bool use_fwd16ws(dfwfm_model* m, int64_t batch, void* stream) {
-  if (m->ws == 0) return false;
-  return (batch + kBM - 1) / kBM <= (int64_t)stream_cu_count(m, stream);
-}
-
-// the deep forward's kernel for `rows` rows on `stream`: 3 fwdp (fwd32's rows on an unmasked stream: persistent,
-// one workgroup per CU), 2 fwd32 (a CU-masked stream shares its CUs with another stream's launches, two workgroups
-// per CU), 1 fwd16ws, 0 fwd_kernel
-int deep_form(dfwfm_model* m, int64_t rows, void* stream) {
-  if (use_fwd32(m, rows, stream)) return (m->persist && stream_cu_count(m, stream) >= m->dev_cus) ? 3 : 2;
-  return use_fwd16ws(m, rows, stream) ? 1 : 0;
-}
-
 }  // namespace
 
 extern "C" {
@@ -637,18 +609,13 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
     if (!pr || atoi(pr) != 0) a.flags |= kPrio;
     if (const char* pe = getenv("DFWFM_PRIO_EPI"); !pe || atoi(pe) != 0) a.flags |= kPrioEpi;
     if (const char* dt = getenv("DFWFM_DEFER_TAIL"); !dt || atoi(dt) != 0) a.flags |= kDeferTail;
-    if (const char* nt = getenv("DFWFM_NT_ROWS"); nt && atoi(nt) != 0) a.flags |= kNtRows;
   }
   // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
-  const int form = (a.flags & kHasDeep) ? deep_form(m, batch, stream) : 0;
-  if (form == 3) a.tiles = (int32_t)((batch + 31) / 32);
-  hipError_t e = form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
-                 : form == 2 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
-                 : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
-                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
-                                              (hipStream_t)stream);
+  const bool r32 = (a.flags & kHasDeep) && use_fwd32(m, batch, stream);
+  hipError_t e = r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                     : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
   return DFWFM_OK;
 }
@@ -674,8 +641,7 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
   if ((int64_t)nb * ((batch + kBM - 1) / kBM) > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "batch set too large");
   // the kernel for the first launch's rows (a set of up to kMaxSet batches); later launches of a larger set use it too
   const int64_t set_rows = (int64_t)(nb < kMaxSet ? nb : kMaxSet) * batch;
-  const int form = m->cfg.use_deep ? deep_form(m, set_rows, stream) : 0;
-  const bool r32 = form >= 2;
+  const bool r32 = m->cfg.use_deep && use_fwd32(m, set_rows, stream);
   const int rows = r32 ? 32 : kBM;
   for (int32_t i0 = 0; i0 < nb; i0 += kMaxSet) {
     const int32_t n = nb - i0 < kMaxSet ? nb - i0 : kMaxSet;
@@ -686,7 +652,6 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     // the next K loop -- 30.33 -> 30.08 us per batch at 2000 steps, 31.3 -> 31.05 on a 20-batch set (r03be)
     if (const char* pe = getenv("DFWFM_PRIO_EPI"); !pe || atoi(pe) != 0) a.flags |= kPrioEpi;
     if (const char* dt = getenv("DFWFM_DEFER_TAIL"); !dt || atoi(dt) != 0) a.flags |= kDeferTail;
-    if (const char* nt = getenv("DFWFM_NT_ROWS"); nt && atoi(nt) != 0) a.flags |= kNtRows;
     a.tail = m->tailI;
     if (n > 1) {
       a.nb = n;
@@ -699,12 +664,9 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     }
     int rc = diag_stamps_buffer(m, (int64_t)n * a.tiles * rows, 1, &a.stamps);
     if (rc != DFWFM_OK) return rc;
-    if (form == 3) a.tiles = (int32_t)((batch + 31) / 32);
-    const hipError_t e = form == 3 ? launch_fwdp(a, m->D, m->lds_p, stream_cu_count(m, stream), (hipStream_t)stream)
-                         : r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
-                         : form == 1 ? launch_fwd16ws(a, m->D, m->lds_ws, (hipStream_t)stream)
-                                     : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
-                                                      (hipStream_t)stream);
+    const hipError_t e = r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                             : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
+                                              (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "batch-set forward launch");
   }
   return DFWFM_OK;

@@ -16,10 +16,6 @@ __device__ __forceinline__ float relu_keep_nan(float v) { return v < 0.f ? 0.f :
 __device__ __forceinline__ void stamp(uint64_t* st, int slot, int tid) {
   if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
 }
-// the same, recorded by thread `who` (a wave-specialised kernel's other wave group)
-__device__ __forceinline__ void stamp_by(uint64_t* st, int slot, int tid, int who) {
-  if (st != nullptr && tid == who) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
-}
 
 // the batch and first row of this workgroup's tile (ROWS samples per workgroup), and that batch's inputs and logits:
 // the batch set of dfwfm_forward_batches (p.nb > 1), else the one batch of the launch
@@ -81,30 +77,6 @@ __device__ __forceinline__ void load_row(float (&v)[D], const float* __restrict_
   } else {
 #pragma unroll
     for (int d = 0; d < D; ++d) v[d] = src[d];
-  }
-}
-
-// the same loads marked non-temporal (the nt cache policy): embedding rows are read once per sample, so they should
-// not push the MLP weights every workgroup re-reads out of the XCD's L2
-template <int D>
-__device__ __forceinline__ void load_row_nt(float (&v)[D], const float* __restrict__ src) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  if constexpr (D % 4 == 0) {
-#pragma unroll
-    for (int d = 0; d < D; d += 4) {
-      const f4 x = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + d));
-      v[d] = x.x; v[d + 1] = x.y; v[d + 2] = x.z; v[d + 3] = x.w;
-    }
-  } else if constexpr (D % 2 == 0) {
-#pragma unroll
-    for (int d = 0; d < D; d += 2) {
-      const f2 x = __builtin_nontemporal_load(reinterpret_cast<const f2*>(src + d));
-      v[d] = x.x; v[d + 1] = x.y;
-    }
-  } else {
-#pragma unroll
-    for (int d = 0; d < D; ++d) v[d] = __builtin_nontemporal_load(src + d);
   }
 }
 

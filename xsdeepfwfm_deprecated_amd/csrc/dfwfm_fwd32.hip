@@ -75,7 +75,7 @@ template <int TPW, int RT, int NG, int NS>
 __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __restrict__ act, int SA,
                                           const LayerStream<TPW, 1, NG>& ls, f32x4 (&b0)[TPW], f32x4 (&b1)[TPW],
                                           f32x4 (&b2)[TPW], int lane, const TailStream<NG>& ts, f32x4 (&tp)[RT],
-                                          bool mid_barrier, int bar_at = -1) {
+                                          bool mid_barrier) {
   const int voff = lane * 16;
   const float* arow = act + (lane & 15) * SA + 4 * (lane >> 4);
   float4 a0[RT], a1[RT], a2[RT];
@@ -91,7 +91,6 @@ __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __
     float4 (&AX)[RT] = (i % 3 == 0) ? a0 : ((i % 3 == 1) ? a1 : a2);
     float4 (&AZ)[RT] = (i % 3 == 0) ? a2 : ((i % 3 == 1) ? a0 : a1);
     if (i + 3 == NS && mid_barrier) __syncthreads();  // the previous layer's split tile (chunk NS - 1) is written
-    if (i == bar_at) __syncthreads();                 // fwd16ws: the rest of the input tile is written (barrier B)
     if (i + 2 < NS) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) AZ[rt] = *reinterpret_cast<const float4*>(arow + rt * 16 * SA + 16 * (i + 2));
@@ -134,71 +133,6 @@ __device__ __forceinline__ void k_loop_rt(f32x4 (&acc)[RT][TPW], const float* __
   }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) tp[rt] = c0[rt] + c1[rt];
-}
-
-// FwFM pieces (fwd_kernel's (row tile m, column tile nt) work units, fw_list order) NP at a time with their MFMA
-// chains interleaved -- and both 16-row halves of each (RT = 2) -- for waves that run them beside another wave group's
-// MFMA K loop: one piece's 10-deep dependent chain at a time left them latency-bound.  Every chain is one piece's
-// steps in order from 4m, so the sums are fwd_kernel's bits.
-template <int NP, int RT, int D>
-__device__ __forceinline__ void fwfm_pieces(const uint8_t* __restrict__ list, int lo, int hi, const float* buf, int SX,
-                                            const float* upk, int S, int F, int MTD, float* part2, int lane) {
-  for (int pi = lo; pi < hi; pi += NP) {
-    int pc[NP], m[NP];
-    bool on[NP];
-    const float* ecol[NP];
-    const float* ua[NP];
-    int smin = S;
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      on[q] = pi + q < hi;
-      pc[q] = list[on[q] ? pi + q : pi];
-      m[q] = pc[q] / D;
-      const int nt = pc[q] - m[q] * D;
-      const int n = nt * 16 + (lane & 15);
-      const int b = n / D;
-      ecol[q] = buf + b * SX + (n - b * D);
-      ua[q] = upk + m[q] * S * 64 + lane;
-      if (on[q]) smin = 4 * m[q] < smin ? 4 * m[q] : smin;
-    }
-    f32x4 acc[NP][RT];
-#pragma unroll
-    for (int q = 0; q < NP; ++q)
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[q][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = smin; s < S; ++s) {
-      float av[NP], bv[NP][RT];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        av[q] = ua[q][s * 64];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) bv[q][rt] = ecol[q][rt * 16 * SX + (4 * s + (lane >> 4)) * D];
-      }
-#pragma unroll
-      for (int q = 0; q < NP; ++q)
-        if (on[q] && s >= 4 * m[q])
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt) acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q][rt], acc[q][rt], 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      if (!on[q]) continue;
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const float* ec = ecol[q] + rt * 16 * SX;
-        float v = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * m[q] + 4 * (lane >> 4) + r;
-          const int kk = (k < F ? k : 0) * D;
-          v = fmaf(k < F ? ec[kk] : 0.f, acc[q][rt][r], v);
-        }
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if (lane < 16) part2[(rt * MTD + pc[q]) * 16 + lane] = v;
-      }
-    }
-  }
 }
 
 }  // namespace
@@ -392,15 +326,9 @@ fwd32_kernel(FwdArgs p) {
         for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
       }
       if (live[k] && needE) {
-        if (flags & kNtRows) {
-          load_row_nt<D>(va[k], pa[k]);
-          if constexpr (QR)
-            if (mode[k] != 0) load_row_nt<D>(vb[k], pb[k]);
-        } else {
-          load_row<D>(va[k], pa[k]);
-          if constexpr (QR)
-            if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
-        }
+        load_row<D>(va[k], pa[k]);
+        if constexpr (QR)
+          if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
       }
       if (live[k] && fo_tab) {
         fa[k] = *qa[k];
@@ -666,836 +594,6 @@ fwd32_kernel(FwdArgs p) {
   }
   stamp(p.stamps, 8, tid);
   stamp_end_rt(p.stamps, tid);
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// fwd16ws_kernel: ONE 16-sample tile per workgroup with its waves specialised -- the form for a lone batch on the whole
-// chip (the reference's call pattern: one forward per batch, model/DeepFMs.py:750-780, :1012-1028), where a 4096-row
-// batch is one 16-row tile per CU and no second workgroup shares the CU to hide the gather and the FwFM.
-//   waves 0-7 (MLP): load Xv and the numerical fields' rows, write those E columns, preload layer 1's weights, and
-//     start layer 1's K loop on the numerical chunks while the categorical rows are still in flight;
-//   waves 8-11 (shallow): load the keys and the categorical / QR rows, write the rest of E and the first order, then
-//     -- concurrently with layer 1's K loop -- the FwFM second order (fwd_kernel's pieces on four waves) and
-//     first + second per sample, and exit.
-// Barriers: A (numerical E written), B (all of E written; inside layer 1's K loop, before the first chunk with a
-// categorical column is read), C (the shallow sums written; the MLP waves' barrier after layer 1's K loop).  A wave
-// that has ended no longer takes part in a barrier (s_barrier waits on the surviving waves), so the MLP waves'
-// later barriers are theirs alone.  Per sample the arithmetic is fwd_kernel's static form (the same FwFM pieces, the
-// same sums, the same K order): the same logits bits as fwd_kernel and fwd32_kernel.
-namespace {
-constexpr int kWsRows = 16;
-constexpr int kWsSW = 4;                    // shallow waves
-constexpr int kWsNTH = 64 * (kNG + kWsSW);  // 768 threads
-constexpr int kWsRPTN = 2;                  // numerical rows per MLP thread (16 * F <= 768 at F <= 48)
-constexpr int kWsRPTC = 3;                  // categorical rows per shallow thread
-
-__host__ __device__ inline Lds32 ldsws_layout(int F, int D, int MT, int S, int SX) {
-  Lds32 L;
-  int o = 0;
-  L.buf = o;   o += kWsRows * SX;
-  L.fs = o;    o += kWsRows;
-  L.dsum = o;  o += kNG * kWsRows;
-  int s = o;
-  L.desc = s;  s += r4(14 * F);
-  L.lw = s;    s += r4(F);
-  L.fwlw = s;  s += r4(F * D);
-  L.upk = s;   s += MT * S * 64;
-  L.fo = s;    s += kWsRows * r4(F);
-  L.part2 = s; s += MT * D * 16;
-  int t = o;
-  L.tailr = t; t += kNG * 64 * 4;
-  L.taild = t; t += 4 * kWsRows;
-  L.total = r4(s > t ? s : t);
-  return L;
-}
-}  // namespace
-
-template <int D, bool QR>
-__global__ void __launch_bounds__(kWsNTH) fwd16ws_kernel(FwdArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool mlpw = wave < kNG;
-  const int F = p.F;
-  const int num = p.num;
-  const int SX = p.SX;
-  const int flags = p.flags;
-  const int Fp = r4(F);
-  const Lds32 L = ldsws_layout(F, D, p.MT, p.S, SX);
-  float* buf = smem + L.buf;
-  float* fs = smem + L.fs;
-  float* dsum = smem + L.dsum;
-  FieldDev* desc = reinterpret_cast<FieldDev*>(smem + L.desc);
-  float* lw_s = smem + L.lw;
-  float* fwlw_s = smem + L.fwlw;
-  float* upk = smem + L.upk;
-  float* fo = smem + L.fo;
-  float* part2 = smem + L.part2;
-  float* tailr = smem + L.tailr;
-  float* taild = smem + L.taild;
-  const TileRef tr = tile_ref<kWsRows>(p);
-  const int64_t b0 = tr.b0;
-  stamp(p.stamps, 0, tid);
-  stamp_start_rt(p.stamps, tid);
-  const int g = wave;
-  LayerStream<kTPW, 1, kNG> ls;
-  f32x4 wb0[kTPW], wb1[kTPW], wb2[kTPW];
-  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float4*>(p.wpack), (short)0, p.wpack_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.mlp_b), (short)0, p.H * p.NT * 16 * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.fc), (short)0, p.NT * 16 * 4, 0x00020000);
-  TailStream<kNG> ts;
-  constexpr int TT = kNG * kTPW;  // the split tile
-  const bool needE = (flags & kNeedE) != 0;
-  const bool fo_tab = (flags & kFoTables) != 0;
-  const int nrows = kWsRows * num;               // numerical rows (MLP threads)
-  const int crows = kWsRows * (F - num);         // categorical rows (shallow threads)
-  __shared__ int ws_done;                        // shallow waves whose FwFM pieces are written
-  if (tid == 64 * kNG) ws_done = 0;              // before barrier A; counted after barrier B
-
-  if constexpr (QR) {  // descriptors staged in LDS by every thread
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    for (int i = tid; i < 7 * F; i += kWsNTH) reinterpret_cast<u32x2*>(desc)[i] = reinterpret_cast<const u32x2*>(p.fields)[i];
-    __syncthreads();
-  }
-  auto fdesc = [&](int f) -> FieldDev { if constexpr (QR) return desc[f]; else return p.fields[f]; };
-
-  if (mlpw) {
-    // ---- MLP waves: numerical rows (E = v_f * Xv, first order emb1[0] * Xv), the E padding, layer 1's weights ----
-    float va[kWsRPTN][D], fa[kWsRPTN], xs[kWsRPTN];
-    bool live[kWsRPTN];
-#pragma unroll
-    for (int k = 0; k < kWsRPTN; ++k) {
-      const int r = tid + k * 64 * kNG;
-      const int f = r >> 4;
-      const int64_t gb = b0 + (r & 15);
-      live[k] = r < nrows && gb < p.batch;
-      xs[k] = live[k] ? tr.xv[gb * p.xv_stride + f] : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < kWsRPTN; ++k) {
-      const int r = tid + k * 64 * kNG;
-      const int f = r >> 4;
-      fa[k] = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) va[k][d] = 0.f;
-      if (live[k]) {
-        const FieldDev fd = fdesc(f);
-        if (needE) load_row<D>(va[k], fd.emb2);
-        if (fo_tab) fa[k] = *fd.emb1;
-      }
-    }
-    ls.init(wrsrc, 0, p.NC0, p.NT, g, 0);
-    ls.preload(wb0, wb1, lane * 16);
-    const int w = p.W0 - F * D;
-    for (int i = tid; i < kWsRows * w; i += 64 * kNG) {
-      const int b = i / w;
-      buf[b * SX + F * D + (i - b * w)] = 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < kWsRPTN; ++k) {
-      const int r = tid + k * 64 * kNG;
-      if (r < nrows) {
-        const int f = r >> 4, b = r & 15;
-        if (needE) {
-          float e[D];
-#pragma unroll
-          for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(0, va[k][d], 0.f, xs[k]) : 0.f;
-          store_row<D>(buf + b * SX + f * D, e);
-        }
-        fo[b * Fp + f] = live[k] ? combine(0, fa[k], 0.f, xs[k]) : 0.f;
-      }
-    }
-    __syncthreads();  // A: the numerical E columns
-    stamp(p.stamps, 1, tid);
-  } else {
-    // ---- shallow waves: keys, categorical / QR rows, the shallow parameters -------------------------------------
-    if (flags & kPrio) __builtin_amdgcn_s_setprio(1);
-    const int st = tid - 64 * kNG;
-    constexpr int RQ = QR ? kWsRPTC : 1;
-    const float* pa[kWsRPTC];
-    const float* qa[kWsRPTC];
-    const float* pb[RQ];
-    const float* qb[RQ];
-    int mode[kWsRPTC];
-    bool live[kWsRPTC];
-#pragma unroll
-    for (int k = 0; k < kWsRPTC; ++k) {
-      const int r = st + k * 64 * kWsSW;
-      const int f = num + (r >> 4);
-      const int64_t gb = b0 + (r & 15);
-      live[k] = r < crows && gb < p.batch;
-      pa[k] = qa[k] = nullptr;
-      if constexpr (QR) pb[k] = qb[k] = nullptr;
-      mode[k] = 0;
-      if (!live[k]) continue;
-      const FieldDev fd = fdesc(f);
-      int64_t idx = tr.xi[gb * p.xi_stride + (f - num)];
-      if (idx < 0 || idx >= fd.n) {
-        atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
-        idx = 0;
-      }
-      if (!QR || fd.c == 0) {
-        pa[k] = fd.emb2 + idx * D;
-        if (fo_tab) qa[k] = fd.emb1 + idx;
-      } else if constexpr (QR) {
-        const int64_t q = idx / fd.c;
-        const int64_t rr = idx - q * fd.c;
-        mode[k] = fd.op == 0 ? 1 : 2;
-        pa[k] = fd.emb2 + q * D;
-        pb[k] = fd.emb2_r + rr * D;
-        if (fo_tab) {
-          qa[k] = fd.emb1 + q;
-          qb[k] = fd.emb1_r + rr;
-        }
-      }
-    }
-    float va[kWsRPTC][D], vb[RQ][D], fa[kWsRPTC], fb[RQ];
-#pragma unroll
-    for (int k = 0; k < kWsRPTC; ++k) {
-      fa[k] = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) va[k][d] = 0.f;
-      if constexpr (QR) {
-        fb[k] = 0.f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
-      }
-      if (live[k] && needE) {
-        load_row<D>(va[k], pa[k]);
-        if constexpr (QR)
-          if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
-      }
-      if (live[k] && fo_tab) {
-        fa[k] = *qa[k];
-        if constexpr (QR)
-          if (mode[k] != 0) fb[k] = *qb[k];
-      }
-    }
-    // the shallow parameters to LDS while the rows are in flight
-    const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
-    for (int i = st; i < n_upk; i += 64 * kWsSW) reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(p.upack)[i];
-    if (flags & kFoFwlw)
-      for (int i = st; i < F * D; i += 64 * kWsSW) fwlw_s[i] = p.fwlw[i];
-    if (flags & kFoLw)
-      for (int i = st; i < F; i += 64 * kWsSW) lw_s[i] = p.lw[i];
-    __syncthreads();  // A
-    stamp_by(p.stamps, 2, tid, 64 * kNG);
-#pragma unroll
-    for (int k = 0; k < kWsRPTC; ++k) {
-      const int r = st + k * 64 * kWsSW;
-      if (r < crows) {
-        const int f = num + (r >> 4), b = r & 15;
-        if (needE) {
-          float e[D];
-#pragma unroll
-          for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(mode[k], va[k][d], QR ? vb[k][d] : 0.f, 1.f) : 0.f;
-          store_row<D>(buf + b * SX + f * D, e);
-        }
-        fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], QR ? fb[k] : 0.f, 1.f) : 0.f;
-      }
-    }
-    stamp_by(p.stamps, 9, tid, 64 * kNG);
-    __syncthreads();  // B: all of E
-    stamp_by(p.stamps, 3, tid, 64 * kNG);
-    // ---- first order (fwlw) and the FwFM second order: fwd_kernel's pieces over the four shallow waves ----------
-    const int sw = wave - kNG;
-    if (flags & kFoFwlw) {
-      for (int r = st; r < kWsRows * F; r += 64 * kWsSW) {
-        const int f = r >> 4;
-        const int b = r & 15;
-        const float* e = buf + b * SX + f * D;
-        const float* wv = fwlw_s + f * D;
-        float sacc = 0.f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) sacc += e[d] * wv[d];
-        fo[b * Fp + f] = sacc;
-      }
-    }
-    if (flags & kHasSecond) {
-      const int S = p.S;
-      fwfm_pieces<3, 1, D>(p.fw_list4, p.fw_off4[sw], p.fw_off4[sw + 1], buf, SX, upk, S, F, p.MT * D, part2, lane);
-    }
-    // the pieces reach the per-sample sums of every shallow wave through LDS; the MLP waves are inside layer 1's K
-    // loop, so instead of a workgroup barrier the four shallow waves count in on an LDS word (all four arrive:
-    // no shallow wave leaves before this point)
-    stamp_by(p.stamps, 10, tid, 64 * kNG);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) atomicAdd(&ws_done, 1);
-    while (__hip_atomic_load(&ws_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWsSW) __builtin_amdgcn_s_sleep(1);
-    {
-      const int b = sw * 4 + (lane >> 4);
-      const int q = lane & 15;
-      float first = 0.f, second = 0.f;
-      for (int f = q; f < F; f += 16) {
-        const float x = fo[b * Fp + f];
-        first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
-      }
-      if (flags & kHasSecond) {
-        for (int d = q; d < D; d += 16) {
-          const int n = b * D + d;
-          for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
-        }
-      }
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) {
-        first += __shfl_xor(first, o);
-        second += __shfl_xor(second, o);
-      }
-      if (q == 0) fs[b] = first + second;
-    }
-    stamp_by(p.stamps, 11, tid, 64 * kNG);
-    __syncthreads();  // C: the MLP waves' barrier after layer 1's K loop
-    return;
-  }
-
-  // ---- phase M (MLP waves): layer 1 starts on the numerical chunks; barrier B before the first categorical one ----
-  const int cB = (num * D) / 16;  // first K chunk with a categorical column
-  if (cB < 2) __syncthreads();    // B (the loop's first two activation reads would need it)
-  auto load_bias = [&](f32x4 (&bq)[kTPW], int h, int nq) {
-#pragma unroll
-    for (int j = 0; j < kTPW; ++j) {
-      int t = g + kNG * j;
-      t = t < p.NT ? t : p.NT - 1;
-      bq[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            brsrc, nq * 4, __builtin_amdgcn_readfirstlane((h * p.NT + t) * 64), 0));
-    }
-  };
-  f32x4 bq[kTPW];
-  load_bias(bq, 0, 4 * (lane >> 4));
-  int layer_off = 0;
-  for (int h = 0; h < p.H; ++h) {
-    int lv = lane;
-    asm volatile("" : "+v"(lv));
-    const int rowl = lv & 15;
-    const int nq = 4 * (lv >> 4);
-    const int NC = h == 0 ? p.NC0 : p.NT;
-    const bool last = h == p.H - 1;
-    const int boff = __builtin_amdgcn_readfirstlane((h * p.NT + TT) * 64 + (g & 3) * 4);
-    const int ntail = TT * 16 + nq + (g & 3);
-    const float bn_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, nq * 4, boff, 0));
-    f32x4 acc[1][kTPW];
-#pragma unroll
-    for (int j = 0; j < kTPW; ++j) acc[0][j] = bq[j];
-    ts.init(layer_off, NC, TT, g);
-    f32x4 tp[1];
-    k_loop_rt<kTPW, 1, kNG, kNS>(acc, buf, SX, ls, wb0, wb1, wb2, lane, ts, tp, h > 0 && (flags & kDeferTail),
-                                 h == 0 && cB >= 2 ? cB - 2 : -1);
-    if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(1);
-    if (h == 0) stamp(p.stamps, 12, tid);
-    __syncthreads();  // every wave has read the layer's input (h == 0: C, the shallow sums are in fs)
-    reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = tp[0];
-    float dpart = 0.f;
-    {
-      float* orow = buf + rowl * SX + nq;
-#pragma unroll
-      for (int j = 0; j < kTPW; ++j) {
-        const int t = g + kNG * j;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = relu_keep_nan(acc[0][j][r]);
-        if (!last) {
-          *reinterpret_cast<f32x4*>(orow + t * 16) = f32x4{v[0], v[1], v[2], v[3]};
-        } else {
-          const f32x4 wf = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(frsrc, nq * 4, t * 64, 0));
-          dpart = fmaf(v[0], wf[0], dpart);
-          dpart = fmaf(v[1], wf[1], dpart);
-          dpart = fmaf(v[2], wf[2], dpart);
-          dpart = fmaf(v[3], wf[3], dpart);
-        }
-      }
-    }
-    if (last) {
-      float d = dpart;
-      d += __shfl_xor(d, 16);
-      d += __shfl_xor(d, 32);
-      if (lane < 16) dsum[g * kWsRows + rowl] = d;
-    }
-    layer_off += p.NT * NC * 64;
-    if (!last) {
-      ls.init(wrsrc, layer_off, p.NT, p.NT, g, 0);
-      ls.preload(wb0, wb1, lane * 16);
-      load_bias(bq, h + 1, nq);
-    }
-    if (h == 0) stamp(p.stamps, 13, tid);
-    __syncthreads();
-    if (g < 4) {
-      const bool valid = ntail < p.N;
-      float wf_t = 0.f;
-      if (last)
-        wf_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                             frsrc, nq * 4, __builtin_amdgcn_readfirstlane(TT * 64 + g * 4), 0));
-      const float* tpp = tailr + lane * 4 + g;
-      float sum = tpp[0];
-#pragma unroll
-      for (int w = 1; w < kNG; ++w) sum += tpp[w * 256];
-      const float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
-      if (!last) {
-        buf[rowl * SX + TT * 16 + nq + g] = v;
-      } else {
-        float c = v * wf_t;
-        c += __shfl_xor(c, 16);
-        c += __shfl_xor(c, 32);
-        if (lane < 16) taild[g * kWsRows + rowl] = c;
-      }
-    }
-    if (last || !(flags & kDeferTail)) __syncthreads();
-    if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(0);
-    stamp(p.stamps, 4 + (h < 3 ? h : 3), tid);
-  }
-  if (tid < kWsRows && b0 + tid < p.batch) {
-    float deepv = dsum[tid];
-#pragma unroll
-    for (int w = 1; w < kNG; ++w) deepv += dsum[w * kWsRows + tid];
-    deepv += ((taild[tid] + taild[kWsRows + tid]) + taild[2 * kWsRows + tid]) + taild[3 * kWsRows + tid];
-    tr.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
-  }
-  stamp(p.stamps, 8, tid);
-  stamp_end_rt(p.stamps, tid);
-}
-
-size_t fwd16ws_lds_bytes(int F, int D, int MT, int S, int SX) {
-  return sizeof(float) * (size_t)ldsws_layout(F, D, MT, S, SX).total;
-}
-
-hipError_t launch_fwd16ws(const FwdArgs& a, int D, size_t lds, hipStream_t s) {
-  if (D != 10) return hipErrorInvalidValue;
-  auto k = (a.flags & kHasQR) ? fwd16ws_kernel<10, true> : fwd16ws_kernel<10, false>;
-  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(fwd_grid(a, kWsRows)), dim3(kWsNTH), lds, s, a);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// fwdp_kernel: a persistent batch-set forward, one workgroup per CU walking 32-sample tiles (w, w + G, ...), its waves
-// specialised and software-pipelined: the MLP waves (0-7) run tile j's three layers -- fwd32's K loop, epilogues and
-// split tile, both 16-row halves per wave, in place in E buffer j % 2 -- while the gather waves (8-11) load tile j+1's
-// rows into buffer (j+1) % 2, run its FwFM pieces and its first + second sums.  Two fwd32 workgroups sharing a CU fall
-// into step (the one behind catches up while the other is outside its K loop), so their gather and shallow phases
-// leave the matrix cores idle together; here the MLP waves never wait for a gather.
-// The two groups meet only at the MLP waves' own barriers (9 per tile: after each layer's K loop, after each
-// epilogue, the split tile's deferred one inside the next K loop, and the last layer's), the gather waves doing their
-// part of tile j+1 in the long intervals: the rows before the 1st (layer 1's K loop), fwlw + the FwFM pieces between
-// the 2nd and the 3rd (layer 2's K loop), the sums between the 5th and the 6th (layer 3's K loop).  After the last
-// tile they leave (a wave that has ended no longer counts in a barrier).  Tile 0 is prepared before the first tile
-// (three barriers).  Per sample the arithmetic is fwd32's: the same logits bits as fwd32 / fwd_kernel.
-namespace {
-constexpr int kPSW = 4;                   // gather waves
-constexpr int kPNTH = 64 * (kNG + kPSW);  // 768 threads
-constexpr int kPRR = 3;                   // rows per gather thread per round (two rounds: 32 x 48 rows)
-
-struct LdsP {
-  int buf0, buf1, fs, dsum, desc, lw, fwlw, upk, fo, part2, tailr, taild, total;
-};
-
-__host__ __device__ inline LdsP ldsp_layout(int F, int D, int MT, int S, int SX) {
-  LdsP L;
-  int o = 0;
-  L.buf0 = o;  o += kRows * SX;
-  L.buf1 = o;  o += kRows * SX;
-  L.fs = o;    o += 2 * kRows;
-  L.dsum = o;  o += kNG * kRows;
-  L.desc = o;  o += r4(14 * F);
-  L.lw = o;    o += r4(F);
-  L.fwlw = o;  o += r4(F * D);
-  L.upk = o;   o += MT * S * 64;
-  L.fo = o;    o += kRows * r4(F);
-  L.part2 = o; o += kRT * MT * D * 16;
-  L.tailr = o; o += kNG * kRT * 64 * 4;
-  L.taild = o; o += 4 * kRows;
-  L.total = r4(o);
-  return L;
-}
-
-// tile t of the launch: its batch's inputs / logits and first row
-__device__ __forceinline__ TileRef ptile(const FwdArgs& p, int t) {
-  if (p.nb > 1) {
-    const int bi = t / p.tiles;
-    return TileRef{p.set_xi[bi], p.set_xv[bi], p.set_out[bi], (int64_t)(t - bi * p.tiles) * kRows};
-  }
-  return TileRef{p.xi, p.xv, p.out, (int64_t)t * kRows};
-}
-}  // namespace
-
-template <int D, bool QR>
-__global__ void __launch_bounds__(kPNTH) fwdp_kernel(FwdArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int F = p.F;
-  const int num = p.num;
-  const int SX = p.SX;
-  const int flags = p.flags | kDeferTail;  // the gather waves' schedule assumes the deferred split-tile barrier
-  const int Fp = r4(F);
-  const LdsP L = ldsp_layout(F, D, p.MT, p.S, SX);
-  float* bufs[2] = {smem + L.buf0, smem + L.buf1};
-  float* fsb = smem + L.fs;
-  float* dsum = smem + L.dsum;
-  FieldDev* desc = reinterpret_cast<FieldDev*>(smem + L.desc);
-  float* lw_s = smem + L.lw;
-  float* fwlw_s = smem + L.fwlw;
-  float* upk = smem + L.upk;
-  float* fo = smem + L.fo;
-  float* part2 = smem + L.part2;
-  float* tailr = smem + L.tailr;
-  float* taild = smem + L.taild;
-  const int ntiles = p.nb > 1 ? p.nb * p.tiles : p.tiles;
-  const int G = gridDim.x;
-  const int t0 = blockIdx.x;
-  if (t0 >= ntiles) return;                       // uniform: no barrier reached
-  const int mine = (ntiles - t0 + G - 1) / G;     // tiles of this workgroup: t0, t0 + G, ...
-  const bool needE = (flags & kNeedE) != 0;
-  const bool fo_tab = (flags & kFoTables) != 0;
-  stamp(p.stamps, 0, tid);
-
-  if constexpr (QR) {
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    for (int i = tid; i < 7 * F; i += kPNTH) reinterpret_cast<u32x2*>(desc)[i] = reinterpret_cast<const u32x2*>(p.fields)[i];
-    __syncthreads();
-  }
-
-  if (wave >= kNG) {
-    // ================================ gather waves =====================================================================
-    const int st = tid - 64 * kNG;
-    const int sw = wave - kNG;
-    const int n_upk = (flags & kHasSecond) ? p.MT * p.S * 16 : 0;
-    for (int i = st; i < n_upk; i += 64 * kPSW) reinterpret_cast<f32x4*>(upk)[i] = reinterpret_cast<const f32x4*>(p.upack)[i];
-    if (flags & kFoFwlw)
-      for (int i = st; i < F * D; i += 64 * kPSW) fwlw_s[i] = p.fwlw[i];
-    if (flags & kFoLw)
-      for (int i = st; i < F; i += 64 * kPSW) lw_s[i] = p.lw[i];
-    // rows of tile t into buffer `buf`: E (both halves) and the table first order, fwd32's arithmetic
-    auto gather = [&](int t, float* buf) {
-      const TileRef tr = ptile(p, t);
-      const int64_t b0 = tr.b0;
-      if (flags & kPrio) __builtin_amdgcn_s_setprio(1);
-      const int w = p.W0 - F * D;
-      for (int i = st; i < kRows * w; i += 64 * kPSW) {
-        const int b = i / w;
-        buf[b * SX + F * D + (i - b * w)] = 0.f;
-      }
-      for (int round = 0; round * kPRR * 64 * kPSW < kRows * F; ++round) {
-        constexpr int RQ = QR ? kPRR : 1;
-        const float* pa[kPRR];
-        const float* qa[kPRR];
-        const float* pb[RQ];
-        const float* qb[RQ];
-        float scale[kPRR];
-        int mode[kPRR];
-        bool live[kPRR];
-#pragma unroll
-        for (int k = 0; k < kPRR; ++k) {
-          const int r = st + (round * kPRR + k) * 64 * kPSW;
-          const int f = r >> 5;
-          const int64_t gb = b0 + (r & 31);
-          live[k] = f < F && gb < p.batch;
-          pa[k] = qa[k] = nullptr;
-          if constexpr (QR) pb[k] = qb[k] = nullptr;
-          scale[k] = 1.f;
-          mode[k] = 0;
-          if (!live[k]) continue;
-          const FieldDev fd = QR ? desc[f] : p.fields[f];
-          if (f < num) {
-            scale[k] = tr.xv[gb * p.xv_stride + f];
-            pa[k] = fd.emb2;
-            qa[k] = fd.emb1;
-          } else {
-            int64_t idx = tr.xi[gb * p.xi_stride + (f - num)];
-            if (idx < 0 || idx >= fd.n) {
-              atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
-              idx = 0;
-            }
-            if (!QR || fd.c == 0) {
-              pa[k] = fd.emb2 + idx * D;
-              if (fo_tab) qa[k] = fd.emb1 + idx;
-            } else if constexpr (QR) {
-              const int64_t q = idx / fd.c;
-              const int64_t rr = idx - q * fd.c;
-              mode[k] = fd.op == 0 ? 1 : 2;
-              pa[k] = fd.emb2 + q * D;
-              pb[k] = fd.emb2_r + rr * D;
-              if (fo_tab) {
-                qa[k] = fd.emb1 + q;
-                qb[k] = fd.emb1_r + rr;
-              }
-            }
-          }
-        }
-        float va[kPRR][D], vb[RQ][D], fa[kPRR], fb[RQ];
-#pragma unroll
-        for (int k = 0; k < kPRR; ++k) {
-          fa[k] = 0.f;
-#pragma unroll
-          for (int d = 0; d < D; ++d) va[k][d] = 0.f;
-          if constexpr (QR) {
-            fb[k] = 0.f;
-#pragma unroll
-            for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
-          }
-          if (live[k] && needE) {
-            load_row<D>(va[k], pa[k]);
-            if constexpr (QR)
-              if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
-          }
-          if (live[k] && fo_tab) {
-            fa[k] = *qa[k];
-            if constexpr (QR)
-              if (mode[k] != 0) fb[k] = *qb[k];
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kPRR; ++k) {
-          const int r = st + (round * kPRR + k) * 64 * kPSW;
-          const int f = r >> 5;
-          const int b = r & 31;
-          if (f < F) {
-            if (needE) {
-              float e[D];
-#pragma unroll
-              for (int d = 0; d < D; ++d) e[d] = live[k] ? combine(mode[k], va[k][d], QR ? vb[k][d] : 0.f, scale[k]) : 0.f;
-              store_row<D>(buf + b * SX + f * D, e);
-            }
-            fo[b * Fp + f] = live[k] ? combine(mode[k], fa[k], QR ? fb[k] : 0.f, scale[k]) : 0.f;
-          }
-        }
-      }
-    };
-    // fwlw first order and the FwFM pieces of the tile in `buf` (every gather wave's rows are written)
-    auto fwfm = [&](const float* buf) {
-      if (flags & kFoFwlw) {
-        for (int r = st; r < kRows * F; r += 64 * kPSW) {
-          const int f = r >> 5;
-          const int b = r & 31;
-          const float* e = buf + b * SX + f * D;
-          const float* wv = fwlw_s + f * D;
-          float sacc = 0.f;
-#pragma unroll
-          for (int d = 0; d < D; ++d) sacc += e[d] * wv[d];
-          fo[b * Fp + f] = sacc;
-        }
-      }
-      if (flags & kHasSecond) {
-        const int S = p.S;
-        const int MTD = p.MT * D;
-        fwfm_pieces<2, kRT, D>(p.fw_list4, p.fw_off4[sw], p.fw_off4[sw + 1], buf, SX, upk, S, F, MTD, part2, lane);
-      }
-    };
-    // first[b] + second[b] of the 32 rows -> fs (fwd32's 16-lane sums; each gather wave two groups of four rows)
-    auto sums = [&](float* fs) {
-      for (int pass = 0; pass < 2; ++pass) {
-        const int b = (pass * kPSW + sw) * 4 + (lane >> 4);
-        const int h = b >> 4;
-        const int bl = b & 15;
-        const int q = lane & 15;
-        float first = 0.f, second = 0.f;
-        for (int f = q; f < F; f += 16) {
-          const float x = fo[b * Fp + f];
-          first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
-        }
-        if (flags & kHasSecond) {
-          const int MTD = p.MT * D;
-          for (int d = q; d < D; d += 16) {
-            const int n = bl * D + d;
-            for (int m = 0; m < p.MT; ++m) second += part2[(h * MTD + m * D + (n >> 4)) * 16 + (n & 15)];
-          }
-        }
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) {
-          first += __shfl_xor(first, o);
-          second += __shfl_xor(second, o);
-        }
-        if (q == 0) fs[b] = first + second;
-      }
-    };
-    // tile 0 before the MLP starts (three barriers)
-    gather(t0, bufs[0]);
-    stamp_by(p.stamps, 1, tid, 64 * kNG);
-    __syncthreads();  // P1
-    fwfm(bufs[0]);
-    stamp_by(p.stamps, 2, tid, 64 * kNG);
-    __syncthreads();  // P2
-    sums(fsb);
-    stamp_by(p.stamps, 3, tid, 64 * kNG);
-    __syncthreads();  // P3
-    // during tile i: tile i + 1, in the long intervals of the MLP waves' 9 barriers
-    for (int i = 0; i + 1 < mine; ++i) {
-      const int tn = t0 + (i + 1) * G;
-      float* bn = bufs[(i + 1) & 1];
-      gather(tn, bn);
-      if (i == 1) stamp_by(p.stamps, 11, tid, 64 * kNG);
-      __syncthreads();  // 1: after layer 1's K loop
-      __syncthreads();  // 2: after layer 1's epilogue
-      fwfm(bn);
-      if (i == 1) stamp_by(p.stamps, 12, tid, 64 * kNG);
-      __syncthreads();  // 3: the split tile's barrier inside layer 2's K loop
-      __syncthreads();  // 4: after layer 2's K loop
-      __syncthreads();  // 5: after layer 2's epilogue
-      sums(fsb + ((i + 1) & 1) * kRows);
-      if (i == 1) stamp_by(p.stamps, 13, tid, 64 * kNG);
-      __syncthreads();  // 6: inside layer 3's K loop
-      __syncthreads();  // 7
-      __syncthreads();  // 8
-      __syncthreads();  // 9
-    }
-    return;
-  }
-
-  // ================================== MLP waves =======================================================================
-  const int g = wave;
-  LayerStream<kTPW, 1, kNG> ls;
-  f32x4 wb0[kTPW], wb1[kTPW], wb2[kTPW];
-  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float4*>(p.wpack), (short)0, p.wpack_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.mlp_b), (short)0, p.H * p.NT * 16 * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.fc), (short)0, p.NT * 16 * 4, 0x00020000);
-  TailStream<kNG> ts;
-  constexpr int TT = kNG * kTPW;
-  auto load_bias = [&](f32x4 (&bq)[kTPW], int h, int nq) {
-#pragma unroll
-    for (int j = 0; j < kTPW; ++j) {
-      int t = g + kNG * j;
-      t = t < p.NT ? t : p.NT - 1;
-      bq[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            brsrc, nq * 4, __builtin_amdgcn_readfirstlane((h * p.NT + t) * 64), 0));
-    }
-  };
-  f32x4 bq[kTPW];
-  ls.init(wrsrc, 0, p.NC0, p.NT, g, 0);
-  ls.preload(wb0, wb1, lane * 16);
-  load_bias(bq, 0, 4 * (lane >> 4));
-  __syncthreads();  // P1
-  __syncthreads();  // P2
-  __syncthreads();  // P3
-  stamp(p.stamps, 9, tid);
-  for (int i = 0; i < mine; ++i) {
-    if (i == 1) stamp(p.stamps, 4, tid);
-    const TileRef tr = ptile(p, t0 + i * G);
-    const int64_t b0 = tr.b0;
-    float* buf = bufs[i & 1];
-    const float* fs = fsb + (i & 1) * kRows;
-    int layer_off = 0;
-    for (int h = 0; h < p.H; ++h) {
-      int lv = lane;
-      asm volatile("" : "+v"(lv));
-      const int rowl = lv & 15;
-      const int nq = 4 * (lv >> 4);
-      const int NC = h == 0 ? p.NC0 : p.NT;
-      const bool last = h == p.H - 1;
-      const int boff = __builtin_amdgcn_readfirstlane((h * p.NT + TT) * 64 + (g & 3) * 4);
-      const int ntail = TT * 16 + nq + (g & 3);
-      const float bn_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc, nq * 4, boff, 0));
-      f32x4 acc[kRT][kTPW];
-#pragma unroll
-      for (int rt = 0; rt < kRT; ++rt)
-#pragma unroll
-        for (int j = 0; j < kTPW; ++j) acc[rt][j] = bq[j];
-      ts.init(layer_off, NC, TT, g);
-      f32x4 tp[kRT];
-      k_loop_rt<kTPW, kRT, kNG, kNS>(acc, buf, SX, ls, wb0, wb1, wb2, lane, ts, tp, h > 0);
-      if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(1);
-      if (i == 1) stamp(p.stamps, 5 + h, tid);  // layer h's K loop done (before its barrier)
-      __syncthreads();  // every wave has read the layer's input: the tile may be overwritten
-#pragma unroll
-      for (int rt = 0; rt < kRT; ++rt) reinterpret_cast<f32x4*>(tailr)[(g * kRT + rt) * 64 + lane] = tp[rt];
-      float dpart[kRT] = {0.f, 0.f};
-#pragma unroll
-      for (int rt = 0; rt < kRT; ++rt) {
-        float* orow = buf + (rt * 16 + rowl) * SX + nq;
-#pragma unroll
-        for (int j = 0; j < kTPW; ++j) {
-          const int t = g + kNG * j;
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = relu_keep_nan(acc[rt][j][r]);
-          if (!last) {
-            *reinterpret_cast<f32x4*>(orow + t * 16) = f32x4{v[0], v[1], v[2], v[3]};
-          } else {
-            const f32x4 wf = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(frsrc, nq * 4, t * 64, 0));
-            dpart[rt] = fmaf(v[0], wf[0], dpart[rt]);
-            dpart[rt] = fmaf(v[1], wf[1], dpart[rt]);
-            dpart[rt] = fmaf(v[2], wf[2], dpart[rt]);
-            dpart[rt] = fmaf(v[3], wf[3], dpart[rt]);
-          }
-        }
-      }
-      if (last) {
-#pragma unroll
-        for (int rt = 0; rt < kRT; ++rt) {
-          float d = dpart[rt];
-          d += __shfl_xor(d, 16);
-          d += __shfl_xor(d, 32);
-          if (lane < 16) dsum[g * kRows + rt * 16 + rowl] = d;
-        }
-      }
-      layer_off += p.NT * NC * 64;
-      if (!last) {  // the next layer's first chunks and biases
-        ls.init(wrsrc, layer_off, p.NT, p.NT, g, 0);
-        ls.preload(wb0, wb1, lane * 16);
-        load_bias(bq, h + 1, nq);
-      } else if (i + 1 < mine) {  // the next tile's layer 1
-        ls.init(wrsrc, 0, p.NC0, p.NT, g, 0);
-        ls.preload(wb0, wb1, lane * 16);
-        load_bias(bq, 0, nq);
-      }
-      __syncthreads();
-      if (g < 4) {
-        const bool valid = ntail < p.N;
-        float wf_t = 0.f;
-        if (last)
-          wf_t = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                               frsrc, nq * 4, __builtin_amdgcn_readfirstlane(TT * 64 + g * 4), 0));
-#pragma unroll
-        for (int rt = 0; rt < kRT; ++rt) {
-          const float* tpp = tailr + (rt * 64 + lane) * 4 + g;
-          float sum = tpp[0];
-#pragma unroll
-          for (int w = 1; w < kNG; ++w) sum += tpp[w * kRT * 256];
-          const float v = valid ? relu_keep_nan(sum + bn_t) : 0.f;
-          if (!last) {
-            buf[(rt * 16 + rowl) * SX + TT * 16 + nq + g] = v;
-          } else {
-            float c = v * wf_t;
-            c += __shfl_xor(c, 16);
-            c += __shfl_xor(c, 32);
-            if (lane < 16) taild[g * kRows + rt * 16 + rowl] = c;
-          }
-        }
-      }
-      if (last) __syncthreads();
-      if (flags & kPrioEpi) __builtin_amdgcn_s_setprio(0);
-    }
-    if (tid < kRows && b0 + tid < p.batch) {
-      float deepv = dsum[tid];
-#pragma unroll
-      for (int w = 1; w < kNG; ++w) deepv += dsum[w * kRows + tid];
-      deepv += ((taild[tid] + taild[kRows + tid]) + taild[2 * kRows + tid]) + taild[3 * kRows + tid];
-      tr.out[b0 + tid] = (fs[tid] + deepv) + p.bias[0];
-    }
-    if (i == 1) stamp(p.stamps, 8, tid);
-  }
-}
-
-size_t fwdp_lds_bytes(int F, int D, int MT, int S, int SX) {
-  return sizeof(float) * (size_t)ldsp_layout(F, D, MT, S, SX).total;
-}
-
-// grid: one workgroup per CU (the LDS keeps a second one off), at most one per tile
-hipError_t launch_fwdp(const FwdArgs& a, int D, size_t lds, int cus, hipStream_t s) {
-  if (D != 10) return hipErrorInvalidValue;
-  auto k = (a.flags & kHasQR) ? fwdp_kernel<10, true> : fwdp_kernel<10, false>;
-  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
-  if (e != hipSuccess) return e;
-  const int64_t ntiles = a.nb > 1 ? (int64_t)a.nb * a.tiles : a.tiles;
-  const unsigned grid = (unsigned)(ntiles < cus ? ntiles : cus);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kPNTH), lds, s, a);
-  return hipGetLastError();
 }
 
 size_t fwd32_lds_bytes(int F, int D, int MT, int S, int SX) {

@@ -30,7 +30,6 @@ constexpr int kPrio = 256;     // raise the wave priority for the phases before 
 constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables)
 constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
 constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
-constexpr int kNtRows = 8192;  // embedding-row loads with the non-temporal cache policy (A/B: DFWFM_NT_ROWS)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kMaxH = 16;      // hidden layers
 constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)
@@ -395,14 +394,6 @@ hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 bool fwd32_supported(int F, int D, int H, int NT, int NC0, int tailI, int NG);
 size_t fwd32_lds_bytes(int F, int D, int MT, int S, int SX);
 hipError_t launch_fwd32(const FwdArgs& a, int D, size_t lds, hipStream_t s);
-// one 16-sample tile per workgroup with specialised waves (MLP / gather + FwFM): a lone batch on the whole chip;
-// the same shapes as fwd32 (fwd32_supported), bit-identical logits
-size_t fwd16ws_lds_bytes(int F, int D, int MT, int S, int SX);
-// persistent batch-set form of fwd32 (one workgroup per CU walking 32-sample tiles, gather waves a tile ahead of
-// the MLP waves): a.tiles must hold the 32-sample tiles per batch; bit-identical logits
-size_t fwdp_lds_bytes(int F, int D, int MT, int S, int SX);
-hipError_t launch_fwdp(const FwdArgs& a, int D, size_t lds, int cus, hipStream_t s);
-hipError_t launch_fwd16ws(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 // per-embedding-size launchers, each compiled in its own translation unit (-DDFWFM_KD=<D>)
 #define DFWFM_PER_D_CAT2(a, b) a##b
 #define DFWFM_PER_D_CAT(a, b) DFWFM_PER_D_CAT2(a, b)
