@@ -1,6 +1,8 @@
 """Per-phase cycle breakdown of the fused backward from in-kernel s_memtime stamps (diagnostic).
 
-    python tools/bwd_stamps.py [--batch 4096] [--iters 5]     (sets DFWFM_DIAG_STAMPS=2)
+    [DFWFM_DIAG_BWD=<bits>] python tools/bwd_stamps.py [--batch 4096] [--iters 5]     (sets DFWFM_DIAG_STAMPS=2)
+
+DFWFM_DIAG_BWD (diagnostics, results invalid for 1 and 2): 1 no G_l stores, 2 no mask loads, 4 the generic K loop
 """
 import argparse
 import ctypes
@@ -44,9 +46,10 @@ print(f"workgroups {n}; 100 MHz clock: first start -> last start {(rt0.max() - r
       f"first start -> last end {(rt1.max() - rt0.min()) / 100:.1f} us, median WG {np.median(rt1 - rt0) / 100:.1f} us")
 order = np.argsort(rt0)
 print("start offsets (us) by rank:", [(int(q), round((rt0[order[q]] - rt0.min()) / 100, 1)) for q in (0, 63, 127, 191, 255) if q < n])
-names = ["P0 stage", "P1 shallow dE (MFMA)", "P2 G_H init", "layer H", "layer H-1", "layer H-2",
-         "P3 dE store", "total"]
-slots = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (8, 9), (0, 9)]
+names = ["P0 stage", "P1 shallow dE (MFMA)", "  . Gram chains (wave 0)", "  . dE pieces (wave 0)",
+         "  . reductions, barrier, Gram sums", "P2 G_H init", "layer H", "layer H-1", "layer H-2", "P3 dE store",
+         "total"]
+slots = [(0, 1), (1, 2), (1, 12), (12, 13), (13, 2), (2, 3), (3, 4), (4, 5), (5, 6), (8, 9), (0, 9)]
 for nm, (s0, s1) in zip(names, slots):
     d = st[:, s1] - st[:, s0]
     print(f"{nm:24s} median {np.median(d):10.0f}  p10 {np.percentile(d, 10):10.0f}  p90 {np.percentile(d, 90):10.0f}")

@@ -1,6 +1,9 @@
 """Per-phase cycle breakdown of the fused forward from in-kernel s_memtime stamps (diagnostic).
 
-    DFWFM_DIAG_STAMPS=1 [DFWFM_R32=1] python tools/phase_stamps.py [--batch 4096] [--iters 20]
+    DFWFM_DIAG_STAMPS=1 [DFWFM_R32=1] python tools/phase_stamps.py [--batch 4096] [--iters 20] [--fwfm] [--batches N]
+
+--fwfm: the MLP-free FwFM-only model (fwd_kernel PART 3); --batches N: N distinct resident batches as one batch set
+(dfwfm_forward_batches), with the launch's workgroup lifetimes and concurrency from the 100 MHz stamps.
 """
 import argparse
 import ctypes
@@ -20,17 +23,24 @@ ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--fwlw", action="store_true")
 ap.add_argument("--train", action="store_true", help="stamp the training-mode forward (activations saved)")
+ap.add_argument("--fwfm", action="store_true", help="the MLP-free FwFM-only model")
+ap.add_argument("--batches", type=int, default=1, help="a batch set of this many distinct batches")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 sizes = synth.CRITEO_FEATURE_SIZES
-m = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1,
+m = DeepFMs(field_size=39, feature_sizes=sizes, embedding_size=10, use_fwfm=1, use_fm=0, use_deep=0 if a.fwfm else 1,
+            use_lw=1,
             use_fwlw=a.fwlw, numerical=13, use_cuda=True)
 shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
 m.load_state_dict({k: torch.from_numpy(v) for k, v in synth.synth_state(shapes, 39, 10, 400, True, True).items()})
 m = m.to(dev).train() if a.train else m.to(dev).eval()
 m.strict_index_check = False
-xi, xv = synth.synth_inputs(sizes, 13, a.batch, seed=5)
-xi, xv = torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)
+data = []
+for i in range(a.batches):
+    xi, xv = synth.synth_inputs(sizes, 13, a.batch, seed=5 + i)
+    data.append((torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)))
+xi, xv = data[0]
+outs = [torch.empty(a.batch, device=dev) for _ in data]
 if a.train:
     from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
     y = torch.zeros(a.batch, device=dev)
@@ -40,10 +50,13 @@ if a.train:
 else:
     with torch.no_grad():
         for _ in range(a.iters):
-            m(xi, xv)
+            if a.batches > 1:
+                m._sync_engine(dev).forward_batches(data, outs)
+            else:
+                m(xi, xv)
 torch.cuda.synchronize()
 rows = 32 if os.environ.get("DFWFM_R32") == "1" else 16  # DFWFM_R32=1: fwd32_kernel's 32-sample workgroups
-grid = (a.batch + rows - 1) // rows
+grid = a.batches * ((a.batch + rows - 1) // rows)
 buf = (ctypes.c_uint64 * (grid * 16))()
 n = _lib.lib().dfwfm_diag_stamps(m._engine.handle, buf, grid * 16,
                                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
@@ -54,9 +67,24 @@ names = ["stage (params, Xi/Xv)", "gather E + table first order", "shallow (fwlw
          "MLP layer 3", "deep reduce + combine"]
 slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (3, 4), (3, 12), (12, 13), (13, 4), (4, 5),
          (5, 6), (6, 8)]
+rt0, rt1 = st[:, 14], st[:, 15] & ((1 << 48) - 1)
+life = (rt1 - rt0) / 100.0
+span = (rt1.max() - rt0.min()) / 100.0
+ev = np.concatenate([np.stack([rt0, np.ones_like(rt0)], 1), np.stack([rt1, -np.ones_like(rt1)], 1)])
+ev = ev[np.argsort(ev[:, 0], kind="stable")]
+conc = np.cumsum(ev[:, 1])
+dt = np.diff(ev[:, 0])
+mean_conc = float((conc[:-1] * dt).sum() / max(dt.sum(), 1))
+print(f"launch span {span:.1f} us on the 100 MHz clock; workgroup lifetime median {np.median(life):.2f} us "
+      f"(p10 {np.percentile(life, 10):.2f}, p90 {np.percentile(life, 90):.2f}); workgroups resident: mean "
+      f"{mean_conc:.0f}, max {conc.max()}; first 10 % of workgroups start within "
+      f"{(np.percentile(rt0, 10) - rt0.min()) / 100:.1f} us, last end - last start {(rt1.max() - rt0.max()) / 100:.1f} us")
 tot = st[:, 8] - st[:, 0]
 print(f"workgroups {n}; total cycles median {np.median(tot):.0f} (p10 {np.percentile(tot, 10):.0f}, "
       f"p90 {np.percentile(tot, 90):.0f})")
+if a.fwfm:  # no MLP: stage, gather, shallow phases, then the combine (slot 8)
+    names = names[:7] + ["combine after the shallow barrier"]
+    slots = slots[:7] + [(11, 8)]
 for nm, sl in zip(names, slots):
     if sl is None:
         continue

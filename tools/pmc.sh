@@ -13,7 +13,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 -s KILL 150 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 64 --warmup 64 --settle-ms 0 --no-gate --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_${TAG}_$i.log 2>&1
+  timeout -k 10 -s KILL 150 rocprofv3 --pmc $grp -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 64 --warmup 64 --settle-ms 0 --no-gate --no-cpu-baseline --no-per-call ${BENCH_ARGS:-} > gpurun_out/pmc_${TAG}_$i.log 2>&1
   rc=$?
   echo "pass $i [$grp] rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi

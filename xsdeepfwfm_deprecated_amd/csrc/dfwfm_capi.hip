@@ -916,7 +916,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     a.W0 = m->W0;
     a.flags = m->flags | (drop ? kDrop : 0);
     // diagnostics only (backward phase costs): DFWFM_DIAG_BWD ORs in kDiagBwd* bits, results invalid
-    if (const char* db = getenv("DFWFM_DIAG_BWD")) a.flags |= atoi(db) << 10;
+    if (const char* db = getenv("DFWFM_DIAG_BWD")) a.flags |= atoi(db) << 20;
     a.drop_p = m->t_drop;
     a.drop_scale = 1.f / (1.f - m->t_drop);
     a.seed = m->t_seed;

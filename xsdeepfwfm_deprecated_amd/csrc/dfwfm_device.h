@@ -405,6 +405,60 @@ __device__ __forceinline__ void load_tile(float* __restrict__ lds, int lds_strid
   }
 }
 
+// Staged copies (load everything first, store later): stage_load reads items tid + k * nth (k < KPT) of n into
+// registers through get(i); stage_store writes them through put(i, v) and copies any items past KPT * nth
+// directly.  Several arrays' stage_loads issued back to back cost one round trip.
+template <int KPT, class T, class Get>
+__device__ __forceinline__ void stage_load(T (&v)[KPT], int n, int tid, int nth, Get get) {
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = tid + k * nth;
+    v[k] = i < n ? get(i) : T{};
+  }
+}
+template <int KPT, class T, class Get, class Put>
+__device__ __forceinline__ void stage_store(const T (&v)[KPT], int n, int tid, int nth, Get get, Put put) {
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = tid + k * nth;
+    if (i < n) put(i, v[k]);
+  }
+  for (int i = tid + KPT * nth; i < n; i += nth) put(i, get(i));
+}
+
+// load_tile split in two (the same tile, the same zero fill): tile_load issues the loads, tile_store writes LDS
+template <int KPT>
+__device__ __forceinline__ void tile_load(f32x4 (&v)[KPT], const float* __restrict__ g, int64_t gstride, int nrows,
+                                          int cols4, int pad4, int tid, int nth) {
+  const int n = kBM * pad4;
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = tid + k * nth;
+    const int b = i / pad4;
+    const int c = i - b * pad4;
+    v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (i < n && b < nrows && c < cols4) v[k] = reinterpret_cast<const f32x4*>(g + b * gstride)[c];
+  }
+}
+template <int KPT>
+__device__ __forceinline__ void tile_store(float* __restrict__ lds, int lds_stride, const f32x4 (&v)[KPT],
+                                           const float* __restrict__ g, int64_t gstride, int nrows, int cols4,
+                                           int pad4, int tid, int nth) {
+  const int n = kBM * pad4;
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = tid + k * nth;
+    const int b = i / pad4;
+    if (i < n) reinterpret_cast<f32x4*>(lds + b * lds_stride)[i - b * pad4] = v[k];
+  }
+  for (int i = tid + KPT * nth; i < n; i += nth) {  // wider tiles
+    const int b = i / pad4;
+    const int c = i - b * pad4;
+    reinterpret_cast<f32x4*>(lds + b * lds_stride)[c] =
+        (b < nrows && c < cols4) ? reinterpret_cast<const f32x4*>(g + b * gstride)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 // Dropout seed of a step: the host's seed, or -- for graph-replayed steps -- that seed mixed with a
 // device step counter (read at kernel time, so every replay draws fresh masks).
 __device__ __forceinline__ uint32_t step_seed(uint32_t base, const int64_t* src) {

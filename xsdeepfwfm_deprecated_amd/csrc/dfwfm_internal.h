@@ -31,6 +31,9 @@ constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_table
 constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
 constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
+// bwd_kernel diagnostics / A/B (DFWFM_DIAG_BWD=<bits> sets them << 20; off the flag range the model itself uses):
+// no G_l stores (results invalid), no mask loads (results invalid), the generic K loop instead of the static form
+constexpr int kBwdNoGStore = 1 << 20, kBwdNoMask = 1 << 21, kBwdGeneric = 1 << 22;
 constexpr int kMaxH = 16;      // hidden layers
 constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)
 
@@ -323,12 +326,13 @@ struct AdamTensor {
   int64_t n;
 };
 constexpr int kAdamBlock = 4096;  // elements per Adam work unit (16 per thread: four float4 of each array in flight)
-constexpr int kAdamList = 84;    // tensors per Adam launch (the list is a kernel argument, < 4 KiB)
+constexpr int kAdamList = 91;    // tensors per Adam launch (the list is a kernel argument, < 4 KiB)
 struct AdamList {
   AdamTensor t[kAdamList];
   int32_t block0[kAdamList];     // first workgroup of each tensor
   int32_t n;
 };
+static_assert(sizeof(AdamList) + 64 <= 4096, "Adam launch arguments over 4 KiB");
 
 // Raises a kernel's dynamic-LDS limit when a launch needs more than previously granted.  Done once
 // per kernel and size, not per launch, so launches recorded into a HIP graph make no attribute calls.

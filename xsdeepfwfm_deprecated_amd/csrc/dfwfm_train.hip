@@ -23,7 +23,7 @@
 namespace dfwfm {
 
 struct BwdLds {
-  int lw, fwlw, rsk, bufE, bufD, bufA, dl, fc, tailr, fo, xv, total;
+  int lw, fwlw, rsk, bufE, bufD, bufA, dl, fc, tailr, fo, xv, gram, total;
 };
 
 __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX, int SY) {
@@ -40,6 +40,7 @@ __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX
   L.tailr = o; o += 8 * 64 * 4;               // split-tail partial products (eight waves)
   L.fo = o;    o += kBM * r4(F);              // fused reductions: first order per field
   L.xv = o;    o += kBM * r4(F);              //                   numerical values (num <= F)
+  L.gram = o;  o += 2 * MT * MT * 256;          //                   field_cov Gram: both chains of every tile
   L.total = r4(o);
   return L;
 }
@@ -85,35 +86,59 @@ bwd_kernel(BwdArgs p) {
   const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
 
   // ---- P0: stage --------------------------------------------------------------
+  // every global read of the phase is issued before the first LDS store (one round trip instead of one per staging
+  // loop); X_H's reads go out too, but land in LDS (bufA, which P1 leaves alone) only after P1
   stamp(p.stamps, 0, tid);
   stamp_rt(p.stamps, 10, tid);
-  if (lwp)
-    for (int i = tid; i < F; i += NTH) lw_s[i] = p.lw[i];
-  if (fwlw)
-    for (int i = tid; i < FD; i += NTH) fwlw_s[i] = p.fwlw[i];
-  if (second)
-    for (int i = tid; i < p.MT * p.S * 16; i += NTH)
-      reinterpret_cast<float4*>(rsk)[i] = reinterpret_cast<const float4*>(p.rsk)[i];
-  if (tid < kBM) dl[tid] = (b0 + tid < p.batch) ? p.dlogit[b0 + tid] : 0.f;
   const int red = p.red;
   float* fo_s = smem + L.fo;
   float* xv_s = smem + L.xv;
   const int num = p.num, Fp = r4(F);
-  if (red & kRedLw)
-    for (int i = tid; i < kBM * F; i += NTH) {
-      const int b = i / F;
-      fo_s[b * Fp + (i - b * F)] = b < nrows ? p.sv_fo[(b0 + b) * F + (i - b * F)] : 0.f;
-    }
-  if (red)
-    for (int i = tid; i < kBM * num; i += NTH) {
-      const int b = i / num;
-      xv_s[b * Fp + (i - b * num)] = b < nrows ? p.xv[(b0 + b) * p.xv_stride + (i - b * num)] : 0.f;
-    }
+  const int64_t b0f = b0 * F;
+  const float* xvb = p.xv + b0 * p.xv_stride;
+  auto get_lw = [&](int i) { return p.lw[i]; };
+  auto get_fwlw = [&](int i) { return p.fwlw[i]; };
+  auto get_fc = [&](int i) { return p.fc[i]; };
+  auto get_dl = [&](int i) { return b0 + i < p.batch ? p.dlogit[b0 + i] : 0.f; };
+  auto get_fo = [&](int i) {
+    const int b = i / F;
+    return b < nrows ? p.sv_fo[b0f + i] : 0.f;
+  };
+  auto get_xv = [&](int i) {
+    const int b = i / num;
+    return b < nrows ? xvb[b * p.xv_stride + (i - b * num)] : 0.f;
+  };
+  auto get_rsk = [&](int i) { return reinterpret_cast<const f32x4*>(p.rsk)[i]; };
+  const int n_lw = lwp ? F : 0, n_fwlw = fwlw ? FD : 0, n_rsk = second ? p.MT * p.S * 16 : 0;
+  const int n_fo = (red & kRedLw) ? kBM * F : 0, n_xv = red ? kBM * num : 0, n_fc = deep ? p.NT * 16 : 0;
+  float v_lw[1], v_fwlw[1], v_fc[1], v_dl[1], v_fo[2], v_xv[1];
+  f32x4 v_rsk[1], v_e[4], v_x[4];
+  stage_load<1>(v_lw, n_lw, tid, NTH, get_lw);
+  stage_load<1>(v_fwlw, n_fwlw, tid, NTH, get_fwlw);
+  stage_load<1>(v_rsk, n_rsk, tid, NTH, get_rsk);
+  stage_load<1>(v_dl, kBM, tid, NTH, get_dl);
+  stage_load<2>(v_fo, n_fo, tid, NTH, get_fo);
+  stage_load<1>(v_xv, n_xv, tid, NTH, get_xv);
+  stage_load<1>(v_fc, n_fc, tid, NTH, get_fc);
+  // the E tile: rows of r4(F*D) floats (zero past F*D), zero-padded to W0 columns; X_H: N columns padded to NT*16
+  const float* xh_g = deep ? p.sv_x[p.H] + b0 * p.N : nullptr;
+  tile_load<4>(v_e, p.sv_e + b0 * r4(FD), r4(FD), second ? nrows : 0, r4(FD) / 4, p.W0 / 4, tid, NTH);
+  if (deep) tile_load<4>(v_x, xh_g, p.N, nrows, p.N / 4, p.NT * 4, tid, NTH);
+  stage_store<1>(v_lw, n_lw, tid, NTH, get_lw, [&](int i, float v) { lw_s[i] = v; });
+  stage_store<1>(v_fwlw, n_fwlw, tid, NTH, get_fwlw, [&](int i, float v) { fwlw_s[i] = v; });
+  stage_store<1>(v_rsk, n_rsk, tid, NTH, get_rsk, [&](int i, f32x4 v) { reinterpret_cast<f32x4*>(rsk)[i] = v; });
+  stage_store<1>(v_dl, kBM, tid, NTH, get_dl, [&](int i, float v) { dl[i] = v; });
+  stage_store<2>(v_fo, n_fo, tid, NTH, get_fo, [&](int i, float v) {
+    const int b = i / F;
+    fo_s[b * Fp + (i - b * F)] = v;
+  });
+  stage_store<1>(v_xv, n_xv, tid, NTH, get_xv, [&](int i, float v) {
+    const int b = i / num;
+    xv_s[b * Fp + (i - b * num)] = v;
+  });
+  stage_store<1>(v_fc, n_fc, tid, NTH, get_fc, [&](int i, float v) { fc_s[i] = v; });
+  tile_store<4>(bufE, SX, v_e, p.sv_e + b0 * r4(FD), r4(FD), second ? nrows : 0, r4(FD) / 4, p.W0 / 4, tid, NTH);
   float* rout = p.part + (size_t)blockIdx.x * red_outputs(F, D, p.N, num);  // fused reductions' partials
-  if (deep)
-    for (int i = tid; i < p.NT * 16; i += NTH) fc_s[i] = p.fc[i];
-  // the E tile: rows of r4(F*D) floats (zero past F*D), zero-padded to W0 columns
-  load_tile<7>(bufE, SX, p.sv_e + b0 * r4(FD), r4(FD), second ? nrows : 0, r4(FD) / 4, p.W0 / 4, tid, NTH);
   for (int i = tid; i < kBM * (p.W0 / 4); i += NTH) {
     const int b = i / (p.W0 / 4);
     reinterpret_cast<f32x4*>(bufD + b * SX)[i - b * (p.W0 / 4)] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -121,26 +146,81 @@ bwd_kernel(BwdArgs p) {
   __syncthreads();
   stamp(p.stamps, 1, tid);
 
-  // ---- P1: dE of the shallow part ---------------------------------------------
-  if (second) {
-    // dE[b,k,d] = dlogit_b * sum_{l != k} Rs[k,l] E[b,l,d]  (+ dfo[b,k] * Wfl[k,d] with fwlw, :344-345)
+  // ---- P1: dE of the shallow part and the field_cov Gram ---------------------------------
+  // The work is dealt to the waves by cost, and every operand of a chain (or of a group of four steps) is read from
+  // LDS before its MFMAs, with the wave-uniform decoding done once per chain:
+  //  * field_cov's Gram (fused reduction): chain h of tile (mk, ml) takes the steps 4g + 2i + h (g < D, i < 2) --
+  //    reduce_kernel's two accumulators -- i.e. (b, d) = divmod(16g + 8i + 4h + (lane >> 4), D): 2D MFMAs; the
+  //    chains' sums go to LDS and are added after the barrier.  Chains round-robin from wave 0.
+  //  * the FwFM dE pieces (m, nt): S dependent MFMAs each, round-robin from the last wave.
+  {
     const int MT = p.MT, S = p.S;
-    constexpr int NTW = (D + NW - 1) / NW;
-    for (int m = 0; m < MT; ++m) {
+    if (red & kRedR) {
+      float* gram = smem + L.gram;
+      // a wave's chains all have its parity h = wave & 1 (c = wave + NW k), so the (b, d) of every step -- its LDS
+      // offset b SX + d and its dlogit -- are the same for all of them: formed once
+      const int hq = 4 * (wave & 1) + (lane >> 4);
+      int off[2 * D];
+      float dlj[2 * D];
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        const int nt = wave + NW * j;
-        if (nt >= D) continue;  // wave-uniform
+      for (int j = 0; j < 2 * D; ++j) {
+        const int nn = 16 * (j >> 1) + 8 * (j & 1) + hq;
+        const int b = nn / D;
+        off[j] = b * SX + (nn - b * D);
+        dlj[j] = dl[b];
+      }
+      for (int c = wave; c < 2 * MT * MT; c += NW) {
+        const int t = c >> 1;
+        const int mk = t / MT, ml = t - mk * MT;
+        const int kA = 16 * mk + (lane & 15), lB = 16 * ml + (lane & 15);
+        const bool va = kA < F, vb = lB < F;
+        const float* ea = bufE + (va ? kA : 0) * D;
+        const float* eb = bufE + (vb ? lB : 0) * D;
+        float av[2 * D], bv[2 * D];
+#pragma unroll
+        for (int j = 0; j < 2 * D; ++j) {
+          const float x = ea[off[j]];
+          av[j] = va ? dlj[j] * x : 0.f;
+          bv[j] = vb ? eb[off[j]] : 0.f;
+        }
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 2 * D; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+        reinterpret_cast<f32x4*>(gram)[c * 64 + lane] = acc;
+      }
+    }
+    stamp(p.stamps, 12, tid);
+    if (second) {
+      // dE[b,k,d] = dlogit_b * sum_{l != k} Rs[k,l] E[b,l,d]  (+ dfo[b,k] * Wfl[k,d] with fwlw, :344-345)
+      for (int it = NW - 1 - wave; it < MT * D; it += NW) {
+        const int m = it / D, nt = it - m * D;
         const int n = nt * 16 + (lane & 15);
         const int b = n / D;
         const int d = n - b * D;
-        const float* ecol = bufE + b * SX + d;
+        const float* ecol = bufE + b * SX + d + (lane >> 4) * D;  // + 4 s D at step s
+        const float* ua = rsk + m * S * 64 + lane;                 // + 64 s
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < S; ++s) {
-          const float av = rsk[(m * S + s) * 64 + lane];
-          const float bv = ecol[(4 * s + (lane >> 4)) * D];
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+        auto group = [&](int s0, auto U_) {
+          constexpr int U = decltype(U_)::value;
+          float av[U], bv[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            av[u] = ua[(s0 + u) * 64];
+            bv[u] = ecol[(s0 + u) * 4 * D];
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+        };
+        int s0 = 0;
+        for (; s0 + 8 <= S; s0 += 8) group(s0, std::integral_constant<int, 8>{});
+        const int rem = S - s0;
+        if (rem >= 4) {
+          group(s0, std::integral_constant<int, 4>{});
+          s0 += 4;
         }
+        if (S - s0 == 3) group(s0, std::integral_constant<int, 3>{});
+        else if (S - s0 == 2) group(s0, std::integral_constant<int, 2>{});
+        else if (S - s0 == 1) group(s0, std::integral_constant<int, 1>{});
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int k = 16 * m + row0 + r;
@@ -153,12 +233,12 @@ bwd_kernel(BwdArgs p) {
       }
     }
   }
-  // ---- R: the dense shallow reductions over this tile (reduce_kernel's arithmetic, same order), from the
-  // E tile still in LDS: bias, fm_1st, fwfm_linear, the numerical fields' first order, field_cov's Gram
+  stamp(p.stamps, 13, tid);
+  // ---- R: the other dense shallow reductions over this tile (reduce_kernel's arithmetic, same order), from the
+  // tiles in LDS: bias, fm_1st, fwfm_linear, the numerical fields' first order
   if (red) {
     float* o_lw = rout + 1;
     float* o_fw = o_lw + F;
-    float* o_R = o_fw + FD;
     if (tid < kBM) {
       const float v = sum16(dl[tid]);
       if (tid == 0) rout[0] = v;
@@ -184,51 +264,26 @@ bwd_kernel(BwdArgs p) {
       float* o_n1 = o_fw + FD + F * F + p.N + num * D;
       o_n1[tid] = sn;
     }
+  }
+  __syncthreads();
+  if (red) {
+    // field_cov: d W[k,l] = 0.5 * sum_b dlogit_b <E_bk, E_bl>, k != l (:363-367) from the two chains of each tile
+    float* o_R = rout + 1 + F + FD;
     if (red & kRedR) {
-      // d W[k,l] = 0.5 * sum_b dlogit_b <E_bk, E_bl>, k != l (:363-367): Gram on MFMA over (b, d)
-      const int MT = p.MT, ntile = MT * MT;
-      constexpr int steps = (kBM * D) / 4;
-      for (int t = wave; t < ntile; t += NW) {
+      const int MT = p.MT;
+      const float* gram = smem + L.gram;
+      for (int e = tid; e < MT * MT * 256; e += NTH) {
+        const int t = e >> 8, ln = (e >> 2) & 63, r = e & 3;
         const int mk = t / MT, ml = t - mk * MT;
-        const int kA = 16 * mk + (lane & 15);
-        const int lB = 16 * ml + (lane & 15);
-        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-        int st = 0;
-        for (; st + 4 <= steps; st += 4) {
-          float av[4], bv[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int n = 4 * (st + u) + (lane >> 4);
-            const int b = n / D;
-            const int d = n - b * D;
-            av[u] = kA < F ? dl[b] * bufE[b * SX + kA * D + d] : 0.f;
-            bv[u] = lB < F ? bufE[b * SX + lB * D + d] : 0.f;
-          }
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc1, 0, 0, 0);
-        }
-        for (; st < steps; ++st) {
-          const int n = 4 * st + (lane >> 4);
-          const int b = n / D;
-          const int d = n - b * D;
-          const float av = kA < F ? dl[b] * bufE[b * SX + kA * D + d] : 0.f;
-          const float bv = lB < F ? bufE[b * SX + lB * D + d] : 0.f;
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
-        }
-        const f32x4 acc = acc0 + acc1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * mk + (lane >> 4) * 4 + r;
-          if (k < F && lB < F) o_R[k * F + lB] = k != lB ? 0.5f * acc[r] : 0.f;
-        }
+        const int k = 16 * mk + (ln >> 4) * 4 + r, lB = 16 * ml + (ln & 15);
+        if (k < F && lB < F) o_R[k * F + lB] = k != lB ? 0.5f * (gram[(2 * t) * 256 + 4 * ln + r] +
+                                                                 gram[(2 * t + 1) * 256 + 4 * ln + r])
+                                                       : 0.f;
       }
     } else {
       for (int i = tid; i < F * F; i += NTH) o_R[i] = 0.f;
     }
   }
-  __syncthreads();
   stamp(p.stamps, 2, tid);
 
   // ---- P2: MLP backward (net_1_fc then net_1_linear_H .. 1, :412-428) ---------------
@@ -236,9 +291,9 @@ bwd_kernel(BwdArgs p) {
     const int H = p.H, N = p.N, NT = p.NT, NP = NT * 16;
     const float scale = drop ? p.drop_scale : 1.f;
     const uint32_t dseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
-    // G_H = dlogit * fc * (X_H > 0) * scale -> bufA (X_H staged there first; stored to the workspace
-    // at the top of layer H, behind its weight preload)
-    load_tile<7>(bufA, SY, p.sv_x[H] + b0 * N, N, nrows, N / 4, NP / 4, tid, NTH);
+    // G_H = dlogit * fc * (X_H > 0) * scale -> bufA (X_H read in P0, written to LDS now; G_H is stored to the
+    // workspace at the top of layer H, behind its weight preload)
+    tile_store<4>(bufA, SY, v_x, xh_g, p.N, nrows, p.N / 4, p.NT * 4, tid, NTH);
     __syncthreads();
     // column n per thread: the fused net_1_fc reduction (sum_b dlogit_b X_H[b, n], reduce_kernel's order)
     // reads the column before it is overwritten with G_H
@@ -263,6 +318,41 @@ bwd_kernel(BwdArgs p) {
     TailStream<NG> ts;
     f32x4 tw[TailStream<NG>::C];
     const int g = wave;
+    // the static form (Criteo's 400-wide layers: 25 chunks, 24 + 1 split tiles per layer, like the forward's
+    // NS = 25 loop): the split tile's share rides on the K loop's register sets (no tail loads and MMA exposed
+    // before the loop), and each layer's first chunks go out before the previous layer's barrier
+    constexpr bool kStatForm = NG == 8 && TPW == 3;
+    const bool stat = kStatForm && NT == 25 && p.NC0 == 25 && NT <= NG * TailStream<NG>::C &&
+                      !(flags & kBwdGeneric);
+    // the epilogue's ReLU / dropout mask sources X_{l-1} for this lane's outputs of the layer's first pass (tile
+    // t0 + g + NG j, rows row0 + r) and of the split tile (row row0 + (g & 3)), loaded behind the layer's preload
+    // and the G_l stores (measured: loaded ahead, before the preload, or from LDS bytes prefetched in P0, the
+    // kernel was 4-14k cycles slower, profiles/r04/r04k_bwdstamps.log, r04l_bwdstamps.log)
+    auto load_masks = [&](int l, int t0, float (&xm)[TPW][4], float& xt) {
+      const int K = l == 1 ? FD : N;
+      const int KT = l == 1 ? p.NC0 : NT;
+      const bool ltail = NG == 8 && KT == NG * TPW + 1 && NT <= NG * TailStream<NG>::C;
+      const int KTm = ltail ? KT - 1 : KT;
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int t = t0 + g + NG * j;
+        const int k = t * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = b0 + row0 + r;
+          xm[j][r] = (l > 1 && t < KTm && k < K && row < p.batch)
+                         ? ((flags & kBwdNoMask) ? 1.f : p.sv_x[l - 1][row * N + k]) : 0.f;
+        }
+      }
+      const int k = (KT - 1) * 16 + (lane & 15);
+      const int64_t row = b0 + row0 + (g & 3);
+      xt = (ltail && t0 == 0 && l > 1 && g < 4 && k < K && row < p.batch)
+               ? ((flags & kBwdNoMask) ? 1.f : p.sv_x[l - 1][row * N + k]) : 0.f;
+    };
+    if (stat) {
+      ls.init(wrsrc, p.wt_off[H], NT, NT - 1, g, 0);
+      ls.preload(wb0, wb1, lane * 16);
+    }
     for (int l = H; l >= 1; --l) {
       const bool fromA = ((H - l) & 1) == 0;
       const float* in = fromA ? bufA : bufB;
@@ -277,36 +367,40 @@ bwd_kernel(BwdArgs p) {
       // output tiles (the layer's inputs k) in passes of NG*TPW: layer 1 may have more tiles
       // (ceil(F*D/16)) than the hidden width the kernel's TPW was sized for
       for (int t0 = 0; t0 < KTm; t0 += NG * TPW) {
-        ls.init(wrsrc, p.wt_off[l] + t0 * NT * 64, NT, KTm - t0, g, 0);
-        ls.preload(wb0, wb1, lane * 16);
-        if (ltail && t0 == 0) {
-          ts.init(p.wt_off[l], NT, T, g);
-          ts.load(wrsrc, tw, lane * 16);
-        }
-        // G_l (this layer's input tile) -> workspace for the weight-gradient GEMM: coalesced rows
-        // from LDS, behind the preload (stores count in vmcnt too)
-        if (t0 == 0 && !(flags & (1 << 10))) store_tile(p.sv_g[l] + b0 * N, N, in, SY, nrows, N / 4, tid, NTH);
-        // epilogue operands: the ReLU/dropout mask source X_{l-1} for this lane's outputs
-        float xm[TPW][4];
-#pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-          const int t = t0 + g + NG * j;
-          const int k = t * 16 + (lane & 15);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int64_t row = b0 + row0 + r;
-            xm[j][r] = (l > 1 && t < KTm && k < K && row < p.batch) ? ((flags & (1 << 11)) ? 1.f : p.sv_x[l - 1][row * N + k]) : 0.f;
+        if (!stat) {
+          ls.init(wrsrc, p.wt_off[l] + t0 * NT * 64, NT, KTm - t0, g, 0);
+          ls.preload(wb0, wb1, lane * 16);
+          if (ltail && t0 == 0) {
+            ts.init(p.wt_off[l], NT, T, g);
+            ts.load(wrsrc, tw, lane * 16);
           }
         }
-        if (ltail && t0 == 0) {
-          const int k = T * 16 + (lane & 15);
-          const int64_t row = b0 + row0 + (g & 3);
-          xt = (l > 1 && g < 4 && k < K && row < p.batch) ? p.sv_x[l - 1][row * N + k] : 0.f;
-          // the tail's share first: its fragments are then dead during the K loop
-          reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.mma(in, SY, tw, lane);
+        // G_l (this layer's input tile) -> workspace for the weight-gradient GEMM: coalesced rows from LDS, behind
+        // the preload (stores count in vmcnt too)
+        if (t0 == 0 && !(flags & kBwdNoGStore)) store_tile(p.sv_g[l] + b0 * N, N, in, SY, nrows, N / 4, tid, NTH);
+        float xm[TPW][4];
+        {
+          float xt0;
+          load_masks(l, t0, xm, xt0);
+          if (ltail && t0 == 0) xt = xt0;
         }
+        // the tail's share first (generic form): its fragments are then dead during the K loop
+        if (ltail && t0 == 0 && !stat) reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = ts.mma(in, SY, tw, lane);
         f32x4 acc[TPW];
-        mlp_k_loop<TPW, 1, NG>(acc, in, SY, ls, wb0, wb1, wb2, lane);
+        if constexpr (kStatForm) {
+          if (stat) {
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            ts.init(p.wt_off[l], NT, T, g);
+            f32x4 tp;
+            mlp_k_loop_s<TPW, NG, 25, false>(acc, in, SY, ls, wb0, wb1, wb2, lane, ts, tp);
+            reinterpret_cast<f32x4*>(tailr)[g * 64 + lane] = tp;
+          } else {
+            mlp_k_loop<TPW, 1, NG>(acc, in, SY, ls, wb0, wb1, wb2, lane);
+          }
+        } else {
+          mlp_k_loop<TPW, 1, NG>(acc, in, SY, ls, wb0, wb1, wb2, lane);
+        }
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
           const int t = t0 + g + NG * j;
@@ -324,6 +418,12 @@ bwd_kernel(BwdArgs p) {
               bufD[b * SX + k] += gv;
             }
           }
+        }
+        // the next layer's first chunks, ahead of the barrier (after the epilogue: any wait on a vector-memory
+        // result after them would wait for them too)
+        if (stat && l > 1) {
+          ls.init(wrsrc, p.wt_off[l - 1], NT, NT - 1, g, 0);
+          ls.preload(wb0, wb1, lane * 16);
         }
       }
       __syncthreads();

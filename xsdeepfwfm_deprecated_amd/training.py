@@ -199,10 +199,16 @@ class FusedTrainStep:
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
         self.state = torch.zeros(_lib.ADAM_STATE_BYTES // 8, dtype=torch.int64, device=dev)
-        # Adam runs as two launches -- everything but the MLP (state), the MLP weights and biases
-        # (state_b) -- so that the first can overlap the weight-gradient GEMM; each state's step counter is
-        # bumped once per step, so both hold the same step and bias corrections
+        # under data parallelism and in the forked layouts Adam runs as two launches -- everything but the MLP
+        # (state), the MLP weights and biases (state_b) -- so that the first can overlap the weight-gradient GEMM;
+        # each state's step counter is bumped once per step, so both hold the same step and bias corrections.  The
+        # one-stream step (default on one process) runs one launch over every tensor on `state`
         self.state_b = torch.zeros_like(self.state)
+        # one process: the step's graph layout (A/B only, read once per instance): none = one stream, the whole
+        # Adam as one launch (default); reduce / spread / tiles = the graph forks after the backward's reductions /
+        # after the scatter / right after the per-tile backward, the weight-gradient GEMM and the MLP's Adam on a
+        # side stream
+        self.fork = os.environ.get("DFWFM_TRAIN_FORK", "none")
         views = {}
         adam = (_lib.dfwfm_adam_tensor * len(params))()
         for i, p in enumerate(params):
@@ -387,8 +393,18 @@ class FusedTrainStep:
                        "dfwfm_adam_step_dev")
 
     def _part2(self):
+        if self.dist is None and self.fork == "none":
+            self._adam_all()  # one counter (`state`) for every step of this instance, graph-replayed or not
+            return
         self._adam_main()
         self._adam_mlp()
+
+    def _adam_all(self):
+        """Every tensor's Adam in one launch (one step counter, `state`): the one-stream step."""
+        b1, b2 = self.betas
+        _lib.check(self.L.dfwfm_adam_step_dev(self.adam, self.n_adam, self.lr, b1, b2, self.eps, self.wd,
+                                              ctypes.c_void_p(self.state.data_ptr()), self._stream()),
+                   "dfwfm_adam_step_dev")
 
     def _exchange(self, run_part1b, run_apply=None):
         """Data parallelism: all-reduce the gradient buffer (RCCL).  Bucketed: the first bucket (every
@@ -469,15 +485,13 @@ class FusedTrainStep:
         g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         ga = None
         if self.dist is None and self.n_adam > self.n_main:
-            # one process: a single graph that forks after the per-tile backward -- the weight-gradient GEMM
-            # and the MLP's Adam on a side stream; the reductions, the table scatter and the other tensors' Adam
-            # (the 58 MB of tables) beside them
-            # (A/B only, DFWFM_TRAIN_FORK: spread = fork after the scatter, none = one stream, tiles = fork right after
-            # the per-tile backward with the reductions' final sums beside the GEMM)
-            # default (reduce): the reductions' final sums (39 small workgroups) run BEFORE the fork -- launched
-            # beside the weight-gradient GEMM they waited for its 225 workgroups to leave the CUs and took 38 us
-            # instead of ~6, holding the scatter and the main Adam behind them (profiles/r04/r04c_proftrain)
-            fork = os.environ.get("DFWFM_TRAIN_FORK", "reduce")
+            # one process, default: ONE stream -- fill, re-pack, forward, loss gradient, backward, reductions,
+            # scatter, weight-gradient GEMM, one Adam launch.  The forked layouts (the GEMM and the MLP's Adam on a
+            # side stream beside the reductions / scatter / main Adam) measured level with it (0.302-0.307 ms,
+            # profiles/r04/r04h_tr-*.log) at 160-230 us of host enqueue per step against 17-29 us: with the
+            # GEMM's 225 workgroups resident, whatever ran beside it (reductions, scatter, Adam) was starved of CU
+            # slots and stretched by about what the overlap saved
+            fork = self.fork
             if fork == "none":
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g1, stream=s):
