@@ -256,6 +256,14 @@ int dfwfm_adam_step_dev(const dfwfm_adam_tensor* tensors, int32_t n, double lr, 
 int dfwfm_bce_grad(const float* logits, const float* labels, int64_t n, double denom, float* dlogit,
                    float* loss_sum, void* stream);
 
+/* dfwfm_bce_grad fused into dfwfm_backward_phases: the per-tile backward (phases must include
+ * DFWFM_BWD_TILES or DFWFM_BWD_TABLES) forms dlogit from the training forward's logits and the labels with
+ * dfwfm_bce_grad's arithmetic (the same dlogit bits), writes it to `dlogit` for the later phases and adds the
+ * per-sample losses to *loss_sum (when non-NULL); one launch fewer per step.  A model without embeddings (no
+ * per-tile backward) runs dfwfm_bce_grad then dfwfm_backward_phases. */
+int dfwfm_backward_phases_bce(dfwfm_model* m, const float* logits, const float* labels, double denom, float* dlogit,
+                              float* loss_sum, const dfwfm_grads* grads, int32_t phases, void* stream);
+
 /* ---- touched-row gradients of the categorical tables (data-parallel exchange) --------------------
  * The reference's tables have dense gradients (nn.Embedding(sparse=False), model/DeepFMs.py:199-210) and
  * its Adam applies coupled L2 to every row (:553-556), so the data-parallel form of its step all-reduces

@@ -526,9 +526,10 @@ def _sparse_setup(m, gpu):
     return fields, dense, views, flat, _lib, ctypes
 
 
-def _sparse_step(m, gpu, xi, xv, y, sparse, split=False):
+def _sparse_step(m, gpu, xi, xv, y, sparse, split=False, bce_fused=False, extras=None):
     """One backward of m on (xi, xv, y) with the dense scatter (sparse=False; the touched-row lists are
-    _local_lists_step's).  Returns {param name: grad}, [] and the logits."""
+    _local_lists_step's).  Returns {param name: grad}, [] and the logits; bce_fused: the loss gradient formed inside
+    the per-tile backward (dfwfm_backward_phases_bce); extras (a dict) receives dlogit and the loss sum."""
     fields, dense, views, flat, _lib, ctypes = _sparse_setup(m, gpu)
     L, eng = _lib.lib(), m._sync_engine(gpu)
     st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
@@ -536,8 +537,11 @@ def _sparse_step(m, gpu, xi, xv, y, sparse, split=False):
     out = torch.empty(len(xi), device=gpu)
     eng.train_forward(xi_d, xv_d, out, 0.0, 0)
     dl = torch.empty(len(xi), device=gpu)
-    _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(y_d.data_ptr()), len(xi),
-                                float(len(xi)), ctypes.c_void_p(dl.data_ptr()), None, st), "bce")
+    loss = torch.zeros(1, device=gpu)
+    if not bce_fused:
+        _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(y_d.data_ptr()), len(xi),
+                                    float(len(xi)), ctypes.c_void_p(dl.data_ptr()), ctypes.c_void_p(loss.data_ptr()),
+                                    st), "bce")
     ptr = lambda t, f: None if (t is None or (sparse and f >= m.num)) else views[id(t)][1].data_ptr()  # noqa
     fg = (_lib.dfwfm_field_grads * len(fields))(*[_lib.dfwfm_field_grads(*[ptr(t, f) for t in tup])
                                                   for f, tup in enumerate(fields)])
@@ -556,8 +560,18 @@ def _sparse_step(m, gpu, xi, xv, y, sparse, split=False):
         ph(_lib.BWD_MLP_WEIGHTS, ctypes.c_void_p(side.cuda_stream))
         ph(_lib.BWD_SPREAD, st)
         torch.cuda.current_stream(gpu).wait_stream(side)
+    elif bce_fused:
+        _lib.check(L.dfwfm_backward_phases_bce(eng.handle, ctypes.c_void_p(out.data_ptr()),
+                                               ctypes.c_void_p(y_d.data_ptr()), float(len(xi)),
+                                               ctypes.c_void_p(dl.data_ptr()), ctypes.c_void_p(loss.data_ptr()),
+                                               ctypes.byref(grads), _lib.BWD_TABLES | _lib.BWD_MLP_WEIGHTS, st),
+                   "bwd bce")
     else:
         _lib.check(L.dfwfm_backward(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), st), "bwd")
+    if extras is not None:
+        torch.cuda.synchronize()
+        extras["dlogit"] = dl.cpu().numpy()
+        extras["loss"] = float(loss.item())
     lists = []
     torch.cuda.synchronize()
     names = {id(p): k for k, p in m.named_parameters()}
@@ -893,6 +907,23 @@ def test_local_row_lists_equal_dense_table_grads(gpu, name):
             d = od[:n].cpu().numpy()
             assert n > 0 and len(np.unique(d)) == n
             assert n <= len(xi) * ncat * 2
+
+
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult", "train_deepfwfm_fwlw", "train_fwfm_nolw"])
+def test_backward_with_fused_bce_equals_separate(gpu, name):
+    """dfwfm_backward_phases_bce (the loss gradient formed in the per-tile backward's staging) against
+    dfwfm_bce_grad + dfwfm_backward: the same dlogit bits, the same gradients, the loss sum to f32 rounding."""
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    e0, e1 = {}, {}
+    g0, _, o0 = _sparse_step(m, gpu, xi, xv, y, sparse=False, extras=e0)
+    g1, _, o1 = _sparse_step(m, gpu, xi, xv, y, sparse=False, bce_fused=True, extras=e1)
+    assert np.array_equal(o0, o1)
+    assert np.array_equal(e0["dlogit"], e1["dlogit"])
+    assert abs(e0["loss"] - e1["loss"]) <= 1e-5 * max(1.0, abs(e0["loss"]))
+    for k in g0:
+        sc = np.abs(g0[k]).max()
+        assert np.abs(g1[k] - g0[k]).max() <= G_TOL * sc + 1e-12, k
 
 
 @pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult", "train_fwfm_nolw"])

@@ -128,6 +128,8 @@ SIGNATURES = {
                                            ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                            _P, _P]),
     "dfwfm_bce_grad": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_double, _P, _P, _P]),
+    "dfwfm_backward_phases_bce": (ctypes.c_int, [_P, _P, _P, ctypes.c_double, _P, _P, ctypes.POINTER(dfwfm_grads),
+                                                 ctypes.c_int32, _P]),
     "dfwfm_sparse_grads_size": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
                                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]),
     "dfwfm_sparse_grads_apply": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, _P, ctypes.c_int64, _P]),

@@ -864,7 +864,15 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   return DFWFM_OK;
 }
 
-static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, int phases, void* stream) {
+struct BceFuse {
+  const float* z;
+  const float* y;
+  float* loss_sum;
+  float denom;
+};
+
+static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, int phases, void* stream,
+                         const BceFuse* bce = nullptr) {
   if (!m || !g) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
   if (phases & ~(DFWFM_BWD_TABLES | DFWFM_BWD_MLP_WEIGHTS | DFWFM_BWD_TILES | DFWFM_BWD_SPREAD | DFWFM_BWD_REDUCE |
                  DFWFM_BWD_SCATTER))
@@ -891,6 +899,13 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     memset(&a, 0, sizeof a);
     a.batch = batch;
     a.dlogit = dlogit;
+    if (bce) {
+      a.bce_z = bce->z;
+      a.bce_y = bce->y;
+      a.bce_dl = const_cast<float*>(dlogit);
+      a.loss_sum = bce->loss_sum;
+      a.bce_denom = bce->denom;
+    }
     a.sv_e = m->sv_e;
     for (int h = 0; h <= H; ++h) {
       a.sv_x[h] = m->sv_x[h];
@@ -949,9 +964,11 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     m->bwd_fused_red = fused_red;
   }
 
-  // 2. dense shallow reductions: per 16-row tile, then summed over tiles
+  // 2. dense shallow reductions: per 16-row tile, then summed over tiles.  When this call also runs the
+  // weight-gradient GEMM, the final sums ride in its launch (launch_dw_reduce; DFWFM_NO_DW_RED=1: separate, A/B)
+  RedArgs r;
+  bool red_pending = false;
   if (phases & DFWFM_BWD_REDUCE) {
-    RedArgs r;
     memset(&r, 0, sizeof r);
     r.batch = batch;
     r.part = m->red_part;
@@ -978,8 +995,12 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     r.N = m->N;
     r.MT = m->MT;
     r.flags = m->flags;
-    e = fused_red ? launch_reduce_final(r, s) : launch_reduce(r, s);
-    if (e != hipSuccess) return hip_fail(e, "reduce launch");
+    red_pending = fused_red && (phases & DFWFM_BWD_MLP_WEIGHTS) && H > 0 && (g->lin_w || g->lin_b) &&
+                  !getenv("DFWFM_NO_DW_RED");
+    if (!red_pending) {
+      e = fused_red ? launch_reduce_final(r, s) : launch_reduce(r, s);
+      if (e != hipSuccess) return hip_fail(e, "reduce launch");
+    }
   }
 
   // 3. categorical tables: privatised (LDS) tasks for small tables, atomic tasks for large ones
@@ -1104,9 +1125,14 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       d.rows_per_split = rows;
       d.blk0[1] = 0;
       for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
-      e = launch_dw(d, d.blk0[H + 1], s);
+      e = red_pending ? launch_dw_reduce(d, d.blk0[H + 1], r, s) : launch_dw(d, d.blk0[H + 1], s);
       if (e != hipSuccess) return hip_fail(e, "dw launch");
+      red_pending = false;
     }
+  }
+  if (red_pending) {
+    e = launch_reduce_final(r, s);
+    if (e != hipSuccess) return hip_fail(e, "reduce launch");
   }
   return DFWFM_OK;
 }
@@ -1117,6 +1143,24 @@ int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, vo
 
 int dfwfm_backward_phases(dfwfm_model* m, const float* dlogit, const dfwfm_grads* g, int32_t phases, void* stream) {
   return backward_impl(m, dlogit, g, phases, stream);
+}
+
+int dfwfm_backward_phases_bce(dfwfm_model* m, const float* z, const float* y, double denom, float* dlogit,
+                              float* loss_sum, const dfwfm_grads* g, int32_t phases, void* stream) {
+  if (!m || !g) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  if (!(denom > 0.0)) return fail(DFWFM_ERR_INVALID_ARG, "denom must be > 0");
+  if (!m->trained) return fail(DFWFM_ERR_STATE, "dfwfm_backward needs a preceding dfwfm_train_forward");
+  const int64_t n = m->t_batch;
+  if (n > 0 && (!z || !y || !dlogit)) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  const bool tiles = (phases & (DFWFM_BWD_TABLES | DFWFM_BWD_TILES)) != 0;
+  if (!tiles || !(m->flags & kNeedE) || n == 0) {
+    // no per-tile backward to carry it: the separate gradient launch
+    hipError_t e = launch_bce_grad(z, y, n, (float)denom, dlogit, loss_sum, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "bce launch");
+    return backward_impl(m, dlogit, g, phases, stream);
+  }
+  const BceFuse b{z, y, loss_sum, (float)denom};
+  return backward_impl(m, dlogit, g, phases, stream, &b);
 }
 
 int dfwfm_adam_step(const dfwfm_adam_tensor* t, int32_t n, double lr, double beta1, double beta2, double eps,

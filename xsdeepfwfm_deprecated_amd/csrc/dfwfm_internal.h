@@ -150,7 +150,14 @@ __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int
 // reductions and the table scatter.
 struct BwdArgs {
   int64_t batch;
-  const float* dlogit;           // [B] dL/dlogit
+  const float* dlogit;           // [B] dL/dlogit (read unless bce_z is set)
+  // BCE fused in (dfwfm_backward_phases_bce): dlogit formed from the logits bce_z and labels bce_y as
+  // bce_grad_kernel does, written to bce_dl, the per-sample losses added to *loss_sum (when non-null)
+  const float* bce_z;
+  const float* bce_y;
+  float* bce_dl;
+  float* loss_sum;
+  float bce_denom;
   const float* sv_e;             // [B][F*D]
   const float* sv_x[kMaxH + 1];  // X_0 .. X_H
   float* sv_g[kMaxH + 1];        // G_1 .. G_H written here ([B][N], dL/dz of each layer)
@@ -416,6 +423,8 @@ hipError_t launch_backward(const BwdArgs& a, int D, int tpw, int ng, size_t lds,
 size_t backward_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
 // the register-direct dwr_kernel: 80 x 80 blocks (nnb, nkb), batch splits of a multiple of kDwRows rows
 hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s);
+// launch_dw with reduce_final's workgroups appended to the same grid (one launch for both)
+hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r, hipStream_t s);
 constexpr int kDwEdge = 80;
 constexpr int kDwRows = 64;  // four waves x whole groups of four four-row k-steps
 hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages

@@ -99,7 +99,9 @@ bwd_kernel(BwdArgs p) {
   auto get_lw = [&](int i) { return p.lw[i]; };
   auto get_fwlw = [&](int i) { return p.fwlw[i]; };
   auto get_fc = [&](int i) { return p.fc[i]; };
-  auto get_dl = [&](int i) { return b0 + i < p.batch ? p.dlogit[b0 + i] : 0.f; };
+  const bool bce = p.bce_z != nullptr;
+  auto get_dl = [&](int i) { return b0 + i < p.batch ? (bce ? p.bce_z : p.dlogit)[b0 + i] : 0.f; };
+  auto get_y = [&](int i) { return b0 + i < p.batch ? p.bce_y[b0 + i] : 0.f; };
   auto get_fo = [&](int i) {
     const int b = i / F;
     return b < nrows ? p.sv_fo[b0f + i] : 0.f;
@@ -111,12 +113,13 @@ bwd_kernel(BwdArgs p) {
   auto get_rsk = [&](int i) { return reinterpret_cast<const f32x4*>(p.rsk)[i]; };
   const int n_lw = lwp ? F : 0, n_fwlw = fwlw ? FD : 0, n_rsk = second ? p.MT * p.S * 16 : 0;
   const int n_fo = (red & kRedLw) ? kBM * F : 0, n_xv = red ? kBM * num : 0, n_fc = deep ? p.NT * 16 : 0;
-  float v_lw[1], v_fwlw[1], v_fc[1], v_dl[1], v_fo[2], v_xv[1];
+  float v_lw[1], v_fwlw[1], v_fc[1], v_dl[1], v_y[1], v_fo[2], v_xv[1];
   f32x4 v_rsk[1], v_e[4], v_x[4];
   stage_load<1>(v_lw, n_lw, tid, NTH, get_lw);
   stage_load<1>(v_fwlw, n_fwlw, tid, NTH, get_fwlw);
   stage_load<1>(v_rsk, n_rsk, tid, NTH, get_rsk);
   stage_load<1>(v_dl, kBM, tid, NTH, get_dl);
+  stage_load<1>(v_y, bce ? kBM : 0, tid, NTH, get_y);
   stage_load<2>(v_fo, n_fo, tid, NTH, get_fo);
   stage_load<1>(v_xv, n_xv, tid, NTH, get_xv);
   stage_load<1>(v_fc, n_fc, tid, NTH, get_fc);
@@ -127,6 +130,17 @@ bwd_kernel(BwdArgs p) {
   stage_store<1>(v_lw, n_lw, tid, NTH, get_lw, [&](int i, float v) { lw_s[i] = v; });
   stage_store<1>(v_fwlw, n_fwlw, tid, NTH, get_fwlw, [&](int i, float v) { fwlw_s[i] = v; });
   stage_store<1>(v_rsk, n_rsk, tid, NTH, get_rsk, [&](int i, f32x4 v) { reinterpret_cast<f32x4*>(rsk)[i] = v; });
+  if (bce && tid < kBM) {
+    // binary_cross_entropy_with_logits and its gradient for this tile's rows: bce_grad_kernel's arithmetic
+    const bool valid = b0 + tid < p.batch;
+    const float x = v_dl[0], t = v_y[0];
+    const float sg = 1.f / (1.f + expf(-x));
+    v_dl[0] = valid ? __fdiv_rn(__fsub_rn(sg, t), p.bce_denom) : 0.f;
+    float l = valid ? fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x))) : 0.f;
+    if (valid) p.bce_dl[b0 + tid] = v_dl[0];
+    l = sum16(l);
+    if (tid == 0 && p.loss_sum) atomicAdd(p.loss_sum, l);
+  }
   stage_store<1>(v_dl, kBM, tid, NTH, get_dl, [&](int i, float v) { dl[i] = v; });
   stage_store<2>(v_fo, n_fo, tid, NTH, get_fo, [&](int i, float v) {
     const int b = i / F;
@@ -741,12 +755,13 @@ __global__ void __launch_bounds__(256) reduce_kernel(RedArgs a) {
 // workgroup, each wave sums a quarter of the blocks in block order (32 loads in flight per lane: the sum is a
 // chain of dependent L2 round trips otherwise -- 8 in flight made it 6 us alone and ~39 us beside the weight
 // GEMM), then the four quarters are combined in a fixed order (deterministic).
-__global__ void __launch_bounds__(256) reduce_final_kernel(RedArgs a, int nblk) {
+// block `bx` of the final sums (64 outputs, the four waves each a quarter of the tiles)
+__device__ __forceinline__ void reduce_final_block(const RedArgs& a, int nblk, int bx) {
   __shared__ float q4[4][64];
   const int F = a.F, D = a.D, N = a.N, num = a.num, FD = F * D, numD = num * D;
   const int P = red_outputs(F, D, N, num);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int o = blockIdx.x * 64 + lane;
+  const int o = bx * 64 + lane;
   const int per = (nblk + 3) / 4;
   const int b0 = wave * per, b1 = b0 + per < nblk ? b0 + per : nblk;
   float s = 0.f;
@@ -796,6 +811,8 @@ __global__ void __launch_bounds__(256) reduce_final_kernel(RedArgs a, int nblk) 
   }
   if (dst) *dst += s * scale;
 }
+
+__global__ void __launch_bounds__(256) reduce_final_kernel(RedArgs a, int nblk) { reduce_final_block(a, nblk, blockIdx.x); }
 
 // ---------------------------------------------------------------------------
 // Categorical-table scatter (reference nn.Embedding / EmbeddingBag / QREmbeddingBag backward with
@@ -929,11 +946,10 @@ __device__ __forceinline__ int dwr_local(int t, int m) { return t < 4 ? 4 * m + 
 // kDwrP: k-steps of loads in flight per wave; NW: waves per workgroup (each a contiguous 1/NW of the split's rows).
 // Measured alike: kDwrP 4 / 6 / 8 (42.1 / 43.5 / 43.6 us) and eight waves per workgroup (43.7 us).
 template <int kDwrP, int NW>
-__global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
+__device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
   __shared__ __attribute__((aligned(16))) float red[2][kDwrT][kDwrLd];
   __shared__ float bred[NW][kDwrT];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int bid = blockIdx.x;
   int l = 1;
   while (l < a.H && bid >= a.blk0[l + 1]) ++l;
   bid -= a.blk0[l];
@@ -1059,6 +1075,22 @@ __global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
     const int n = n0 + r, k = k0 + c;
     if (n < N && k < K) atomicAdd(gW + (int64_t)n * K + k, red[0][r][c] + red[1][r][c]);
   }
+}
+
+template <int kDwrP, int NW>
+__global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
+  dwr_block<kDwrP, NW>(a, blockIdx.x);
+}
+
+// The weight-gradient GEMM and the shallow reductions' final sums as ONE launch (the one-stream step): the GEMM is
+// one round of workgroups that leaves CUs idle (225 for 256 CUs at Criteo-39), and the final sums' workgroups
+// (39) run there instead of in a launch of their own after it
+template <int kDwrP, int NW>
+__global__ void __launch_bounds__(64 * NW) dwr_reduce_kernel(DwArgs a, RedArgs r, int nblk, int dw_blocks) {
+  if ((int)blockIdx.x < dw_blocks)
+    dwr_block<kDwrP, NW>(a, blockIdx.x);
+  else
+    reduce_final_block(r, nblk, (int)blockIdx.x - dw_blocks);
 }
 
 // ---------------------------------------------------------------------------
@@ -1327,6 +1359,21 @@ hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
     if (q * w * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(total_blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r, hipStream_t s) {
+  if (total_blocks <= 0) return launch_reduce_final(r, s);
+  const int64_t q = a.rows_per_split / 4 + 4;
+  for (int l = 1; l <= a.H; ++l) {
+    const int64_t w = a.ldx[l] > a.N ? a.ldx[l] : a.N;
+    if (q * w * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
+  }
+  const int nblk = (int)((r.batch + kBM - 1) / kBM);
+  const int P = red_outputs(r.F, r.D, r.N, r.num);
+  const int rblocks = (P + 63) / 64;
+  hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(total_blocks + rblocks), dim3(256), 0, s, a, r, nblk,
+                     total_blocks);
   return hipGetLastError();
 }
 

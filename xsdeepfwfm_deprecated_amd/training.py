@@ -354,13 +354,14 @@ class FusedTrainStep:
                                          ctypes.c_void_p(xv.data_ptr()), xv.stride(0), n,
                                          ctypes.c_void_p(self.out.data_ptr()), self.drop, self.seed, st),
                    "dfwfm_train_forward")
-        _lib.check(L.dfwfm_bce_grad(ctypes.c_void_p(self.out.data_ptr()), ctypes.c_void_p(y.data_ptr()), n,
-                                    float(denom), ctypes.c_void_p(self.dlogit.data_ptr()),
-                                    ctypes.c_void_p(self.loss_sum.data_ptr()), st), "dfwfm_bce_grad")
         if phases is None:
             phases = _lib.BWD_TABLES if self._bucketed() else (_lib.BWD_TABLES | _lib.BWD_MLP_WEIGHTS)
-        _lib.check(L.dfwfm_backward_phases(h, ctypes.c_void_p(self.dlogit.data_ptr()), ctypes.byref(self.grads),
-                                           phases, st), "dfwfm_backward_phases")
+        # the loss gradient rides in the per-tile backward (dfwfm_backward_phases_bce: the same dlogit bits as
+        # dfwfm_bce_grad, one launch fewer)
+        _lib.check(L.dfwfm_backward_phases_bce(h, ctypes.c_void_p(self.out.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                               float(denom), ctypes.c_void_p(self.dlogit.data_ptr()),
+                                               ctypes.c_void_p(self.loss_sum.data_ptr()), ctypes.byref(self.grads),
+                                               phases, st), "dfwfm_backward_phases_bce")
         if self.sparse:
             self._sparse_lists(st)
 
