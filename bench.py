@@ -471,6 +471,8 @@ def main():
     # teardown (a masked stream left to process exit crashed in __cxa_finalize under rocprofv3)
     graphs = None
     torch.cuda.synchronize(dev)
+    # and the torch wrappers of those streams go first: nothing may hold a handle that is about to be destroyed
+    streams = st = None
     if _stream_handles:
         hip = _hip_runtime()
         for h in _stream_handles:

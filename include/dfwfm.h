@@ -104,6 +104,12 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
                           const float* fm_1st, const float* bias,
                           const float* const* lin_w, const float* const* lin_b,
                           const float* fc_w, void* stream);
+/* The same, and zero[0, nzero) (device floats, 16-byte aligned, nzero a multiple of 4) zeroed in the same launch:
+ * a training step's gradient buffer, so the re-pack and the zeroing run side by side (one launch, not two). */
+int dfwfm_model_set_dense_zero(dfwfm_model* m, const float* field_cov, const float* fwfm_lin,
+                               const float* fm_1st, const float* bias,
+                               const float* const* lin_w, const float* const* lin_b,
+                               const float* fc_w, float* zero, int64_t nzero, void* stream);
 
 /* The hot path: logits[b] for b in [0, batch).
  *   xi  int64 [batch, F - numerical] (row stride xi_stride elements): categorical indices

@@ -27,7 +27,7 @@ def header_functions():
 def test_header_declares_expected_api():
     assert header_functions() == sorted([
         "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_backward_phases",
-        "dfwfm_bce_grad", "dfwfm_backward_phases_bce",
+        "dfwfm_bce_grad", "dfwfm_backward_phases_bce", "dfwfm_model_set_dense_zero",
         "dfwfm_diag_stamps", "dfwfm_eval_metrics", "dfwfm_forward", "dfwfm_forward_batches",
         "dfwfm_forward_workspace_bytes",
         "dfwfm_forward_ws", "dfwfm_last_error", "dfwfm_model_build_fwfm_pairs", "dfwfm_model_build_sparse_mlp", "dfwfm_model_create", "dfwfm_model_destroy",

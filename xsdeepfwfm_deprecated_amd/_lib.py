@@ -107,6 +107,8 @@ SIGNATURES = {
     "dfwfm_model_destroy": (None, [_P]),
     "dfwfm_model_set_tables": (ctypes.c_int, [_P, ctypes.POINTER(dfwfm_field_tables), ctypes.c_int32, _P]),
     "dfwfm_model_set_dense": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P]),
+    "dfwfm_model_set_dense_zero": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P,
+                                                  ctypes.c_int64, _P]),
     "dfwfm_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
     "dfwfm_forward_batches": (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P, ctypes.c_int64,
                                              ctypes.c_int64, _P, _P]),

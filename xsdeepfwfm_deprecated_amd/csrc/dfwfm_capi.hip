@@ -368,10 +368,12 @@ int dfwfm_model_set_tables(dfwfm_model* m, const dfwfm_field_tables* t, int32_t 
   return DFWFM_OK;
 }
 
-int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* fwfm_lin, const float* fm_1st,
+static int set_dense_impl(dfwfm_model* m, const float* field_cov, const float* fwfm_lin, const float* fm_1st,
                           const float* bias, const float* const* lin_w, const float* const* lin_b,
-                          const float* fc_w, void* stream) {
+                          const float* fc_w, float* zero, int64_t nzero, void* stream) {
   if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  if (nzero < 0 || (nzero > 0 && (!zero || (nzero & 3) || (reinterpret_cast<uintptr_t>(zero) & 15))))
+    return fail(DFWFM_ERR_INVALID_ARG, "zero range: 16-byte aligned, a multiple of 4 floats");
   hipStream_t s = (hipStream_t)stream;
   const dfwfm_config& c = m->cfg;
   if (c.use_fwfm && !field_cov) return fail(DFWFM_ERR_INVALID_ARG, "use_fwfm needs field_cov");
@@ -393,6 +395,19 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
     j.block0 = blocks;
     blocks += (int)((total + 255) / 256);
   };
+  // the zero range first (its blocks are the long ones), in float4 units of kPackZeroPT per thread
+  if (nzero > 0) {
+    const int64_t n4 = nzero / 4;
+    if ((n4 + 256 * kPackZeroPT - 1) / (256 * kPackZeroPT) > 0x3fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "zero range");
+    PackJob& j = L.j[L.n++];
+    j.src = nullptr;
+    j.dst = zero;
+    j.total = n4;
+    j.type = kPackZero;
+    j.a = j.b = j.d = 0;
+    j.block0 = blocks;
+    blocks += (int)((n4 + 256 * kPackZeroPT - 1) / (256 * kPackZeroPT));
+  }
   if (c.use_fwfm || c.use_fm) {
     const int64_t tot = (int64_t)m->MT * m->S * 64;
     job(kPackFwfm, field_cov, m->d_upack, tot, m->F, c.use_fm ? 1 : 0, m->S);
@@ -423,6 +438,18 @@ int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* f
   m->flags &= ~kPairs;  // and so is the FwFM pair list
   for (int h = 0; h < m->H; ++h) m->lin_w[h] = lin_w ? lin_w[h] : nullptr;
   return DFWFM_OK;
+}
+
+int dfwfm_model_set_dense(dfwfm_model* m, const float* field_cov, const float* fwfm_lin, const float* fm_1st,
+                          const float* bias, const float* const* lin_w, const float* const* lin_b,
+                          const float* fc_w, void* stream) {
+  return set_dense_impl(m, field_cov, fwfm_lin, fm_1st, bias, lin_w, lin_b, fc_w, nullptr, 0, stream);
+}
+
+int dfwfm_model_set_dense_zero(dfwfm_model* m, const float* field_cov, const float* fwfm_lin, const float* fm_1st,
+                               const float* bias, const float* const* lin_w, const float* const* lin_b,
+                               const float* fc_w, float* zero, int64_t nzero, void* stream) {
+  return set_dense_impl(m, field_cov, fwfm_lin, fm_1st, bias, lin_w, lin_b, fc_w, zero, nzero, stream);
 }
 
 }  // extern "C"

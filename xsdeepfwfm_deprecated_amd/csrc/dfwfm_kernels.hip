@@ -878,6 +878,15 @@ __global__ void __launch_bounds__(256) pack_dense_kernel(const PackList L) {
     else hi = mid - 1;
   }
   const PackJob& j = L.j[lo];
+  if (j.type == kPackZero) {
+    // a bulk zero (the training step's gradient buffer): 16-byte stores, the block's threads on consecutive float4
+    float4* d = reinterpret_cast<float4*>(j.dst);
+    const int64_t q0 = (int64_t)(bid - j.block0) * 256 * kPackZeroPT + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < kPackZeroPT; ++u)
+      if (q0 + u * 256 < j.total) d[q0 + u * 256] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   const int64_t i = (int64_t)(bid - j.block0) * 256 + threadIdx.x;
   if (i < j.total) pack_elem(j, i);
 }

@@ -868,6 +868,7 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
   const int ne = ns * w;
   // elements in groups of SU per thread: all SU value loads are issued before the first atomic (an
   // atomic between two loads keeps the compiler from batching them: one memory round trip per element)
+  // (measured: the first group's values issued with the keys' loads, 28.1 -> 29.7 us for the two launches)
   constexpr int SU = 8;
   if constexpr (PRIV) {
     int* flag = reinterpret_cast<int*>(acc + T.rows * w);

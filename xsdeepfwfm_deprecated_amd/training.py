@@ -347,8 +347,9 @@ class FusedTrainStep:
 
     def _part1(self, n, denom, phases=None):
         L, st, h = self.L, self._stream(), self.eng.handle
-        self.grad.zero_()
-        _lib.check(L.dfwfm_model_set_dense(h, *self.dense_args, st), "dfwfm_model_set_dense")
+        # the dense weights re-packed and the gradient buffer zeroed in one launch
+        _lib.check(L.dfwfm_model_set_dense_zero(h, *self.dense_args, ctypes.c_void_p(self.grad.data_ptr()),
+                                                self.grad.numel(), st), "dfwfm_model_set_dense_zero")
         xi, xv, y = self._in
         _lib.check(L.dfwfm_train_forward(h, ctypes.c_void_p(xi.data_ptr()), xi.stride(0),
                                          ctypes.c_void_p(xv.data_ptr()), xv.stride(0), n,
