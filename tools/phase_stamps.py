@@ -63,10 +63,11 @@ n = _lib.lib().dfwfm_diag_stamps(m._engine.handle, buf, grid * 16,
 st = np.frombuffer(buf, dtype=np.uint64).reshape(grid, 16)[:n].astype(np.int64)
 names = ["stage (params, Xi/Xv)", "gather E + table first order", "shallow (fwlw, FwFM MFMA, sums)",
          "  . fwlw first order", "  . FwFM MFMA (wave 0)", "  . barrier wait", "  . first/second sums",
+         "    . sums code (wave 0)", "    . sums end -> MLP start",
          "MLP layer 1", "  . K loop (wave 0)", "  . epilogue (wave 0)", "  . barrier wait", "MLP layer 2",
          "MLP layer 3", "deep reduce + combine"]
-slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (3, 4), (3, 12), (12, 13), (13, 4), (4, 5),
-         (5, 6), (6, 8)]
+slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (11, 7), (7, 3), (3, 4), (3, 12), (12, 13),
+         (13, 4), (4, 5), (5, 6), (6, 8)]
 rt0, rt1 = st[:, 14], st[:, 15] & ((1 << 48) - 1)
 life = (rt1 - rt0) / 100.0
 span = (rt1.max() - rt0.min()) / 100.0
@@ -85,6 +86,9 @@ print(f"workgroups {n}; total cycles median {np.median(tot):.0f} (p10 {np.percen
 if a.fwfm:  # no MLP: stage, gather, shallow phases, then the combine (slot 8)
     names = names[:7] + ["combine after the shallow barrier"]
     slots = slots[:7] + [(11, 8)]
+elif os.environ.get("DFWFM_R32") == "1":  # fwd32 has no slot 7
+    names = names[:7] + names[9:]
+    slots = slots[:7] + slots[9:]
 for nm, sl in zip(names, slots):
     if sl is None:
         continue

@@ -34,12 +34,20 @@ __device__ __forceinline__ TileRef tile_ref(const FwdArgs& p) {
   return TileRef{p.xi, p.xv, p.out, (int64_t)blockIdx.x * ROWS};
 }
 
-// sum over the 16 lanes of an aligned 16-lane group
+// one DPP-moved copy of v (the move rides on the VALU; a __shfl_xor is an LDS-crossbar round trip)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// sum over the 16 lanes of an aligned 16-lane group (a DPP row), every lane gets the total: row_ror:8,
+// row_ror:4, then quad_perm [2,3,0,1] and [1,0,3,2].  Each step adds the partner of lane i ^ 8, ^ 4, ^ 2, ^ 1
+// (a rotation by 8 is i ^ 8; after it every value is symmetric under ^ 8, so a rotation by 4 adds i ^ 4's).
 __device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 8);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 1);
+  v += dpp_f<0x128>(v);
+  v += dpp_f<0x124>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0xB1>(v);
   return v;
 }
 

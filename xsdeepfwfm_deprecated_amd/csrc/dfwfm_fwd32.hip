@@ -452,28 +452,39 @@ fwd32_kernel(FwdArgs p) {
   stamp(p.stamps, 11, tid);
   {
     // first[b] (lw projection or plain sum) and second[b]: 16 lanes per sample, every 16th term, then a 16-lane
-    // butterfly -- eight waves x four samples = the 32 rows
+    // DPP sum -- eight waves x four samples = the 32 rows.  All LDS reads issue before the first add (no chain
+    // of dependent LDS round trips, see fwd_kernel's sums).
     const int b = wave * 4 + (lane >> 4);
     const int h = b >> 4;
     const int bl = b & 15;
     const int q = lane & 15;
     float first = 0.f, second = 0.f;
-    for (int f = q; f < F; f += 16) {
-      const float x = fo[b * Fp + f];
-      first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
+    for (int f0 = 0; f0 < F; f0 += 64) {
+      float x[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int f = min(f0 + 16 * k + q, F - 1);
+        x[k] = fo[b * Fp + f];
+        l[k] = (flags & kFoLw) ? lw_s[f] : 1.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) first = f0 + 16 * k + q < F ? fmaf(x[k], l[k], first) : first;
     }
     if (flags & kHasSecond) {
-      const int MTD = p.MT * D;
+      const int MT = p.MT;
       for (int d = q; d < D; d += 16) {
         const int n = bl * D + d;
-        for (int m = 0; m < p.MT; ++m) second += part2[(h * MTD + m * D + (n >> 4)) * 16 + (n & 15)];
+        const float* pp = part2 + (h * MT * D + (n >> 4)) * 16 + (n & 15);  // + m * D * 16 for row tile m
+        float v[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) v[m] = pp[min(m, MT - 1) * D * 16];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) second += m < MT ? v[m] : 0.f;
+        for (int m = 4; m < MT; ++m) second += pp[m * D * 16];
       }
     }
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) {
-      first += __shfl_xor(first, o);
-      second += __shfl_xor(second, o);
-    }
+    first = sum16(first);
+    second = sum16(second);
     if (q == 0) fs[b] = first + second;
   }
   stamp(p.stamps, 3, tid);

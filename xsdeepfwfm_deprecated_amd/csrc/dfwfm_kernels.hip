@@ -574,33 +574,46 @@ fwd_kernel(FwdArgs p) {
     }
   }
   if (wave < 4) {
-    // first[b] (lw projection or plain sum over fields) and second[b] (sum over d): 16 lanes per
-    // sample each take every 16th term, then a 16-lane butterfly (a serial 39-term LDS chain in 16
-    // threads cost ~5k cycles)
+    // first[b] (lw projection or plain sum over fields) and second[b] (sum over d): 16 lanes per sample
+    // each take every 16th term, then a 16-lane DPP sum.  Every LDS read is issued before the first add:
+    // this runs while waves 4-7 already stream layer 1 through the LDS, and a chain of a dozen dependent
+    // LDS round trips (loop-carried reads, __shfl_xor butterflies) took ~10k cycles there.
     const int b = wave * 4 + (lane >> 4);
     const int q = lane & 15;
     float first = 0.f, second = 0.f;
-    for (int f = q; f < F; f += 16) {
-      const float x = fo[b * Fp + f];
-      first = (flags & kFoLw) ? fmaf(x, lw_s[f], first) : first + x;
+    for (int f0 = 0; f0 < F; f0 += 64) {
+      float x[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int f = min(f0 + 16 * k + q, F - 1);
+        x[k] = fo[b * Fp + f];
+        l[k] = (flags & kFoLw) ? lw_s[f] : 1.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) first = f0 + 16 * k + q < F ? fmaf(x[k], l[k], first) : first;
     }
     if (flags & kHasSecond) {
       if constexpr (PART == 3) {
         second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
       } else {
+        const int MT = p.MT;
         for (int d = q; d < D; d += 16) {  // D = 32: two terms per lane
           const int n = b * D + d;
-          for (int m = 0; m < p.MT; ++m) second += part2[(m * D + (n >> 4)) * 16 + (n & 15)];
+          const float* pp = part2 + (n >> 4) * 16 + (n & 15);  // part2[(m * D + (n >> 4)) * 16 + (n & 15)]
+          float v[4];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) v[m] = pp[min(m, MT - 1) * D * 16];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) second += m < MT ? v[m] : 0.f;
+          for (int m = 4; m < MT; ++m) second += pp[m * D * 16];
         }
       }
     }
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) {
-      first += __shfl_xor(first, o);
-      second += __shfl_xor(second, o);
-    }
+    first = sum16(first);
+    second = sum16(second);
     if (q == 0) fs[b] = first + second;
   }
+  if (p.H < 4) stamp(p.stamps, 7, tid);  // diagnostics: the sums' end (slot 7 is a layer slot only past three layers)
 
   if (!deep) {
     __syncthreads();
