@@ -711,6 +711,39 @@ def test_resident_inputs_graphs_equal_copied_inputs(gpu):
     assert np.median(e) < 1e-4 and np.quantile(e, 0.999) < 0.02, (np.median(e), np.quantile(e, 0.999))
 
 
+def test_step_many_equals_single_steps(gpu):
+    """FusedTrainStep.step_many captures consecutive steps over a ring of resident batches as ONE graph; the
+    parameters and the running loss after 1 + 2 x 3 steps equal seven step() calls (same kernels, dropout seeds and
+    Adam counts from the device counter), up to the weight-gradient GEMM's split-K float atomics (the bar above)."""
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_deepfwfm_lw")
+    B = 64
+    bat = [tuple(torch.from_numpy(a).to(gpu) for a in b) for b in _batches(cfg, xi, xv, y, B, 3)]
+    res, losses = [], []
+    for many in (False, True):
+        m = build(cfg, params, gpu, is_deep_dropout=True)
+        m.train()
+        torch.manual_seed(5)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, resident_inputs=True)
+        t.step(*bat[0])
+        for _ in range(2):
+            if many:
+                t.step_many([bat[1], bat[2], bat[0]])
+            else:
+                for k in (1, 2, 0):
+                    t.step(*bat[k])
+        torch.cuda.synchronize()
+        assert t.steps == 7
+        if many:
+            assert any(k[0] == "many" for k in t._graph_sets)
+        losses.append(float(t.loss_sum.item()))
+        res.append({n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()})
+        t.close()
+    e = np.concatenate([np.abs(res[0][n] - res[1][n]).reshape(-1) / 1e-3 for n in res[0]])
+    assert np.median(e) < 1e-4 and np.quantile(e, 0.999) < 0.02, (np.median(e), np.quantile(e, 0.999))
+    assert abs(losses[0] - losses[1]) <= 1e-4 * abs(losses[0]), losses
+
+
 def _nccl_world1_worker(port, q, name, graph_comm):
     """A world-size-1 RCCL process group (backend "nccl" is RCCL on ROCm): the packed touched-row all-gather
     (all_gather_into_tensor branch of gather_packed) and FusedTrainStep's bucketed exchange run over RCCL --

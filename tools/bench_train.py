@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--apply-worlds", default="",
                     help="with --exchange-world1: afterwards time the apply of W ranks' lists (comma list of W; the "
                          "lists of W distinct batches built by the step itself)")
+    ap.add_argument("--steps-per-graph", type=int, default=1,
+                    help="fused, one rank: K > 1 replays K consecutive steps over the resident ring as one graph "
+                         "(FusedTrainStep.step_many; --steps must be a multiple of K)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; started here unless "
                                                            "torchrun already set WORLD_SIZE)")
     a = ap.parse_args()
@@ -103,8 +106,16 @@ def main():
         opt.step()
         return loss
 
-    for i in range(a.warmup):
-        step(i)
+    K = a.steps_per_graph if (trainer is not None and world == 1 and not a.exchange_world1) else 1
+    if K > 1:
+        if a.steps % K or a.warmup % K:
+            raise SystemExit("--steps and --warmup must be multiples of --steps-per-graph")
+        step(0)  # the first step runs eagerly (step_many needs one behind it)
+
+        def step_k(i):
+            return trainer.step_many([batches[(i + j) % 4] for j in range(K)])
+    for i in range(0, a.warmup, K):
+        step(i) if K == 1 else step_k(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -112,8 +123,8 @@ def main():
     t1 = torch.cuda.Event(enable_timing=True)
     wall0 = time.perf_counter()
     t0.record()
-    for i in range(a.steps):
-        loss = step(i)
+    for i in range(0, a.steps, K):
+        loss = step(i) if K == 1 else step_k(i)
     host = time.perf_counter() - wall0  # the host's enqueue time (ahead of the GPU if well under the step time)
     t1.record()
     torch.cuda.synchronize(dev)
@@ -129,7 +140,7 @@ def main():
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms / a.steps, 4), "per_gpu_batch": B,
            "first_order": a.first_order, "dropout": not a.no_dropout, "wall_s": round(wall, 3),
            "host_enqueue_us_per_step": round(host * 1e6 / a.steps, 1),
-           "mode": a.mode, "inputs": "copied" if (a.copy_inputs or a.mode != "fused") else "resident (read in place)",
+           "mode": a.mode, "steps_per_graph": K, "inputs": "copied" if (a.copy_inputs or a.mode != "fused") else "resident (read in place)",
            "final_loss_sum": round(float(loss.item()), 4)}
     if trainer is not None and getattr(trainer, "sparse", False):
         # touched-row lists all-gathered per step (fixed capacity: sum over tables of min(batch, rows))
