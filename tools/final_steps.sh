@@ -16,5 +16,6 @@ bash tools/gpu_steps.sh "$T" \
  'qr20|200|python bench.py --config qr --steps 20 --warmup 5 --no-cpu-baseline' \
  'pruned20|200|python bench.py --config pruned --steps 20 --warmup 5 --no-cpu-baseline' \
  'train|200|python tools/bench_train.py --steps 500 --warmup 20' \
+ 'train4|200|python tools/bench_train.py --steps 500 --warmup 20 --steps-per-graph 4' \
  "proftrain|200|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_proftrain -o run --output-format csv -- python3 tools/bench_train.py --steps 50" \
  'latency|300|python tools/latency.py --calls 300'
