@@ -6,7 +6,8 @@ T=${1:-final}
 bash tools/gpu_steps.sh "$T" \
  't-tests|1100|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread' \
  'smoke|300|python -c "import __graft_entry__ as g; g.smoke()"' \
- 'bench20|300|python bench.py' \
+ 'bench|300|python bench.py' \
+ 'bench20|200|python bench.py --steps 20 --warmup 5' \
  "prof20|300|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof20 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5" \
  'bench2000|300|python bench.py --steps 2000 --warmup 400 --no-cpu-baseline' \
  'fwfm20|200|python bench.py --config fwfm --steps 20 --warmup 5 --no-cpu-baseline' \
