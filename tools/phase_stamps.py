@@ -84,8 +84,10 @@ tot = st[:, 8] - st[:, 0]
 print(f"workgroups {n}; total cycles median {np.median(tot):.0f} (p10 {np.percentile(tot, 10):.0f}, "
       f"p90 {np.percentile(tot, 90):.0f})")
 if a.fwfm:  # no MLP: stage, gather, shallow phases, then the combine (slot 8)
-    names = names[:7] + ["combine after the shallow barrier"]
-    slots = slots[:7] + [(11, 8)]
+    names = ["stage (params, Xi/Xv)", "gather E + table first order", "shallow + combine",
+             "  . fwlw first order", "  . FwFM MFMA (wave 0)", "  . barrier wait", "  . sums (wave 0)",
+             "  . barrier + logits out"]
+    slots = [(0, 1), (1, 2), (2, 8), (2, 9), (9, 10), (10, 11), (11, 7), (7, 8)]
 elif os.environ.get("DFWFM_R32") == "1":  # fwd32 has no slot 7
     names = names[:7] + names[9:]
     slots = slots[:7] + slots[9:]
