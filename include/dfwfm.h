@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DFWFM_ABI_VERSION 2
+#define DFWFM_ABI_VERSION 3  /* 3: dfwfm_sparse_grads removed, dfwfm_model_set_dense_zero / dfwfm_backward_phases_bce added */
 
 typedef enum {
   DFWFM_OK = 0,

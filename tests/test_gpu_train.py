@@ -366,12 +366,15 @@ def test_data_parallel_fit_two_ranks(gpu):
     assert num / den < 2e-6, num / den
 
 
-@pytest.mark.parametrize("D,N,H,fwlw", [(4, 256, 1, 0), (16, 512, 2, 0), (8, 96, 3, 1), (10, 144, 2, 1),
-                                        (16, 340, 1, 1)])
-def test_train_step_shape_sweep_matches_oracle(gpu, D, N, H, fwlw):
+@pytest.mark.parametrize("F,D,N,H,fwlw", [(39, 4, 256, 1, 0), (39, 16, 512, 2, 0), (39, 8, 96, 3, 1),
+                                          (39, 10, 144, 2, 1), (39, 16, 340, 1, 1),
+                                          # the backward LDS envelope: 149.4 KiB with the field_cov Gram in the G
+                                          # buffer (a separate Gram region made it 167.4 KiB and refused it)
+                                          (45, 16, 400, 1, 0)])
+def test_train_step_shape_sweep_matches_oracle(gpu, F, D, N, H, fwlw):
     """Gradients of one HIP step vs the training oracle over embedding sizes and MLP shapes."""
     from test_gpu_parity import _sweep_case
-    cfg, params, xi, xv = _sweep_case(39, 13, D, N, H, fwlw, seed=7 * D + N + H)
+    cfg, params, xi, xv = _sweep_case(F, 13, D, N, H, fwlw, seed=7 * D + N + H)
     y = (np.arange(len(xi)) % 3 == 0).astype(np.float32)
     m = build(cfg, params, gpu, is_deep_dropout=False)
     out, loss, grads, newp = hip_step(m, xi, xv, y, gpu, 1e-3, 3e-7)

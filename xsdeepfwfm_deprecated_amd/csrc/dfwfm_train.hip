@@ -34,13 +34,14 @@ __host__ __device__ inline BwdLds bwd_layout(int F, int D, int MT, int S, int SX
   L.rsk = o;   o += MT * S * 64;
   L.bufE = o;  o += kBM * (SX > SY ? SX : SY);  // E tile; reused as the second G buffer
   L.bufD = o;  o += kBM * SX;                   // dE tile
-  L.bufA = o;  o += kBM * SY;                   // G buffer
+  // G buffer; until P2 stores X_H into it, it holds the field_cov Gram's chains (P1 -> the reduction after it)
+  L.bufA = o;  o += kBM * SY > 2 * MT * MT * 256 ? kBM * SY : 2 * MT * MT * 256;
+  L.gram = L.bufA;
   L.dl = o;    o += kBM;
   L.fc = o;    o += SY;                       // net_1_fc (G_H = dlogit * fc * mask)
   L.tailr = o; o += 8 * 64 * 4;               // split-tail partial products (eight waves)
   L.fo = o;    o += kBM * r4(F);              // fused reductions: first order per field
   L.xv = o;    o += kBM * r4(F);              //                   numerical values (num <= F)
-  L.gram = o;  o += 2 * MT * MT * 256;          //                   field_cov Gram: both chains of every tile
   L.total = r4(o);
   return L;
 }
@@ -306,7 +307,8 @@ bwd_kernel(BwdArgs p) {
     const float scale = drop ? p.drop_scale : 1.f;
     const uint32_t dseed = drop ? step_seed(p.seed, p.seed_src) : 0u;
     // G_H = dlogit * fc * (X_H > 0) * scale -> bufA (X_H read in P0, written to LDS now; G_H is stored to the
-    // workspace at the top of layer H, behind its weight preload)
+    // workspace at the top of layer H, behind its weight preload).  bufA held the field_cov Gram until now.
+    if (red & kRedR) __syncthreads();
     tile_store<4>(bufA, SY, v_x, xh_g, p.N, nrows, p.N / 4, p.NT * 4, tid, NTH);
     __syncthreads();
     // column n per thread: the fused net_1_fc reduction (sum_b dlogit_b X_H[b, n], reduce_kernel's order)

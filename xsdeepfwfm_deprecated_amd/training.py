@@ -137,6 +137,10 @@ def packed_layout(fams):
     return a16(nbytes + 4 * len(fams))
 
 
+# DFWFM_TRAIN_FORK: the one-process step's graph layout
+_FORKS = frozenset(("none", "reduce", "spread", "tiles"))
+
+
 class FusedTrainStep:
     """One reference training step -- fit()'s inner-loop body (:619-637): zero_grad, forward,
     BCE-with-logits, backward, Adam(lr, weight_decay) -- as HIP launches on pre-built pointers, captured
@@ -151,10 +155,12 @@ class FusedTrainStep:
     resident_inputs: full batches whose (xi, xv, y) tensors recur (a ring of device-resident input buffers,
     e.g. a loader double-buffering into fixed tensors) are read in place -- one captured graph set per buffer
     set (at most ``max_graph_sets``, least recently used dropped) -- instead of being copied into the step's
-    own input buffers first (three copy launches per step)."""
+    own input buffers first (three copy launches per step).  step_many (several steps per graph) needs it: its
+    graphs read their batches in place and live in a cache of their own (``max_many_sets``)."""
 
     def __init__(self, model, batch_size, lr=1e-3, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8,
-                 use_graph=True, dist=None, sparse_exchange=True, resident_inputs=False, max_graph_sets=8):
+                 use_graph=True, dist=None, sparse_exchange=True, resident_inputs=False, max_graph_sets=8,
+                 max_many_sets=2):
         dev = model._device()
         if dev.type != "cuda":
             raise _lib.DfwfmError("FusedTrainStep runs only on a HIP device")
@@ -166,6 +172,8 @@ class FusedTrainStep:
         self.resident_inputs = bool(resident_inputs)
         self.max_graph_sets = max(1, int(max_graph_sets))
         self._graph_sets = {}  # (denom, drop, workspace generation, input pointers) -> (graphs, inputs)
+        self.max_many_sets = max(1, int(max_many_sets))
+        self._many_sets = {}  # step_many's K-step graphs, keyed like _graph_sets (their own LRU: no evictions of step()'s)
         self.eng = model._sync_engine(dev)
         self.L = _lib.lib()
         params = [p for p in model.parameters() if p.requires_grad]
@@ -209,6 +217,8 @@ class FusedTrainStep:
         # after the scatter / right after the per-tile backward, the weight-gradient GEMM and the MLP's Adam on a
         # side stream
         self.fork = os.environ.get("DFWFM_TRAIN_FORK", "none")
+        if self.fork not in _FORKS:
+            raise ValueError(f"DFWFM_TRAIN_FORK={self.fork!r}: expected one of {sorted(_FORKS)}")
         views = {}
         adam = (_lib.dfwfm_adam_tensor * len(params))()
         for i, p in enumerate(params):
@@ -330,6 +340,7 @@ class FusedTrainStep:
         self._attached = False
         self.graphs = None
         self._graph_sets = {}
+        self._many_sets = {}
 
     def __del__(self):
         try:
@@ -653,8 +664,10 @@ class FusedTrainStep:
         calling step() on each in turn (the dropout seed and Adam's step count come from the device counter every
         step bumps), without the ~9 us of idle between two graph replays.  One process, one-stream step only;
         otherwise (data parallelism, a forked layout, the first step, a batch that is not full or not readable in
-        place) it runs step() per batch.  Returns the running loss sum like step()."""
-        direct = [self._direct_inputs(xi, xv, y, int(xi.shape[0])) for xi, xv, y in batches]
+        place, or resident_inputs=False: each new set of input pointers would be a K-step capture) it runs step()
+        per batch.  Returns the running loss sum like step()."""
+        direct = [self._direct_inputs(xi, xv, y, int(xi.shape[0])) for xi, xv, y in batches] \
+            if self.resident_inputs else [None]
         if (not batches or not self.use_graph or self.dist is not None or self.fork != "none" or self.steps < 1
                 or any(int(xi.shape[0]) != self.B for xi, _, _ in batches) or any(d is None for d in direct)):
             for xi, xv, y in batches:
@@ -666,10 +679,10 @@ class FusedTrainStep:
         denom = float(self.B)
         key = ("many", denom, self.drop, self._ws_generation(),
                tuple((t.data_ptr(), tuple(t.stride())) for d in direct for t in d))
-        hit = self._graph_sets.pop(key, None)
+        hit = self._many_sets.pop(key, None)
         if hit is None:
-            if len(self._graph_sets) >= self.max_graph_sets:
-                self._graph_sets.pop(next(iter(self._graph_sets)))
+            if len(self._many_sets) >= self.max_many_sets:
+                self._many_sets.pop(next(iter(self._many_sets)))
             s = torch.cuda.Stream(self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
             g = torch.cuda.CUDAGraph()
@@ -681,7 +694,7 @@ class FusedTrainStep:
                         self._part2()
             torch.cuda.current_stream(self.dev).wait_stream(s)
             hit = ((g, None, None, None, None), direct)
-        self._graph_sets[key] = hit
+        self._many_sets[key] = hit
         hit[0][0].replay()
         self.steps += len(batches)
         self.eng._dense_key = None
