@@ -223,6 +223,61 @@ def algorithmic_counts(cfg, sizes=None):
 GATE_STEPS = 640  # steps queued behind the host gate before it is released (see _HostGate)
 
 
+def max_over_ranks(x, world, dev):
+    """The slowest rank's value of x (the timed region's length): all-reduce MAX over the process group."""
+    if world <= 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64 if dev.type == "cpu" else torch.float32, device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_value(world, steps, ms):
+    """Whole-job samples/s: every rank ran `steps` batches of BATCH in at most `ms` (the max over ranks)."""
+    return world * BATCH * steps / (ms / 1e3)
+
+
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def stub_main(a, stub_ms):
+    """CPU rehearsal of the N-rank path (DFWFM_BENCH_STUB_MS set; tests/test_launch.py): the same rank processes
+    (spawn_ranks), rank environment, barriers around the timed region and max-over-ranks aggregation as main(),
+    over gloo, with each step's forward replaced by a host sleep of stub_ms x (1 + rank / world) -- rank N-1 is the
+    slowest, so the aggregate must be world x BATCH x steps over ITS region.  Never touches a GPU."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    env = {k: os.environ.get(k) for k in RANK_ENV}
+    if world > 1:
+        dist.init_process_group("gloo")
+    per_step = stub_ms * (1.0 + rank / world) / 1e3
+    for _ in range(a.warmup):
+        time.sleep(per_step)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        time.sleep(per_step)
+    ms_rank = (time.perf_counter() - t0) * 1e3
+    if world > 1:
+        dist.barrier()
+    cpu = torch.device("cpu")
+    ms = max_over_ranks(ms_rank, world, cpu)
+    envs, times = [env], [ms_rank]
+    if world > 1:
+        envs, times = [None] * world, [None] * world
+        dist.all_gather_object(envs, env)
+        dist.all_gather_object(times, ms_rank)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(aggregate_value(world, a.steps, ms), 1),
+                          "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": round(ms / a.steps, 6), "higher_is_better": True, "scaling": "weak",
+                          "stub": {"ms_per_step": stub_ms, "rank_env": envs, "rank_ms": times}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     # --gpus N without torchrun: start N ranks (one process per GPU) before anything touches the GPU, and exit
@@ -231,6 +286,8 @@ def main():
     rc = spawn_ranks(a.gpus)
     if rc is not None:
         sys.exit(rc)
+    if os.environ.get("DFWFM_BENCH_STUB_MS"):  # CPU rehearsal of the rank path (tests only)
+        return stub_main(a, float(os.environ["DFWFM_BENCH_STUB_MS"]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -477,14 +534,11 @@ def main():
         hip = _hip_runtime()
         for h in _stream_handles:
             hip.hipStreamDestroy(h)
-    if world > 1:
-        t = torch.tensor([ms], device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        ms = float(t.item())
+    ms = max_over_ranks(ms, world, dev)
 
     ms_per_step = ms / a.steps
     mfma_bound = "mfma"
-    value = world * BATCH * a.steps / (ms / 1e3)
+    value = aggregate_value(world, a.steps, ms)
     flops, bytes_ = algorithmic_counts(cfg, sizes)
     if a.config == "pruned" and sparse_on:
         # the sparse tower does the nonzero products only: 2 x nonzero hidden weights + fc, and the
@@ -559,9 +613,7 @@ def main():
     if not a.no_per_call and not (a.config == "pruned" and sparse_on):
         pc = per_call_leg(eng, batches, dev, a.steps, flops, bytes_, a.config)
         if world > 1:
-            t = torch.tensor([pc["us_per_batch"]], device=dev)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            pc["us_per_batch"] = round(float(t.item()), 3)
+            pc["us_per_batch"] = round(max_over_ranks(pc["us_per_batch"], world, dev), 3)
             pc["samples_per_s"] = round(world * BATCH / (pc["us_per_batch"] / 1e6), 1)
         result["per_call"] = pc
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -68,3 +68,34 @@ def test_spawn_ranks_is_a_no_op_inside_a_rank(monkeypatch):
     assert spawn_ranks(2, argv=["-c", "raise SystemExit(1)"]) is None
     monkeypatch.delenv("WORLD_SIZE")
     assert spawn_ranks(1, argv=["-c", "raise SystemExit(1)"]) is None
+
+
+def test_bench_gpus8_spawns_ranks_and_aggregates_max(tmp_path):
+    """bench.py --gpus 8 on the CPU (DFWFM_BENCH_STUB_MS: the forward replaced by a host sleep of stub x (1 + rank /
+    world) per step, gloo): eight child ranks with RANK / LOCAL_RANK / WORLD_SIZE set, barriers around the timed
+    region, and ONE JSON line from rank 0 whose value is 8 x 4096 x steps over the SLOWEST rank's region."""
+    import json
+    import subprocess
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["DFWFM_BENCH_STUB_MS"] = "20"
+    steps = 5
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", str(steps),
+                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 8 and r["steps"] == steps and r["scaling"] == "weak"
+    envs = r["stub"]["rank_env"]
+    assert sorted(int(e["RANK"]) for e in envs) == list(range(8))
+    for e in envs:
+        assert e["LOCAL_RANK"] == e["RANK"] and e["WORLD_SIZE"] == "8" and e["MASTER_ADDR"] == "127.0.0.1"
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+    times = r["stub"]["rank_ms"]
+    slowest = max(times)
+    assert times.index(slowest) == 7  # rank 7 sleeps 1.875x rank 0's stub per step
+    assert abs(r["ms_per_step"] * steps - slowest) < 1e-3 * slowest + 1e-3
+    assert abs(r["value"] - 8 * 4096 * steps / (slowest / 1e3)) <= 0.1 + 1e-6 * r["value"]
+    assert slowest >= steps * 20 * 1.875 * 0.99

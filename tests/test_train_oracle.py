@@ -170,7 +170,7 @@ def _sparse_protocol_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])  # 8: BASELINE configs[4] is DP = 8
 def test_touched_row_exchange_protocol_gloo(world):
     """configs[4] exchange at oracle level on CPU: `world` gloo ranks' touched-row lists of both table families,
     all-gathered at fixed capacity in training.packed_layout's buffer and added in rank order, equal the dense
@@ -195,3 +195,29 @@ def test_touched_row_exchange_protocol_gloo(world):
     for got, prefix in zip(res[0], ("fm_2nd_embeddings", "fm_1st_embeddings")):
         dense = np.concatenate([g[f"{prefix}.{f}.weight"].reshape(-1) for f in range(13, 39)])
         assert np.abs(got - dense).max() <= 2e-5 * np.abs(dense).max()
+
+
+def _criteo_fams(B, world=1):
+    """The two table families' exchange capacities at Criteo-39 (sum over the 26 categorical tables of min(rows,
+    per-rank batch), as dfwfm_sparse_grads_size reports them) and their packed layout."""
+    from xsdeepfwfm_deprecated_amd import synth
+    from xsdeepfwfm_deprecated_amd.training import packed_layout
+    cap = sum(min(B, n) for n in synth.CRITEO_FEATURE_SIZES[13:])
+    fams = [dict(cap=cap, w=10), dict(cap=cap, w=1)]
+    return fams, packed_layout(fams)
+
+
+def test_exchange_workspace_fits_dp8_and_refuses_oversize():
+    """configs[4]: eight ranks of B = 4096 at Criteo-39 fit the exchange workspace (3.45 MB of packed lists per rank,
+    DESIGN.md section 6); a world whose all-gathered buffer would not fit is refused with a clear error before
+    anything is captured (FusedTrainStep._setup_sparse calls the same check)."""
+    from xsdeepfwfm_deprecated_amd.training import check_exchange
+    fams, nbytes = _criteo_fams(4096)
+    assert fams[0]["cap"] == 57531 and 3.4e6 < nbytes < 3.5e6
+    assert check_exchange(8, nbytes, fams) == 8 * nbytes
+    with pytest.raises(ValueError, match="exceed the exchange workspace"):
+        check_exchange(8, nbytes, fams, max_bytes=8 * nbytes - 1)
+    with pytest.raises(ValueError, match="exceed the exchange workspace"):
+        check_exchange(1024, nbytes, fams)  # 3.5 GB of receive buffer
+    with pytest.raises(ValueError, match="32-bit grid"):
+        check_exchange(1, 16, [dict(cap=2 ** 28, w=10)], max_bytes=2 ** 62)

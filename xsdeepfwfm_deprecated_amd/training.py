@@ -137,6 +137,31 @@ def packed_layout(fams):
     return a16(nbytes + 4 * len(fams))
 
 
+# the exchange's receive workspace: world x packed bytes, all-gathered in one collective and walked by
+# dfwfm_sparse_grads_apply, whose grid and per-list counts are 32-bit (DFWFM_DP_EXCHANGE_MAX_BYTES lowers it)
+EXCHANGE_MAX_BYTES = 2 ** 31 - 1
+
+
+def check_exchange(world, nbytes, fams, max_bytes=None):
+    """Refuse, before anything is allocated or captured, a data-parallel exchange whose all-gathered receive buffer
+    (world x nbytes of packed touched-row lists) would exceed the exchange workspace, or a list too long for the
+    apply kernel's 32-bit counts / grid.  Returns the receive buffer's size in bytes."""
+    limit = int(max_bytes if max_bytes is not None else
+                os.environ.get("DFWFM_DP_EXCHANGE_MAX_BYTES", EXCHANGE_MAX_BYTES))
+    total = int(world) * int(nbytes)
+    if world < 1:
+        raise ValueError(f"data-parallel exchange: world size {world}")
+    if total > limit:
+        raise ValueError(f"data-parallel exchange: {world} ranks x {nbytes:,} bytes of packed touched-row lists = "
+                         f"{total:,} bytes exceed the exchange workspace ({limit:,} bytes); use fewer ranks, a "
+                         f"smaller per-rank batch, or sparse_exchange=False (dense all-reduce of the tables)")
+    for f in fams:
+        if f["cap"] * f["w"] > 2 ** 31 - 1:
+            raise ValueError(f"data-parallel exchange: a list of {f['cap']:,} rows x {f['w']} floats exceeds the "
+                             "apply kernel's 32-bit grid")
+    return total
+
+
 # DFWFM_TRAIN_FORK: the one-process step's graph layout (DESIGN.md section 4)
 _FORKS = frozenset(("none", "reduce", "spread", "tiles"))
 
@@ -300,6 +325,7 @@ class FusedTrainStep:
                 fams.append(dict(fam=fam, dest=dest, cap=int(cap.value), w=int(w.value), ws_bytes=int(ws.value)))
         nbytes = packed_layout(fams)
         world = self.dist.get_world_size()
+        check_exchange(world, nbytes, fams)  # refused before any buffer is allocated or a graph captured
         self.sp_send = torch.zeros(nbytes, dtype=torch.uint8, device=self.dev)
         self.sp_recv = torch.zeros(world, nbytes, dtype=torch.uint8, device=self.dev)
         self.sp_fams = fams
