@@ -75,6 +75,10 @@ struct dfwfm_model {
   float* sv_de;
   float* sv_x0;           // X_0 after deep-tower dropout (without dropout X_0 is sv_e)
   float* red_part;        // per-16-row-tile partial sums of the shallow reductions
+  float* dw_part;         // weight-gradient GEMM: per (block, split) slices (deterministic split-K, dwr_block)
+  float* dw_bpart;
+  int32_t* dw_ticket;     // per block, zero between launches
+  int64_t dw_slices;      // blocks x splits the slices hold
   FieldDev h_fields[64];  // host copy of the field descriptors (scatter task planning)
   // the last dfwfm_train_forward, replayed by dfwfm_backward
   const int64_t* t_xi;
@@ -88,6 +92,7 @@ struct dfwfm_model {
   bool trained;
   bool bwd_tables;  // the per-tile backward (sv_de) ran for the last dfwfm_train_forward
   bool bwd_fused_red;  // ... with the dense shallow reductions fused in (per-tile partials written)
+  float* bwd_loss_sum; // ... and the loss gradient fused in too: the tiles' losses are partials, summed into this
   bool tables_set;
   bool dense_set;
 };
@@ -513,7 +518,36 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   memcpy(a.fw_off8, m->fw_off8, sizeof a.fw_off8);
 }
 
-// Activation workspace for `batch` rows: E [B][F*D], fo [B][F], X_0 [B][r4(F*D)], X_h and G_h [B][N].
+// The weight-gradient GEMM's grid for `batch` rows: 80 x 80 blocks per layer (per_split of them over all layers) in
+// `splits` batch splits of `rows` rows.  One workgroup per CU at most (tools/ubench_dw, Criteo-39, B = 4096: 3 splits
+// = 225 workgroups 42 us; 6 splits 47 us; past one round of workgroups 60+ us), each split over >= 128 rows.
+int dw_plan(const dfwfm_model* m, int64_t batch, int* per_split, int64_t* splits, int64_t* rows) {
+  const int edge = kDwEdge, quantum = kDwRows;
+  const int nnb = (m->N + edge - 1) / edge;
+  int ps = 0;
+  for (int l = 1; l <= m->H; ++l) ps += nnb * (((l == 1 ? m->F * m->D : m->N) + edge - 1) / edge);
+  *per_split = ps;
+  *splits = *rows = 0;
+  if (ps == 0 || batch <= 0) return DFWFM_OK;
+  int64_t sp = 256 / ps;
+  if (const char* ds = getenv("DFWFM_DW_SPLITS")) sp = atoi(ds);  // tuning only
+  const int64_t max_splits = (batch + 127) / 128;
+  if (sp > max_splits) sp = max_splits;
+  if (sp < 1) sp = 1;
+  // a wave's raw-buffer range (a quarter of a split's rows x the widest row, in bytes) must fit 31 bits
+  const int64_t wmax = r4(m->F * m->D) > m->N ? r4(m->F * m->D) : m->N;
+  const int64_t rows_cap = ((0x7fffffffLL / (wmax * 4)) * 4 - 4 * quantum) / quantum * quantum;
+  if (rows_cap < quantum) return fail(DFWFM_ERR_UNSUPPORTED, "MLP rows of %lld floats", (long long)wmax);
+  if ((batch + sp - 1) / sp > rows_cap) sp = (batch + rows_cap - 1) / rows_cap;
+  int64_t r = (batch + sp - 1) / sp;
+  r = (r + quantum - 1) / quantum * quantum;  // whole k-step groups per wave
+  *splits = (batch + r - 1) / r;
+  *rows = r;
+  return DFWFM_OK;
+}
+
+// Activation workspace for `batch` rows: E [B][F*D], fo [B][F], X_0 [B][r4(F*D)], X_h and G_h [B][N]; and the
+// weight-gradient GEMM's split slices and tickets.
 int ensure_workspace(dfwfm_model* m, int64_t batch) {
   if (batch <= m->ws_batch) return DFWFM_OK;
   const int64_t FD = (int64_t)m->F * m->D;
@@ -521,13 +555,25 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   const int64_t per_row = SE + FD + m->F + (m->H > 0 ? SE + 2 * (int64_t)m->H * m->N : 0);
   const int64_t red_blocks = (batch + kBM - 1) / kBM;
   const int64_t red_floats = red_blocks * red_outputs(m->F, m->D, m->N, m->num);
+  int per_split = 0;
+  int64_t splits = 0, rows = 0;
+  int rc = dw_plan(m, batch, &per_split, &splits, &rows);
+  if (rc != DFWFM_OK) return rc;
+  const int64_t slices = splits > 1 ? (int64_t)per_split * splits : 0;
+  const int64_t dw_floats = slices * (kDwEdge * kDwEdge + kDwEdge) + (per_split + 3);  // slices, db slices, tickets
   if (m->d_ws) (void)hipFree(m->d_ws);
   m->d_ws = nullptr;
   m->ws_batch = 0;
-  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_ws), sizeof(float) * (size_t)(per_row * batch + red_floats + 64)));
+  const size_t total = (size_t)(per_row * batch + red_floats + dw_floats + 64);
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_ws), sizeof(float) * total));
   // every array starts 16-byte aligned: the row counts are multiples of 4 or the offsets are padded
   auto al = [](int64_t x) { return (x + 3) & ~(int64_t)3; };
   float* p = m->d_ws;
+  m->dw_ticket = reinterpret_cast<int32_t*>(p);  p += al(per_split);
+  HIP_TRY(hipMemset(m->dw_ticket, 0, sizeof(int32_t) * (size_t)(per_split > 0 ? per_split : 1)));
+  m->dw_part = p;   p += slices * kDwEdge * kDwEdge;
+  m->dw_bpart = p;  p += al(slices * kDwEdge);
+  m->dw_slices = slices;
   m->sv_e = p;   p += al(SE * batch);
   m->sv_de = p;  p += al(FD * batch);
   m->red_part = p;  p += al(red_floats);
@@ -850,6 +896,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   m->trained = false;
   m->bwd_tables = false;
   m->bwd_fused_red = false;
+  m->bwd_loss_sum = nullptr;
   int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
   if (rc != DFWFM_OK) return rc;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(DFWFM_ERR_INVALID_ARG, "dropout_p outside [0, 1)");
@@ -989,6 +1036,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     if (e != hipSuccess) return hip_fail(e, "backward launch");
     m->bwd_tables = true;
     m->bwd_fused_red = fused_red;
+    m->bwd_loss_sum = (fused_red && bce) ? bce->loss_sum : nullptr;
   }
 
   // 2. dense shallow reductions: per 16-row tile, then summed over tiles.  When this call also runs the
@@ -1022,6 +1070,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     r.N = m->N;
     r.MT = m->MT;
     r.flags = m->flags;
+    r.loss_sum = fused_red ? m->bwd_loss_sum : nullptr;
     red_pending = fused_red && (phases & DFWFM_BWD_MLP_WEIGHTS) && H > 0 && (g->lin_w || g->lin_b) &&
                   !getenv("DFWFM_NO_DW_RED");
     if (!red_pending) {
@@ -1030,8 +1079,64 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     }
   }
 
-  // 3. categorical tables: privatised (LDS) tasks for small tables, atomic tasks for large ones
-  if ((phases & DFWFM_BWD_SCATTER) && g->fields) {
+  // 3. categorical tables.  Default: the deterministic sorted scatter (one task per field and row kind, both table
+  // families); DFWFM_SCATTER=atomic: the atomic scatter (privatised LDS tasks for small tables, global atomics for
+  // large ones), whose sums come in arrival order (A/B only)
+  const bool atomic_scatter = getenv("DFWFM_SCATTER") && !strcmp(getenv("DFWFM_SCATTER"), "atomic");
+  if ((phases & DFWFM_BWD_SCATTER) && g->fields && !atomic_scatter) {
+    SortScatterArgs sa;
+    memset(&sa, 0, sizeof sa);
+    sa.D = D;
+    sa.F = F;
+    sa.num = num;
+    sa.fields = m->d_fields;
+    sa.xi = m->t_xi;
+    sa.xi_stride = m->t_xs;
+    sa.batch = batch;
+    sa.sv_de = m->sv_de;
+    sa.dlogit = dlogit;
+    sa.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
+    const bool need2 = (m->flags & kNeedE) != 0, need1 = (m->flags & kFoTables) != 0;
+    auto add = [&](float* g2, float* g1, const float* o2, const float* o1, int64_t c, int f, int kind) -> int {
+      if (!need2) g2 = nullptr;
+      if (!need1) g1 = nullptr;
+      if (!g2 && !g1) return DFWFM_OK;
+      if (sa.ntasks == kSortScatterList) {
+        hipError_t er = launch_sort_scatter(sa, s);
+        if (er != hipSuccess) return hip_fail(er, "scatter launch");
+        sa.ntasks = 0;
+      }
+      SortScatterTask& t = sa.t[sa.ntasks++];
+      t.g2 = g2;
+      t.g1 = g1;
+      t.o2 = need2 ? o2 : nullptr;
+      t.o1 = need1 ? o1 : nullptr;
+      t.c = (int32_t)c;
+      t.field = (int16_t)f;
+      t.kind = (int8_t)kind;
+      t.pad = 0;
+      return DFWFM_OK;
+    };
+    int rc = DFWFM_OK;
+    for (int f = num; f < F && rc == DFWFM_OK; ++f) {
+      const FieldDev& fd = m->h_fields[f];
+      const dfwfm_field_grads& fg = g->fields[f];
+      if (fd.n > 0x7fffffffLL) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: table of more than 2^31 rows", f);
+      if (fd.c == 0) {
+        rc = add(fg.emb2, fg.emb1, nullptr, nullptr, 0, f, 0);
+      } else {
+        if (fd.c > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: QR collisions too large", f);
+        const bool mult = fd.op == 0;
+        rc = add(fg.emb2, fg.emb1, mult ? fd.emb2_r : nullptr, mult ? fd.emb1_r : nullptr, fd.c, f, 1);
+        if (rc == DFWFM_OK)
+          rc = add(fg.emb2_r, fg.emb1_r, mult ? fd.emb2 : nullptr, mult ? fd.emb1 : nullptr, fd.c, f, 2);
+      }
+    }
+    if (rc != DFWFM_OK) return rc;
+    e = launch_sort_scatter(sa, s);
+    if (e != hipSuccess) return hip_fail(e, "scatter launch");
+  }
+  if ((phases & DFWFM_BWD_SCATTER) && g->fields && atomic_scatter) {
     ScatterArgs priv, atom;
     memset(&priv, 0, sizeof priv);
     priv.D = D;
@@ -1117,7 +1222,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     memset(&d, 0, sizeof d);
     d.H = H;
     d.N = m->N;
-    const int edge = kDwEdge, quantum = kDwRows;
+    const int edge = kDwEdge;
     d.nnb = (m->N + edge - 1) / edge;
     d.batch = batch;
     int per_split = 0;
@@ -1132,24 +1237,19 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       per_split += d.nnb * d.nkb[l];
     }
     if (per_split > 0) {
-      // batch splits: one workgroup per CU at most (tools/ubench_dw, Criteo-39, B = 4096: 3 splits = 225
-      // workgroups 42 us; 6 splits 47 us; past one round of workgroups 60+ us), each over >= 128 rows
-      int64_t splits = 256 / per_split;
-      if (const char* ds = getenv("DFWFM_DW_SPLITS")) splits = atoi(ds);  // tuning only
-      const int64_t max_splits = (batch + 127) / 128;
-      if (splits > max_splits) splits = max_splits;
-      if (splits < 1) splits = 1;
-      // a wave's raw-buffer range (a quarter of a split's rows x the widest row, in bytes) must fit 31 bits
-      int64_t wmax = m->N;
-      for (int l = 1; l <= H; ++l) wmax = d.ldx[l] > wmax ? d.ldx[l] : wmax;
-      const int64_t rows_cap = ((0x7fffffffLL / (wmax * 4)) * 4 - 4 * quantum) / quantum * quantum;
-      if (rows_cap < quantum) return fail(DFWFM_ERR_UNSUPPORTED, "MLP rows of %lld floats", (long long)wmax);
-      if ((batch + splits - 1) / splits > rows_cap) splits = (batch + rows_cap - 1) / rows_cap;
-      int64_t rows = (batch + splits - 1) / splits;
-      rows = (rows + quantum - 1) / quantum * quantum;  // whole k-step groups per wave
-      splits = (batch + rows - 1) / rows;
+      // the split plan the workspace was sized for (over every layer's K blocks: per_split <= plan_blocks)
+      int plan_blocks = 0;
+      int64_t splits = 0, rows = 0;
+      int rc = dw_plan(m, batch, &plan_blocks, &splits, &rows);
+      if (rc != DFWFM_OK) return rc;
+      if (splits > 1 && (int64_t)per_split * splits > m->dw_slices)
+        return fail(DFWFM_ERR_STATE, "weight-gradient split slices: %lld needed, %lld allocated (DFWFM_DW_SPLITS "
+                    "changed after the workspace was sized?)", (long long)per_split * splits, (long long)m->dw_slices);
       d.splits = (int32_t)splits;
       d.rows_per_split = rows;
+      d.part = m->dw_part;
+      d.bpart = m->dw_bpart;
+      d.ticket = m->dw_ticket;
       d.blk0[1] = 0;
       for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
       e = red_pending ? launch_dw_reduce(d, d.blk0[H + 1], r, s) : launch_dw(d, d.blk0[H + 1], s);

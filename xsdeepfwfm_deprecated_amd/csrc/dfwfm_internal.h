@@ -209,12 +209,14 @@ struct RedArgs {
   float* g_num2[64];             // numerical field f: d v_f [D]
   float* g_num1[64];             // numerical field f: d w1_f [1]
   float* part;                   // [ceil(B/16)][red_outputs] per-tile partial sums (no atomics)
+  float* loss_sum;               // the per-tile BCE sums (last slot, the fused backward with the loss gradient) or null
   int32_t F, D, num, N, MT;
   int32_t flags;
 };
-// packed per-block outputs of the reduction: bias | lw[F] | fwlw[F*D] | R[F*F] | fc[N] | num2[num*D] | num1[num]
+// packed per-block outputs of the reduction: bias | lw[F] | fwlw[F*D] | R[F*F] | fc[N] | num2[num*D] | num1[num] |
+// the tile's loss (summed into loss_sum in tile order, like the gradients: the same bits on every run)
 __host__ __device__ inline int red_outputs(int F, int D, int N, int num) {
-  return 1 + F + F * D + F * F + N + num * D + num;
+  return 1 + F + F * D + F * F + N + num * D + num + 1;
 }
 
 // Embedding-table scatter: one task per (categorical field, table) with dense grads.  Tables of at
@@ -247,6 +249,39 @@ struct ScatterArgs {
   const float* lw;      // [F] or null (dfo = dlogit)
   int32_t chunk;        // samples per workgroup of a non-privatised task
 };
+
+// Deterministic table scatter (sort_scatter_kernel): one task per (categorical field, row kind) -- the rows a
+// field's samples hit in its plain table, or its QR quotient / remainder table -- covering both table families
+// (second order, width D; first order, width 1).  A workgroup sorts the batch's (row, sample) keys in LDS and sums
+// every row's contributions in a fixed order, so the gradients are the same bits on every run.
+constexpr int kSortSeg = 4096;      // samples sorted per pass (larger batches: passes in sample order)
+constexpr int kSortCh = 32;         // sorted positions per chunk of the segmented sums
+constexpr int kSortThreads = 1024;
+struct SortScatterTask {
+  float* g2;            // second-order table grad (width D) or null
+  float* g1;            // first-order table grad (width 1) or null
+  const float* o2;      // QR mult: the partner second-order table (its row multiplies the gradient) or null
+  const float* o1;      // QR mult: the partner first-order table or null
+  int32_t c;            // QR collisions (kind 1, 2)
+  int16_t field;        // model field index
+  int8_t kind;          // 0 plain row idx, 1 quotient row idx / c, 2 remainder row idx % c
+  int8_t pad;
+};
+static_assert(sizeof(SortScatterTask) == 40, "sort scatter task layout");
+constexpr int kSortScatterList = 64;  // tasks per launch (the list is a kernel argument, < 4 KiB)
+struct SortScatterArgs {
+  SortScatterTask t[kSortScatterList];
+  int32_t ntasks;
+  int32_t D, F, num;
+  const FieldDev* fields;
+  const int64_t* xi;
+  int64_t xi_stride;
+  int64_t batch;
+  const float* sv_de;
+  const float* dlogit;
+  const float* lw;      // [F] or null (dfo = dlogit)
+};
+size_t sort_scatter_lds_bytes(int D);
 
 // Touched-row gradients of one table family (dfwfm_sparse.hip): one task per categorical table.
 struct SparseTask {
@@ -322,6 +357,11 @@ struct DwArgs {
   int32_t H, N, nnb, splits;
   int64_t batch;
   int64_t rows_per_split;
+  // deterministic split-K (splits > 1): per (block, split) slices of the 80 x 80 block and of db, and a
+  // self-resetting ticket per block (zero when no launch is in flight); see dwr_block
+  float* part;
+  float* bpart;
+  int32_t* ticket;
 };
 
 // One tensor of a fused Adam step.
@@ -432,6 +472,7 @@ hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages
 hipError_t launch_reduce_final(const RedArgs& a, hipStream_t s);  // the second stage only (bwd_kernel red)
 hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s);
+hipError_t launch_sort_scatter(const SortScatterArgs& a, hipStream_t s);
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
                        float eps, float wd, float bc2_sqrt, hipStream_t s);
 // device-side step: state = {int64 step; float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt}

@@ -140,7 +140,10 @@ bwd_kernel(BwdArgs p) {
     float l = valid ? fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x))) : 0.f;
     if (valid) p.bce_dl[b0 + tid] = v_dl[0];
     l = sum16(l);
-    if (tid == 0 && p.loss_sum) atomicAdd(p.loss_sum, l);
+    // with the fused reductions the tile's loss is a partial like its gradients (reduce_final adds the tiles in
+    // order); else an atomic add
+    if (tid == 0 && red) p.part[(size_t)blockIdx.x * red_outputs(F, D, p.N, num) + red_outputs(F, D, p.N, num) - 1] = l;
+    else if (tid == 0 && p.loss_sum) atomicAdd(p.loss_sum, l);
   }
   stage_store<1>(v_dl, kBM, tid, NTH, get_dl, [&](int i, float v) { dl[i] = v; });
   stage_store<2>(v_fo, n_fo, tid, NTH, get_fo, [&](int i, float v) {
@@ -806,10 +809,11 @@ __device__ __forceinline__ void reduce_final_block(const RedArgs& a, int nblk, i
     dst = a.g_fc ? a.g_fc + i : nullptr;
   } else if ((i -= N) < numD) {
     dst = a.g_num2[i / D] ? a.g_num2[i / D] + i % D : nullptr;
-  } else {
-    i -= numD;
+  } else if ((i -= numD) < num) {
     dst = a.g_num1[i];
     if (lwp) scale = a.lw[i];
+  } else {
+    dst = a.loss_sum;  // the tiles' losses (only the fused backward with the loss gradient writes them)
   }
   if (dst) *dst += s * scale;
 }
@@ -927,6 +931,172 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
         if (at[u] >= 0) atomicAdd(T.g + at[u], v[u]);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic categorical-table scatter (the default; scatter_kernel's atomics add a row's contributions in
+// arrival order, so two runs of the same step differed in the last bits).  One workgroup per task (field, row kind),
+// both table families at once.  Per pass over <= kSortSeg samples:
+//   1. keys (row << 12 | sample) into LDS -- unique, so any correct sort gives the same order -- and each sample's
+//      QR partner row; 2. bitonic sort in LDS; 3. the sorted positions in chunks of kSortCh: a work item (component,
+//      chunk) walks its chunk's positions in order, summing each run of equal rows; a run that starts and ends inside
+//      the chunk is added to its row at once, a run cut by the chunk's start / end leaves its partial sum in LDS
+//      (lead / trail); 4. the chunk holding a cut run's head adds trail + the following chunks' leads in chunk
+//      order.  Every row is added by exactly one thread per pass (passes follow each other behind a barrier), in an
+//      order fixed by the sorted positions: the same bits on every run.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid) {
+  for (int k = 2; k <= np; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < (np >> 1); i += kSortThreads) {
+        const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+        const int hi = lo + j;
+        const bool asc = (lo & k) == 0;
+        const uint64_t x = key[lo], y = key[hi];
+        if ((x > y) == asc) {
+          key[lo] = y;
+          key[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__host__ __device__ inline int sort_scatter_nch() { return kSortSeg / kSortCh; }
+
+__global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterArgs a) {
+  constexpr int CH = kSortCh;
+  const int NCH = sort_scatter_nch();
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int D = a.D, FD = a.F * D, ncomp = D + 1;  // components: 0..D-1 second-order row, D first order
+  uint64_t* key = reinterpret_cast<uint64_t*>(smem);
+  int32_t* partv = reinterpret_cast<int32_t*>(key + kSortSeg);
+  float* lead = reinterpret_cast<float*>(partv + kSortSeg);  // [NCH][ncomp]
+  float* trail = lead + NCH * ncomp;
+  uint8_t* cflag = reinterpret_cast<uint8_t*>(trail + NCH * ncomp);  // bit 0: first run continues from the
+                                                                     // previous chunk, 1: last run continues into
+                                                                     // the next, 2: one run
+  const SortScatterTask T = a.t[blockIdx.x];
+  const FieldDev fd = a.fields[T.field];
+  const int f = T.field, col = f - a.num;
+  const float lwf = a.lw ? a.lw[f] : 1.f;
+  for (int64_t s0 = 0; s0 < a.batch; s0 += kSortSeg) {
+    const int n = (int)((a.batch - s0) < kSortSeg ? (a.batch - s0) : kSortSeg);
+    int np = 2;
+    while (np < n) np <<= 1;
+    for (int i = tid; i < np; i += kSortThreads) {
+      uint64_t k = ~0ull;
+      if (i < n) {
+        int64_t idx = a.xi[(s0 + i) * a.xi_stride + col];
+        if (idx < 0 || idx >= fd.n) idx = 0;  // the forward clamped (and flagged) it the same way
+        int64_t row = idx, part = 0;
+        if (T.kind == 1) {
+          row = idx / T.c;
+          part = idx - row * T.c;
+        } else if (T.kind == 2) {
+          part = idx / T.c;
+          row = idx - part * T.c;
+        }
+        k = ((uint64_t)row << 12) | (uint64_t)i;
+        partv[i] = (int32_t)part;
+      }
+      key[i] = k;
+    }
+    __syncthreads();
+    bitonic_sort_lds(key, np, tid);
+    const int nch = (n + CH - 1) / CH;
+    for (int c = tid; c < nch; c += kSortThreads) {
+      const int p0 = c * CH, p1 = (p0 + CH < n ? p0 + CH : n) - 1;
+      const uint64_t r0 = key[p0] >> 12, r1 = key[p1] >> 12;
+      const bool cin = p0 > 0 && (key[p0 - 1] >> 12) == r0;
+      const bool cout = p1 + 1 < n && (key[p1 + 1] >> 12) == r1;
+      cflag[c] = (uint8_t)((cin ? 1 : 0) | (cout ? 2 : 0) | (r0 == r1 ? 4 : 0));
+    }
+    __syncthreads();
+    // 3. runs inside each chunk; item = component-major, so a wave's items share their component (and table)
+    for (int it = tid; it < ncomp * nch; it += kSortThreads) {
+      const int j = it / nch, c = it - j * nch;
+      const bool fam2 = j < D;
+      float* g = fam2 ? T.g2 : T.g1;
+      if (!g) continue;
+      const int w = fam2 ? D : 1, jj = fam2 ? j : 0;
+      const float* o = fam2 ? T.o2 : T.o1;
+      const int p0 = c * CH, cnt = n - p0 < CH ? n - p0 : CH;
+      const int fl = cflag[c];
+      float v[CH];
+      uint32_t rw[CH];
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        v[q] = 0.f;
+        rw[q] = 0xffffffffu;
+        if (q < cnt) {
+          const uint64_t k = key[p0 + q];
+          const int sm = (int)(k & 4095);
+          rw[q] = (uint32_t)(k >> 12);
+          const int64_t b = s0 + sm;
+          float x = fam2 ? a.sv_de[b * FD + f * D + jj] : a.dlogit[b] * lwf;
+          if (o) x *= o[(int64_t)partv[sm] * w + jj];
+          v[q] = x;
+        }
+      }
+      float s = 0.f;
+      uint32_t cur = rw[0];
+      bool first = true;
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        if (q < cnt) {
+          if (rw[q] != cur) {  // a run ends inside the chunk
+            if (first && (fl & 1)) lead[c * ncomp + j] = s;
+            else atomicAdd(g + (int64_t)cur * w + jj, s);  // the row's only adder in this pass
+            first = false;
+            cur = rw[q];
+            s = 0.f;
+          }
+          s += v[q];
+        }
+      }
+      if (first && (fl & 1)) lead[c * ncomp + j] = s;  // continues from the previous chunk (maybe into the next)
+      else if (fl & 2) trail[c * ncomp + j] = s;     // its head is here, its tail in the next chunk(s)
+      else atomicAdd(g + (int64_t)cur * w + jj, s);
+    }
+    __syncthreads();
+    // 4. runs cut by chunk ends: the chunk with the head adds its trail and the following chunks' leads in order
+    for (int it = tid; it < ncomp * nch; it += kSortThreads) {
+      const int j = it / nch, c = it - j * nch;
+      const int fl = cflag[c];
+      if (!(fl & 2) || (fl & 5) == 5) continue;  // no run leaves this chunk, or it is not headed here
+      const bool fam2 = j < D;
+      float* g = fam2 ? T.g2 : T.g1;
+      if (!g) continue;
+      float s = trail[c * ncomp + j];
+      int c2 = c + 1;
+      while (true) {
+        s += lead[c2 * ncomp + j];
+        if ((cflag[c2] & 6) == 6) ++c2;  // one run that continues: the whole chunk belongs to the run
+        else break;
+      }
+      const int p1 = c * CH + CH - 1;  // a chunk with a continuing last run is full
+      const uint32_t row = (uint32_t)(key[p1] >> 12);
+      atomicAdd(g + (int64_t)row * (fam2 ? D : 1) + (fam2 ? j : 0), s);
+    }
+    __threadfence();
+    __syncthreads();  // the next pass's adds to the same rows come after these
+  }
+}
+
+size_t sort_scatter_lds_bytes(int D) {
+  const int NCH = sort_scatter_nch();
+  return (size_t)kSortSeg * 12 + (size_t)2 * NCH * (D + 1) * 4 + (size_t)NCH;
+}
+
+hipError_t launch_sort_scatter(const SortScatterArgs& a, hipStream_t s) {
+  if (a.ntasks <= 0 || a.batch <= 0) return hipSuccess;
+  const size_t lds = sort_scatter_lds_bytes(a.D);
+  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(sort_scatter_kernel), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(a.ntasks), dim3(kSortThreads), lds, s, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -1065,18 +1235,57 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
     }
   }
   __syncthreads();
-  if (gB && tid < kDwrT && n0 + tid < N) {
-    float b = bred[0][tid];
+  // Deterministic split-K: with one split the block is added to dW (and db) directly -- one writer per element.
+  // Otherwise every split writes its block to its own slice of a.part, and the LAST split to finish (a per-block
+  // ticket, reset by that split) sums the slices in split order and adds them: the same bits on every run (the
+  // split-K float atomics this replaces summed in arrival order).
+  constexpr int BE = kDwrT * kDwrT;
+  const int splits = a.splits;
+  const int ublk = a.blk0[l] / splits + rem;  // the block's index over all layers, without the split
+  float bsum = 0.f;
+  if (gB && tid < kDwrT) {
+    bsum = bred[0][tid];
 #pragma unroll
-    for (int w = 1; w < NW; ++w) b += bred[w][tid];
-    atomicAdd(gB + n0 + tid, b);
+    for (int w = 1; w < NW; ++w) bsum += bred[w][tid];
   }
+  if (splits > 1) {
+    float* mine = a.part + ((size_t)ublk * splits + split) * BE;
+    for (int e = tid; e < BE; e += 64 * NW) {
+      const int r = e / kDwrT, c = e - r * kDwrT;
+      mine[e] = red[0][r][c] + red[1][r][c];
+    }
+    if (gB && tid < kDwrT) a.bpart[((size_t)ublk * splits + split) * kDwrT + tid] = bsum;
+    __threadfence();  // this split's slices are visible device-wide before its ticket
+    __syncthreads();
+    __shared__ int s_last;
+    if (tid == 0) s_last = atomicAdd(a.ticket + ublk, 1) == splits - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: every other split's slices
+    if (tid == 0) a.ticket[ublk] = 0;  // ready for the next launch
+    const float* sl = a.part + (size_t)ublk * splits * BE;
+    if (gB && tid < kDwrT) {
+      const float* bp = a.bpart + (size_t)ublk * splits * kDwrT + tid;
+      float b = bp[0];
+      for (int sp = 1; sp < splits; ++sp) b += bp[sp * kDwrT];
+      if (n0 + tid < N) gB[n0 + tid] += b;
+    }
+    if (!gW) return;
+    for (int e = tid; e < BE; e += 64 * NW) {
+      const int r = e / kDwrT, c = e - r * kDwrT;
+      const int n = n0 + r, k = k0 + c;
+      float v = sl[e];
+      for (int sp = 1; sp < splits; ++sp) v += sl[sp * BE + e];
+      if (n < N && k < K) gW[(int64_t)n * K + k] += v;
+    }
+    return;
+  }
+  if (gB && tid < kDwrT && n0 + tid < N) gB[n0 + tid] += bsum;
   if (!gW) return;
-  // one atomic per element, consecutive lanes on consecutive k of a row (a wave's atomics cover 256 contiguous bytes)
-  for (int e = tid; e < kDwrT * kDwrT; e += 64 * NW) {
+  for (int e = tid; e < BE; e += 64 * NW) {
     const int r = e / kDwrT, c = e - r * kDwrT;
     const int n = n0 + r, k = k0 + c;
-    if (n < N && k < K) atomicAdd(gW + (int64_t)n * K + k, red[0][r][c] + red[1][r][c]);
+    if (n < N && k < K) gW[(int64_t)n * K + k] += red[0][r][c] + red[1][r][c];
   }
 }
 
