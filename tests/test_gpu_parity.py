@@ -205,6 +205,35 @@ def test_device_metrics_match_sklearn(gpu, n, levels, rate):
     assert m["n"] == n and m["positives"] == float((y == 1).sum())
 
 
+def test_device_metrics_deterministic_and_degenerate(gpu):
+    """The hand-written ranking (radix passes, scans) gives the same bits on every call (no float atomics), and the
+    degenerate cases match sklearn: one sample, every prediction tied, tiles ending inside a tie group."""
+    from sklearn.metrics import auc, precision_recall_curve, roc_auc_score
+    from xsdeepfwfm_deprecated_amd.metrics import DeviceMetrics
+    dm = DeviceMetrics(gpu)
+    rng = np.random.default_rng(9)
+    n = 3 * 4096 + 77
+    z = np.round(rng.normal(size=n) * 3).astype(np.float32)  # 20-odd distinct values: groups span many tiles
+    y = (rng.random(n) < 1 / (1 + np.exp(-z))).astype(np.float32)
+    zt, yt = torch.from_numpy(z).to(gpu), torch.from_numpy(y).to(gpu)
+    a, b = dm(zt, yt), dm(zt, yt)
+    assert a == b
+    pred = torch.sigmoid(torch.from_numpy(z)).numpy().astype("float64")
+    assert a["distinct_predictions"] == len(np.unique(pred))
+    assert abs(a["auc"] - roc_auc_score(y, pred)) < 1e-12
+    prec, rec, _ = precision_recall_curve(y, pred)
+    assert abs(a["prauc"] - auc(rec, prec)) < 1e-12
+    # every prediction tied: one group, AUC 0.5
+    zc = torch.full((5000,), 0.25, device=gpu)
+    yc = torch.from_numpy((np.arange(5000) % 7 == 0).astype(np.float32)).to(gpu)
+    c = dm(zc, yc)
+    assert c["distinct_predictions"] == 1 and abs(c["auc"] - 0.5) < 1e-15
+    prec, rec, _ = precision_recall_curve(yc.cpu().numpy(), np.full(5000, 0.5))
+    assert abs(c["prauc"] - auc(rec, prec)) < 1e-12
+    one = dm(torch.tensor([0.3], device=gpu), torch.tensor([1.0], device=gpu))
+    assert one["n"] == 1 and one["positives"] == 1 and one["distinct_predictions"] == 1
+
+
 def test_eval_by_batch_matches_reference_auc(gpu):
     """eval_by_batch (device logits + device metrics) reproduces the reference's AUC on tiny-criteo."""
     cfg, params, xi, xv, y, l32, l64, auc_ref = load_golden("tiny_deepfwfm_lw")

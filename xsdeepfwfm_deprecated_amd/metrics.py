@@ -1,7 +1,7 @@
 """Evaluation metrics of the reference harness (model/DeepFMs.py:22, 781-800).
 
 * ``DeviceMetrics``: AUC, PR-AUC, log-loss, RCE and CTR of a whole evaluation set on the device
-  (C ABI ``dfwfm_eval_metrics``: one radix sort + scans, sklearn 1.7 definitions) -- what
+  (C ABI ``dfwfm_eval_metrics``: a hand-written radix ranking + scans, sklearn 1.7 definitions, the same bits every call) -- what
   ``DeepFMs.eval_by_batch`` uses; a single 64-byte copy back per evaluation.
 * ``roc_auc_score`` / ``prauc`` / ``rce`` / ``ctr``: the reference's host functions (sklearn), kept for
   the reference API (``eval_metric`` default, ``compute_prauc``, ``compute_rce``) on host arrays.
