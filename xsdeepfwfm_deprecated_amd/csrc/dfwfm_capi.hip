@@ -1083,9 +1083,13 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   // families); DFWFM_SCATTER=atomic: the atomic scatter (privatised LDS tasks for small tables, global atomics for
   // large ones), whose sums come in arrival order (A/B only)
   const bool atomic_scatter = getenv("DFWFM_SCATTER") && !strcmp(getenv("DFWFM_SCATTER"), "atomic");
+  // the sorted scatter's last tasks ride in the weight-gradient GEMM's launch when this call runs both (the scatter's
+  // workgroups take the CUs the GEMM's one round leaves idle); DFWFM_SCATTER_MERGE=0: separate launches (A/B)
+  const bool merge_scatter = (phases & DFWFM_BWD_MLP_WEIGHTS) && H > 0 && (g->lin_w || g->lin_b) &&
+                             !(getenv("DFWFM_SCATTER_MERGE") && atoi(getenv("DFWFM_SCATTER_MERGE")) == 0);
+  SortScatterArgs sa;
+  memset(&sa, 0, sizeof sa);
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && !atomic_scatter) {
-    SortScatterArgs sa;
-    memset(&sa, 0, sizeof sa);
     sa.D = D;
     sa.F = F;
     sa.num = num;
@@ -1133,8 +1137,11 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       }
     }
     if (rc != DFWFM_OK) return rc;
-    e = launch_sort_scatter(sa, s);
-    if (e != hipSuccess) return hip_fail(e, "scatter launch");
+    if (!merge_scatter) {
+      e = launch_sort_scatter(sa, s);
+      if (e != hipSuccess) return hip_fail(e, "scatter launch");
+      sa.ntasks = 0;
+    }
   }
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && atomic_scatter) {
     ScatterArgs priv, atom;
@@ -1252,10 +1259,19 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       d.ticket = m->dw_ticket;
       d.blk0[1] = 0;
       for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
-      e = red_pending ? launch_dw_reduce(d, d.blk0[H + 1], r, s) : launch_dw(d, d.blk0[H + 1], s);
+      if (sa.ntasks > 0) {
+        e = launch_dw_scatter(d, d.blk0[H + 1], red_pending ? &r : nullptr, sa, s);
+        sa.ntasks = 0;
+      } else {
+        e = red_pending ? launch_dw_reduce(d, d.blk0[H + 1], r, s) : launch_dw(d, d.blk0[H + 1], s);
+      }
       if (e != hipSuccess) return hip_fail(e, "dw launch");
       red_pending = false;
     }
+  }
+  if (sa.ntasks > 0) {  // the GEMM had nothing to do: the held-back scatter tasks on their own
+    e = launch_sort_scatter(sa, s);
+    if (e != hipSuccess) return hip_fail(e, "scatter launch");
   }
   if (red_pending) {
     e = launch_reduce_final(r, s);

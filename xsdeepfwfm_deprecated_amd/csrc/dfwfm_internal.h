@@ -268,7 +268,7 @@ struct SortScatterTask {
   int8_t pad;
 };
 static_assert(sizeof(SortScatterTask) == 40, "sort scatter task layout");
-constexpr int kSortScatterList = 64;  // tasks per launch (the list is a kernel argument, < 4 KiB)
+constexpr int kSortScatterList = 32;  // tasks per launch (a kernel argument: beside DwArgs + RedArgs, < 4 KiB)
 struct SortScatterArgs {
   SortScatterTask t[kSortScatterList];
   int32_t ntasks;
@@ -473,6 +473,9 @@ hipError_t launch_reduce_final(const RedArgs& a, hipStream_t s);  // the second 
 hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_sort_scatter(const SortScatterArgs& a, hipStream_t s);
+// one launch: the scatter tasks of sa, the weight-gradient GEMM, and (r non-null) the reductions' final sums
+hipError_t launch_dw_scatter(const DwArgs& a, int total_blocks, const RedArgs* r, const SortScatterArgs& sa,
+                             hipStream_t s);
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
                        float eps, float wd, float bc2_sqrt, hipStream_t s);
 // device-side step: state = {int64 step; float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt}

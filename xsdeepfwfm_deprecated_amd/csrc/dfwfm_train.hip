@@ -16,6 +16,7 @@
 //   adam_kernel     torch.optim.Adam's update (coupled L2, bias correction) over a tensor list.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "dfwfm_device.h"
 #include "dfwfm_internal.h"
@@ -997,10 +998,11 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 //      order.  Every row is added by exactly one thread per pass (passes follow each other behind a barrier), in an
 //      order fixed by the sorted positions: the same bits on every run.
 // ---------------------------------------------------------------------------
+template <int NTH>
 __device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid) {
   for (int k = 2; k <= np; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < (np >> 1); i += kSortThreads) {
+      for (int i = tid; i < (np >> 1); i += NTH) {
         const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
         const int hi = lo + j;
         const bool asc = (lo & k) == 0;
@@ -1016,10 +1018,11 @@ __device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid)
 
 __host__ __device__ inline int sort_scatter_nch() { return kSortSeg / kSortCh; }
 
-__global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterArgs a) {
+// one task (a.t[task]) by a workgroup of NTH threads, in smem (sort_scatter_lds_bytes)
+template <int NTH>
+__device__ __forceinline__ void sort_scatter_block(const SortScatterArgs& a, int task, float* smem) {
   constexpr int CH = kSortCh;
   const int NCH = sort_scatter_nch();
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int D = a.D, FD = a.F * D, ncomp = D + 1;  // components: 0..D-1 second-order row, D first order
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
@@ -1029,7 +1032,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
   uint8_t* cflag = reinterpret_cast<uint8_t*>(trail + NCH * ncomp);  // bit 0: first run continues from the
                                                                      // previous chunk, 1: last run continues into
                                                                      // the next, 2: one run
-  const SortScatterTask T = a.t[blockIdx.x];
+  const SortScatterTask T = a.t[task];
   const FieldDev fd = a.fields[T.field];
   const int f = T.field, col = f - a.num;
   const float lwf = a.lw ? a.lw[f] : 1.f;
@@ -1037,7 +1040,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
     const int n = (int)((a.batch - s0) < kSortSeg ? (a.batch - s0) : kSortSeg);
     int np = 2;
     while (np < n) np <<= 1;
-    for (int i = tid; i < np; i += kSortThreads) {
+    for (int i = tid; i < np; i += NTH) {
       uint64_t k = ~0ull;
       if (i < n) {
         int64_t idx = a.xi[(s0 + i) * a.xi_stride + col];
@@ -1056,9 +1059,9 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
       key[i] = k;
     }
     __syncthreads();
-    bitonic_sort_lds(key, np, tid);
+    bitonic_sort_lds<NTH>(key, np, tid);
     const int nch = (n + CH - 1) / CH;
-    for (int c = tid; c < nch; c += kSortThreads) {
+    for (int c = tid; c < nch; c += NTH) {
       const int p0 = c * CH, p1 = (p0 + CH < n ? p0 + CH : n) - 1;
       const uint64_t r0 = key[p0] >> 12, r1 = key[p1] >> 12;
       const bool cin = p0 > 0 && (key[p0 - 1] >> 12) == r0;
@@ -1067,7 +1070,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
     }
     __syncthreads();
     // 3. runs inside each chunk; item = component-major, so a wave's items share their component (and table)
-    for (int it = tid; it < ncomp * nch; it += kSortThreads) {
+    for (int it = tid; it < ncomp * nch; it += NTH) {
       const int j = it / nch, c = it - j * nch;
       const bool fam2 = j < D;
       float* g = fam2 ? T.g2 : T.g1;
@@ -1114,7 +1117,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
     }
     __syncthreads();
     // 4. runs cut by chunk ends: the chunk with the head adds its trail and the following chunks' leads in order
-    for (int it = tid; it < ncomp * nch; it += kSortThreads) {
+    for (int it = tid; it < ncomp * nch; it += NTH) {
       const int j = it / nch, c = it - j * nch;
       const int fl = cflag[c];
       if (!(fl & 2) || (fl & 5) == 5) continue;  // no run leaves this chunk, or it is not headed here
@@ -1135,6 +1138,11 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
     __threadfence();
     __syncthreads();  // the next pass's adds to the same rows come after these
   }
+}
+
+__global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  sort_scatter_block<kSortThreads>(a, blockIdx.x, smem);
 }
 
 size_t sort_scatter_lds_bytes(int D) {
@@ -1355,6 +1363,22 @@ __global__ void __launch_bounds__(64 * NW) dwr_reduce_kernel(DwArgs a, RedArgs r
     dwr_block<kDwrP, NW>(a, blockIdx.x);
   else
     reduce_final_block(r, nblk, (int)blockIdx.x - dw_blocks);
+}
+
+// The backward's last launch of the one-stream step: the table scatter's tasks (one 256-thread workgroup each, first:
+// they take their CUs while the weight-gradient GEMM's one round of workgroups takes the others), the GEMM, then the
+// shallow reductions' final sums.  Independent outputs; a dependency-free way to overlap the scatter with the GEMM.
+template <int kDwrP, int NW>
+__global__ void __launch_bounds__(64 * NW) dwr_scatter_kernel(DwArgs a, RedArgs r, SortScatterArgs sa, int nblk,
+                                                              int dw_blocks) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int bid = (int)blockIdx.x;
+  if (bid < sa.ntasks)
+    sort_scatter_block<64 * NW>(sa, bid, smem);
+  else if (bid < sa.ntasks + dw_blocks)
+    dwr_block<kDwrP, NW>(a, bid - sa.ntasks);
+  else if (r.part)
+    reduce_final_block(r, nblk, bid - sa.ntasks - dw_blocks);
 }
 
 // ---------------------------------------------------------------------------
@@ -1638,6 +1662,30 @@ hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r,
   const int rblocks = (P + 63) / 64;
   hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(total_blocks + rblocks), dim3(256), 0, s, a, r, nblk,
                      total_blocks);
+  return hipGetLastError();
+}
+
+hipError_t launch_dw_scatter(const DwArgs& a, int total_blocks, const RedArgs* r, const SortScatterArgs& sa,
+                             hipStream_t s) {
+  const int64_t q = a.rows_per_split / 4 + 4;
+  for (int l = 1; l <= a.H; ++l) {
+    const int64_t w = a.ldx[l] > a.N ? a.ldx[l] : a.N;
+    if (q * w * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
+  }
+  RedArgs rr;
+  int rblocks = 0, nblk = 0;
+  if (r) {
+    rr = *r;
+    nblk = (int)((r->batch + kBM - 1) / kBM);
+    rblocks = (red_outputs(r->F, r->D, r->N, r->num) + 63) / 64;
+  } else {
+    memset(&rr, 0, sizeof rr);
+  }
+  const size_t lds = sort_scatter_lds_bytes(sa.D);
+  auto k = dwr_scatter_kernel<4, 4>;
+  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3(sa.ntasks + total_blocks + rblocks), dim3(256), lds, s, a, rr, sa, nblk, total_blocks);
   return hipGetLastError();
 }
 
