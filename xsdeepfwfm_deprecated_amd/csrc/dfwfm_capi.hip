@@ -77,7 +77,6 @@ struct dfwfm_model {
   float* red_part;        // per-16-row-tile partial sums of the shallow reductions
   float* dw_part;         // weight-gradient GEMM: per (block, split) slices (deterministic split-K, dwr_block)
   float* dw_bpart;
-  int32_t* dw_ticket;     // per block, zero between launches
   int64_t dw_slices;      // blocks x splits the slices hold
   FieldDev h_fields[64];  // host copy of the field descriptors (scatter task planning)
   // the last dfwfm_train_forward, replayed by dfwfm_backward
@@ -547,7 +546,7 @@ int dw_plan(const dfwfm_model* m, int64_t batch, int* per_split, int64_t* splits
 }
 
 // Activation workspace for `batch` rows: E [B][F*D], fo [B][F], X_0 [B][r4(F*D)], X_h and G_h [B][N]; and the
-// weight-gradient GEMM's split slices and tickets.
+// weight-gradient GEMM's split slices.
 int ensure_workspace(dfwfm_model* m, int64_t batch) {
   if (batch <= m->ws_batch) return DFWFM_OK;
   const int64_t FD = (int64_t)m->F * m->D;
@@ -560,7 +559,7 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   int rc = dw_plan(m, batch, &per_split, &splits, &rows);
   if (rc != DFWFM_OK) return rc;
   const int64_t slices = splits > 1 ? (int64_t)per_split * splits : 0;
-  const int64_t dw_floats = slices * (kDwEdge * kDwEdge + kDwEdge) + (per_split + 3);  // slices, db slices, tickets
+  const int64_t dw_floats = slices * (kDwEdge * kDwEdge + kDwEdge);  // the blocks' and the bias sums' slices
   if (m->d_ws) (void)hipFree(m->d_ws);
   m->d_ws = nullptr;
   m->ws_batch = 0;
@@ -569,8 +568,6 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   // every array starts 16-byte aligned: the row counts are multiples of 4 or the offsets are padded
   auto al = [](int64_t x) { return (x + 3) & ~(int64_t)3; };
   float* p = m->d_ws;
-  m->dw_ticket = reinterpret_cast<int32_t*>(p);  p += al(per_split);
-  HIP_TRY(hipMemset(m->dw_ticket, 0, sizeof(int32_t) * (size_t)(per_split > 0 ? per_split : 1)));
   m->dw_part = p;   p += slices * kDwEdge * kDwEdge;
   m->dw_bpart = p;  p += al(slices * kDwEdge);
   m->dw_slices = slices;
@@ -1256,7 +1253,6 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       d.rows_per_split = rows;
       d.part = m->dw_part;
       d.bpart = m->dw_bpart;
-      d.ticket = m->dw_ticket;
       d.blk0[1] = 0;
       for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
       if (sa.ntasks > 0) {

@@ -357,11 +357,10 @@ struct DwArgs {
   int32_t H, N, nnb, splits;
   int64_t batch;
   int64_t rows_per_split;
-  // deterministic split-K (splits > 1): per (block, split) slices of the 80 x 80 block and of db, and a
-  // self-resetting ticket per block (zero when no launch is in flight); see dwr_block
+  // deterministic split-K (splits > 1): per (block, split) slices of the 80 x 80 block and of db, added in split
+  // order by dw_sum_kernel; see dwr_block
   float* part;
   float* bpart;
-  int32_t* ticket;
 };
 
 // One tensor of a fused Adam step.

@@ -1069,12 +1069,24 @@ __device__ __forceinline__ void sort_scatter_block(const SortScatterArgs& a, int
       cflag[c] = (uint8_t)((cin ? 1 : 0) | (cout ? 2 : 0) | (r0 == r1 ? 4 : 0));
     }
     __syncthreads();
-    // 3. runs inside each chunk; item = component-major, so a wave's items share their component (and table)
-    for (int it = tid; it < ncomp * nch; it += NTH) {
-      const int j = it / nch, c = it - j * nch;
+    // 3. runs inside each chunk.  Items: (chunk, d) of the second-order family with d fastest -- the lanes of one
+    // chunk read one sample's 40-byte dE row per position and add one 40-byte table row per run: coalesced -- then
+    // one item per chunk for the first-order family
+    const int n2 = T.g2 ? nch * D : 0, n1 = T.g1 ? nch : 0;
+    auto item = [&](int it, int& c, int& j) {
+      if (it < n2) {
+        c = it / D;
+        j = it - c * D;
+      } else {
+        c = it - n2;
+        j = D;
+      }
+    };
+    for (int it = tid; it < n2 + n1; it += NTH) {
+      int c, j;
+      item(it, c, j);
       const bool fam2 = j < D;
       float* g = fam2 ? T.g2 : T.g1;
-      if (!g) continue;
       const int w = fam2 ? D : 1, jj = fam2 ? j : 0;
       const float* o = fam2 ? T.o2 : T.o1;
       const int p0 = c * CH, cnt = n - p0 < CH ? n - p0 : CH;
@@ -1117,13 +1129,13 @@ __device__ __forceinline__ void sort_scatter_block(const SortScatterArgs& a, int
     }
     __syncthreads();
     // 4. runs cut by chunk ends: the chunk with the head adds its trail and the following chunks' leads in order
-    for (int it = tid; it < ncomp * nch; it += NTH) {
-      const int j = it / nch, c = it - j * nch;
+    for (int it = tid; it < n2 + n1; it += NTH) {
+      int c, j;
+      item(it, c, j);
       const int fl = cflag[c];
       if (!(fl & 2) || (fl & 5) == 5) continue;  // no run leaves this chunk, or it is not headed here
       const bool fam2 = j < D;
       float* g = fam2 ? T.g2 : T.g1;
-      if (!g) continue;
       float s = trail[c * ncomp + j];
       int c2 = c + 1;
       while (true) {
@@ -1135,8 +1147,10 @@ __device__ __forceinline__ void sort_scatter_block(const SortScatterArgs& a, int
       const uint32_t row = (uint32_t)(key[p1] >> 12);
       atomicAdd(g + (int64_t)row * (fam2 ? D : 1) + (fam2 ? j : 0), s);
     }
-    __threadfence();
-    __syncthreads();  // the next pass's adds to the same rows come after these
+    // the next pass's adds to the same rows come after these (this workgroup's own atomics, retired before the
+    // barrier; no device-scope fence: nothing another workgroup reads)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
   }
 }
 
@@ -1296,9 +1310,9 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
   }
   __syncthreads();
   // Deterministic split-K: with one split the block is added to dW (and db) directly -- one writer per element.
-  // Otherwise every split writes its block to its own slice of a.part, and the LAST split to finish (a per-block
-  // ticket, reset by that split) sums the slices in split order and adds them: the same bits on every run (the
-  // split-K float atomics this replaces summed in arrival order).
+  // Otherwise every split writes its block to its own slice of a.part and the next launch (dw_sum_kernel) adds the
+  // slices in split order: the same bits on every run (the split-K float atomics this replaces summed in arrival
+  // order; a last-split ticket needs device-scope fences, whose L2 write-backs cost more than the launch).
   constexpr int BE = kDwrT * kDwrT;
   const int splits = a.splits;
   const int ublk = a.blk0[l] / splits + rem;  // the block's index over all layers, without the split
@@ -1309,35 +1323,13 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
     for (int w = 1; w < NW; ++w) bsum += bred[w][tid];
   }
   if (splits > 1) {
+    // this split's block and column sums to its slices; dw_sum_kernel adds the slices in split order
     float* mine = a.part + ((size_t)ublk * splits + split) * BE;
     for (int e = tid; e < BE; e += 64 * NW) {
       const int r = e / kDwrT, c = e - r * kDwrT;
       mine[e] = red[0][r][c] + red[1][r][c];
     }
     if (gB && tid < kDwrT) a.bpart[((size_t)ublk * splits + split) * kDwrT + tid] = bsum;
-    __threadfence();  // this split's slices are visible device-wide before its ticket
-    __syncthreads();
-    __shared__ int s_last;
-    if (tid == 0) s_last = atomicAdd(a.ticket + ublk, 1) == splits - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();  // acquire: every other split's slices
-    if (tid == 0) a.ticket[ublk] = 0;  // ready for the next launch
-    const float* sl = a.part + (size_t)ublk * splits * BE;
-    if (gB && tid < kDwrT) {
-      const float* bp = a.bpart + (size_t)ublk * splits * kDwrT + tid;
-      float b = bp[0];
-      for (int sp = 1; sp < splits; ++sp) b += bp[sp * kDwrT];
-      if (n0 + tid < N) gB[n0 + tid] += b;
-    }
-    if (!gW) return;
-    for (int e = tid; e < BE; e += 64 * NW) {
-      const int r = e / kDwrT, c = e - r * kDwrT;
-      const int n = n0 + r, k = k0 + c;
-      float v = sl[e];
-      for (int sp = 1; sp < splits; ++sp) v += sl[sp * BE + e];
-      if (n < N && k < K) gW[(int64_t)n * K + k] += v;
-    }
     return;
   }
   if (gB && tid < kDwrT && n0 + tid < N) gB[n0 + tid] += bsum;
@@ -1352,6 +1344,42 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
 template <int kDwrP, int NW>
 __global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
   dwr_block<kDwrP, NW>(a, blockIdx.x);
+}
+
+// the split slices of every weight / bias gradient element added in split order (the GEMM's second launch when it
+// splits the batch): one thread per element of dW_l (then of db_l), layer by layer
+__global__ void __launch_bounds__(256) dw_sum_kernel(DwArgs a, int64_t total) {
+  constexpr int BE = kDwrT * kDwrT;
+  const int splits = a.splits;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    int64_t i = e;
+    int l = 1;
+    // weights of layer l (N x K), then its bias (N)
+    for (; l <= a.H; ++l) {
+      const int64_t nw = a.gW[l] ? (int64_t)a.N * a.K[l] : 0, nb = a.gB[l] ? a.N : 0;
+      if (i < nw + nb) break;
+      i -= nw + nb;
+    }
+    if (l > a.H) return;
+    const int64_t nw = a.gW[l] ? (int64_t)a.N * a.K[l] : 0;
+    const int ub0 = a.blk0[l] / splits;
+    if (i < nw) {
+      const int n = (int)(i / a.K[l]), k = (int)(i - (int64_t)n * a.K[l]);
+      const int nb = n / kDwrT, kb = k / kDwrT;
+      const float* sl = a.part + ((size_t)(ub0 + nb * a.nkb[l] + kb) * splits) * BE + (n - nb * kDwrT) * kDwrT +
+                        (k - kb * kDwrT);
+      float v = sl[0];
+      for (int sp = 1; sp < splits; ++sp) v += sl[(size_t)sp * BE];
+      a.gW[l][i] += v;
+    } else {
+      const int n = (int)(i - nw);
+      const int nb = n / kDwrT;
+      const float* bp = a.bpart + ((size_t)(ub0 + nb * a.nkb[l]) * splits) * kDwrT + (n - nb * kDwrT);
+      float v = bp[0];
+      for (int sp = 1; sp < splits; ++sp) v += bp[(size_t)sp * kDwrT];
+      a.gB[l][n] += v;
+    }
+  }
 }
 
 // The weight-gradient GEMM and the shallow reductions' final sums as ONE launch (the one-stream step): the GEMM is
@@ -1638,6 +1666,16 @@ hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream
   return hipGetLastError();
 }
 
+static hipError_t launch_dw_sum(const DwArgs& a, hipStream_t s) {
+  if (a.splits <= 1) return hipSuccess;
+  int64_t total = 0;
+  for (int l = 1; l <= a.H; ++l) total += (a.gW[l] ? (int64_t)a.N * a.K[l] : 0) + (a.gB[l] ? a.N : 0);
+  if (total <= 0) return hipSuccess;
+  const int64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(dw_sum_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s, a, total);
+  return hipGetLastError();
+}
+
 hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
   if (total_blocks <= 0) return hipSuccess;
   // a wave's raw-buffer ranges and k-step offsets are 32-bit byte counts over its quarter of a split's rows
@@ -1647,7 +1685,8 @@ hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
     if (q * w * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(total_blocks), dim3(256), 0, s, a);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  return e != hipSuccess ? e : launch_dw_sum(a, s);
 }
 
 hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r, hipStream_t s) {
@@ -1662,7 +1701,8 @@ hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r,
   const int rblocks = (P + 63) / 64;
   hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(total_blocks + rblocks), dim3(256), 0, s, a, r, nblk,
                      total_blocks);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  return e != hipSuccess ? e : launch_dw_sum(a, s);
 }
 
 hipError_t launch_dw_scatter(const DwArgs& a, int total_blocks, const RedArgs* r, const SortScatterArgs& sa,
@@ -1686,7 +1726,8 @@ hipError_t launch_dw_scatter(const DwArgs& a, int total_blocks, const RedArgs* r
   hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3(sa.ntasks + total_blocks + rblocks), dim3(256), lds, s, a, rr, sa, nblk, total_blocks);
-  return hipGetLastError();
+  e = hipGetLastError();
+  return e != hipSuccess ? e : launch_dw_sum(a, s);
 }
 
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
