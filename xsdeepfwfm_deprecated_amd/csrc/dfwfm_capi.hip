@@ -1080,13 +1080,10 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   // families); DFWFM_SCATTER=atomic: the atomic scatter (privatised LDS tasks for small tables, global atomics for
   // large ones), whose sums come in arrival order (A/B only)
   const bool atomic_scatter = getenv("DFWFM_SCATTER") && !strcmp(getenv("DFWFM_SCATTER"), "atomic");
-  // the sorted scatter's last tasks ride in the weight-gradient GEMM's launch when this call runs both (the scatter's
-  // workgroups take the CUs the GEMM's one round leaves idle); DFWFM_SCATTER_MERGE=0: separate launches (A/B)
-  const bool merge_scatter = (phases & DFWFM_BWD_MLP_WEIGHTS) && H > 0 && (g->lin_w || g->lin_b) &&
-                             !(getenv("DFWFM_SCATTER_MERGE") && atoi(getenv("DFWFM_SCATTER_MERGE")) == 0);
-  SortScatterArgs sa;
-  memset(&sa, 0, sizeof sa);
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && !atomic_scatter) {
+    SortScatterArgs sa;
+    memset(&sa, 0, sizeof sa);
+    int sblocks = 0;
     sa.D = D;
     sa.F = F;
     sa.num = num;
@@ -1098,16 +1095,24 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     sa.dlogit = dlogit;
     sa.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
     const bool need2 = (m->flags & kNeedE) != 0, need1 = (m->flags & kFoTables) != 0;
-    auto add = [&](float* g2, float* g1, const float* o2, const float* o1, int64_t c, int f, int kind) -> int {
+    auto add = [&](float* g2, float* g1, const float* o2, const float* o1, int64_t c, int f, int kind,
+                   int64_t rows) -> int {
       if (!need2) g2 = nullptr;
       if (!need1) g1 = nullptr;
       if (!g2 && !g1) return DFWFM_OK;
       if (sa.ntasks == kSortScatterList) {
-        hipError_t er = launch_sort_scatter(sa, s);
+        hipError_t er = launch_sort_scatter(sa, sblocks, s);
         if (er != hipSuccess) return hip_fail(er, "scatter launch");
         sa.ntasks = 0;
+        sblocks = 0;
       }
       SortScatterTask& t = sa.t[sa.ntasks++];
+      // row buckets, one workgroup each: a few hundred samples per bucket for the large tables (4096 rows sort in
+      // 78 dependent LDS stages on one CU; eight buckets of ~512 in 45 shorter ones, on eight)
+      t.nbuck = (int8_t)(rows >= 64 ? 8 : rows >= 16 ? 4 : rows >= 4 ? 2 : 1);
+      t.block0 = sblocks;
+      t.pad = 0;
+      sblocks += t.nbuck;
       t.g2 = g2;
       t.g1 = g1;
       t.o2 = need2 ? o2 : nullptr;
@@ -1115,7 +1120,6 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       t.c = (int32_t)c;
       t.field = (int16_t)f;
       t.kind = (int8_t)kind;
-      t.pad = 0;
       return DFWFM_OK;
     };
     int rc = DFWFM_OK;
@@ -1124,21 +1128,19 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       const dfwfm_field_grads& fg = g->fields[f];
       if (fd.n > 0x7fffffffLL) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: table of more than 2^31 rows", f);
       if (fd.c == 0) {
-        rc = add(fg.emb2, fg.emb1, nullptr, nullptr, 0, f, 0);
+        rc = add(fg.emb2, fg.emb1, nullptr, nullptr, 0, f, 0, fd.n);
       } else {
         if (fd.c > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: QR collisions too large", f);
         const bool mult = fd.op == 0;
-        rc = add(fg.emb2, fg.emb1, mult ? fd.emb2_r : nullptr, mult ? fd.emb1_r : nullptr, fd.c, f, 1);
+        rc = add(fg.emb2, fg.emb1, mult ? fd.emb2_r : nullptr, mult ? fd.emb1_r : nullptr, fd.c, f, 1,
+                 (fd.n + fd.c - 1) / fd.c);
         if (rc == DFWFM_OK)
-          rc = add(fg.emb2_r, fg.emb1_r, mult ? fd.emb2 : nullptr, mult ? fd.emb1 : nullptr, fd.c, f, 2);
+          rc = add(fg.emb2_r, fg.emb1_r, mult ? fd.emb2 : nullptr, mult ? fd.emb1 : nullptr, fd.c, f, 2, fd.c);
       }
     }
     if (rc != DFWFM_OK) return rc;
-    if (!merge_scatter) {
-      e = launch_sort_scatter(sa, s);
-      if (e != hipSuccess) return hip_fail(e, "scatter launch");
-      sa.ntasks = 0;
-    }
+    e = launch_sort_scatter(sa, sblocks, s);
+    if (e != hipSuccess) return hip_fail(e, "scatter launch");
   }
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && atomic_scatter) {
     ScatterArgs priv, atom;
@@ -1255,19 +1257,10 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       d.bpart = m->dw_bpart;
       d.blk0[1] = 0;
       for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
-      if (sa.ntasks > 0) {
-        e = launch_dw_scatter(d, d.blk0[H + 1], red_pending ? &r : nullptr, sa, s);
-        sa.ntasks = 0;
-      } else {
-        e = red_pending ? launch_dw_reduce(d, d.blk0[H + 1], r, s) : launch_dw(d, d.blk0[H + 1], s);
-      }
+      e = red_pending ? launch_dw_reduce(d, d.blk0[H + 1], r, s) : launch_dw(d, d.blk0[H + 1], s);
       if (e != hipSuccess) return hip_fail(e, "dw launch");
       red_pending = false;
     }
-  }
-  if (sa.ntasks > 0) {  // the GEMM had nothing to do: the held-back scatter tasks on their own
-    e = launch_sort_scatter(sa, s);
-    if (e != hipSuccess) return hip_fail(e, "scatter launch");
   }
   if (red_pending) {
     e = launch_reduce_final(r, s);

@@ -352,105 +352,6 @@ __device__ __forceinline__ void mlp_k_loop_s(f32x4 (&acc)[TPW], const float* __r
 }
 
 
-// FwFM second order of the deep forwards, Y = U * E_b on MFMA (rows k: fields, MT tiles of 16; columns n = b*D + d:
-// D tiles of 16; contraction over l: fields, S steps of 4), cut into pieces pc = (row tile m, column tile nt) of
-// steps s = 4m .. S-1 (U's rows 16m.. vanish for l <= 16m); each piece leaves its 16 column sums of
-// sum_k E[b,k,d] * Y[k, n] in part2 (RT row halves: part2[(rt * MT * D + pc) * 16 + lane]).  The wave takes pieces
-// plist[p_lo, p_hi) (host-balanced).  Every piece's MFMAs run in step order onto one accumulator per row half, so
-// the sums are the same bits however the work is scheduled; the schedule here: two steps per group, the next
-// group's LDS operands (U fragments, E columns) read before the current group's MFMAs across piece boundaries, so
-// the chains run back to back instead of waiting out an LDS round trip per group.  buf: the E tile (RT halves of
-// 16 rows, row stride SX, zero past F*D up to 4*S fields); upk: U's A fragments [MT][S][64].
-template <int RT>
-__device__ __forceinline__ void fwfm_pieces(const uint8_t* __restrict__ plist, int p_lo, int p_hi, int S, int D, int F,
-                                            int MT, int SX, const float* __restrict__ buf,
-                                            const float* __restrict__ upk, float* __restrict__ part2, int lane) {
-  if (p_lo >= p_hi) return;
-  struct Ops {
-    float a[2];
-    float b[RT][2];
-  };
-  const int rq = lane >> 4;
-  auto ecol = [&](int pc) {
-    const int nt = pc - (pc / D) * D;
-    const int n = nt * 16 + (lane & 15);
-    const int b = n / D;
-    return buf + b * SX + (n - b * D);  // E[b][l][d] = ecol[l * D] (+ 16 SX per row half)
-  };
-  auto read = [&](int pc, int s) {
-    Ops o;
-    const int m = pc / D;
-    const float* ua = upk + m * S * 64 + lane;
-    const float* ec = ecol(pc);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const bool ok = s + u < S;  // an odd S: the last group's second step is a zero MFMA (acc + 0)
-      const int su = ok ? s + u : s;
-      o.a[u] = ok ? ua[su * 64] : 0.f;
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) o.b[rt][u] = ok ? ec[rt * 16 * SX + (4 * su + rq) * D] : 0.f;
-    }
-    return o;
-  };
-  int pi = p_lo;
-  int pc = plist[pi];
-  int s = 4 * (pc / D);
-  Ops cur = read(pc, s);
-  f32x4 acc[RT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  while (true) {
-    int npi = pi, npc = pc, ns = s + 2;
-    const bool last_group = ns >= S;
-    if (last_group) {
-      npi = pi + 1;
-      if (npi < p_hi) {
-        npc = plist[npi];
-        ns = 4 * (npc / D);
-      }
-    }
-    const bool more = npi < p_hi;
-    Ops nxt = cur;
-    if (more) nxt = read(npc, ns);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.a[u], cur.b[rt][u], acc[rt], 0, 0, 0);
-    if (last_group) {
-      // the piece's column sums: sum over its 16 rows k of E[b,k,d] * Y[k,n], then over the four lane groups
-      const int m = pc / D;
-      const float* ec = ecol(pc);
-      float v[RT];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        v[rt] = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * m + 4 * rq + r;
-          const int kk = (k < F ? k : 0) * D;
-          v[rt] = fmaf(k < F ? ec[rt * 16 * SX + kk] : 0.f, acc[rt][r], v[rt]);
-        }
-      }
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) v[rt] += __shfl_xor(v[rt], 16);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) v[rt] += __shfl_xor(v[rt], 32);
-      if (lane < 16)
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) part2[(rt * MT * D + pc) * 16 + lane] = v[rt];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (!more) break;
-    pi = npi;
-    pc = npc;
-    s = ns;
-    cur = nxt;
-  }
-}
-
 // Counter-based dropout mask (deep tower; reference nn.Dropout(0.5), model/DeepFMs.py:260-282):
 // keep element (layer, row, col) of a step iff the top 24 bits of a murmur3-finalised key
 // (seed ^ row*K1 ^ col*K2 ^ layer*K3) / 2^24 >= p.  The same function regenerates the mask in the

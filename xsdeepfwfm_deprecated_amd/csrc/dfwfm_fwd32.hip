@@ -391,9 +391,61 @@ fwd32_kernel(FwdArgs p) {
   }
   stamp(p.stamps, 9, tid);
   if (flags & kHasSecond) {
-    // both 16-row halves of every piece (one U fragment read feeds two MFMA chains; each chain's order is
-    // fwd_kernel's, so the sums are the same bits), the next group's operands in flight during the current MFMAs
-    fwfm_pieces<kRT>(p.fw_list8, p.fw_off8[wave], p.fw_off8[wave + 1], p.S, D, F, p.MT, SX, buf, upk, part2, lane);
+    // both 16-row halves of a piece at once: one U fragment read feeds two independent MFMA chains (each chain's
+    // order is fwd_kernel's, so the sums are the same bits), which halves this phase's dependent latency
+    const int S = p.S;
+    const int MTD = p.MT * D;
+    const int p_lo = p.fw_off8[wave], p_hi = p.fw_off8[wave + 1];
+    for (int pi = p_lo; pi < p_hi; ++pi) {
+      const int pc = p.fw_list8[pi];
+      const int m = pc / D;
+      const int nt = pc - m * D;
+      const int n = nt * 16 + (lane & 15);
+      const int b = n / D;
+      const float* ecol0 = buf + b * SX + (n - b * D);  // E[b][l][d] = ecol0[l * D]; the second half 16 rows on
+      const float* ecol1 = ecol0 + 16 * SX;
+      const float* ua = upk + m * S * 64 + lane;
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      auto group = [&](int s0, auto U_) {
+        constexpr int U = decltype(U_)::value;
+        float av[U], bv0[U], bv1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int l = (4 * (s0 + u) + (lane >> 4)) * D;
+          av[u] = ua[(s0 + u) * 64];
+          bv0[u] = ecol0[l];
+          bv1[u] = ecol1[l];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv0[u], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv1[u], acc1, 0, 0, 0);
+        }
+      };
+      int s0 = 4 * m;
+      for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
+      const int rem = S - s0;
+      if (rem == 3) group(s0, std::integral_constant<int, 3>{});
+      else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
+      else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
+      float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * m + 4 * (lane >> 4) + r;
+        const int kk = (k < F ? k : 0) * D;
+        v0 = fmaf(k < F ? ecol0[kk] : 0.f, acc0[r], v0);
+        v1 = fmaf(k < F ? ecol1[kk] : 0.f, acc1[r], v1);
+      }
+      v0 += __shfl_xor(v0, 16);
+      v1 += __shfl_xor(v1, 16);
+      v0 += __shfl_xor(v0, 32);
+      v1 += __shfl_xor(v1, 32);
+      if (lane < 16) {
+        part2[pc * 16 + lane] = v0;
+        part2[(MTD + pc) * 16 + lane] = v1;
+      }
+    }
   }
   stamp(p.stamps, 10, tid);
   __syncthreads();

@@ -256,7 +256,7 @@ struct ScatterArgs {
 // every row's contributions in a fixed order, so the gradients are the same bits on every run.
 constexpr int kSortSeg = 4096;      // samples sorted per pass (larger batches: passes in sample order)
 constexpr int kSortCh = 32;         // sorted positions per chunk of the segmented sums
-constexpr int kSortThreads = 1024;
+constexpr int kSortThreads = 256;
 struct SortScatterTask {
   float* g2;            // second-order table grad (width D) or null
   float* g1;            // first-order table grad (width 1) or null
@@ -265,10 +265,12 @@ struct SortScatterTask {
   int32_t c;            // QR collisions (kind 1, 2)
   int16_t field;        // model field index
   int8_t kind;          // 0 plain row idx, 1 quotient row idx / c, 2 remainder row idx % c
-  int8_t pad;
+  int8_t nbuck;         // row buckets (row % nbuck), one workgroup each
+  int32_t block0;       // the task's first workgroup
+  int32_t pad;
 };
-static_assert(sizeof(SortScatterTask) == 40, "sort scatter task layout");
-constexpr int kSortScatterList = 32;  // tasks per launch (a kernel argument: beside DwArgs + RedArgs, < 4 KiB)
+static_assert(sizeof(SortScatterTask) == 48, "sort scatter task layout");
+constexpr int kSortScatterList = 64;  // tasks per launch (the list is a kernel argument, < 4 KiB)
 struct SortScatterArgs {
   SortScatterTask t[kSortScatterList];
   int32_t ntasks;
@@ -471,10 +473,7 @@ hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages
 hipError_t launch_reduce_final(const RedArgs& a, hipStream_t s);  // the second stage only (bwd_kernel red)
 hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s);
-hipError_t launch_sort_scatter(const SortScatterArgs& a, hipStream_t s);
-// one launch: the scatter tasks of sa, the weight-gradient GEMM, and (r non-null) the reductions' final sums
-hipError_t launch_dw_scatter(const DwArgs& a, int total_blocks, const RedArgs* r, const SortScatterArgs& sa,
-                             hipStream_t s);
+hipError_t launch_sort_scatter(const SortScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
                        float eps, float wd, float bc2_sqrt, hipStream_t s);
 // device-side step: state = {int64 step; float step_size, omb1, b2, omb2, eps, wd, bc2_sqrt}

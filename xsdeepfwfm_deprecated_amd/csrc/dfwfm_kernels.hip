@@ -499,12 +499,54 @@ fwd_kernel(FwdArgs p) {
       }
     }
   } else if (flags & kHasSecond) {
-    // Y = U * E_b on MFMA as (row tile m, column tile nt) pieces (fwfm_pieces), balanced over the waves on the host
-    // (fw_list): every piece leaves its 16 column sums in part2[pc], so the result does not depend on the wave count
+    // Y = U * E_b on MFMA: rows k (fields, MT tiles of 16), columns n = b*D + d (D tiles of 16), contraction
+    // over l (fields, S steps of 4).  second[b] = sum_{k,d} E[b,k,d] * Y[k, b*D+d].  The work is cut into
+    // pieces pc = (row tile m, column tile nt) of S - 4m steps each (U's rows 16m.. vanish for l <= 16m); the
+    // host balances the pieces over the waves (fw_list), and every piece leaves its 16 column sums in
+    // part2[pc] -- so the result does not depend on the wave count.
+    const int S = p.S;
     const uint8_t* plist = NW == 8 ? p.fw_list8 : p.fw_list4;
     const int p_lo = NW == 8 ? p.fw_off8[wave] : p.fw_off4[wave];
     const int p_hi = NW == 8 ? p.fw_off8[wave + 1] : p.fw_off4[wave + 1];
-    fwfm_pieces<1>(plist, p_lo, p_hi, p.S, D, F, p.MT, SX, bufX, upk, part2, lane);
+    for (int pi = p_lo; pi < p_hi; ++pi) {
+      const int pc = plist[pi];
+      const int m = pc / D;
+      const int nt = pc - m * D;
+      const int n = nt * 16 + (lane & 15);
+      const int b = n / D;
+      const float* ecol = bufX + b * SX + (n - b * D);  // E[b][l][d] = ecol[l * D]
+      const float* ua = upk + m * S * 64 + lane;        // A fragment of step s: ua[s * 64]
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      // steps in groups: every operand of a group is read from LDS before its MFMAs
+      auto group = [&](int s0, auto U_) {
+        constexpr int U = decltype(U_)::value;
+        float av[U], bv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          av[u] = ua[(s0 + u) * 64];
+          bv[u] = ecol[(4 * (s0 + u) + (lane >> 4)) * D];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+      };
+      int s0 = 4 * m;
+      for (; s0 + 4 <= S; s0 += 4) group(s0, std::integral_constant<int, 4>{});
+      const int rem = S - s0;
+      if (rem == 3) group(s0, std::integral_constant<int, 3>{});
+      else if (rem == 2) group(s0, std::integral_constant<int, 2>{});
+      else if (rem == 1) group(s0, std::integral_constant<int, 1>{});
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * m + 4 * (lane >> 4) + r;
+        const float e = ecol[(k < F ? k : 0) * D];
+        v = fmaf(k < F ? e : 0.f, acc[r], v);
+      }
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) part2[pc * 16 + lane] = v;
+    }
   }
   // layer 0's tail fragments once the gather rows are dead (live across the gather, they spilled)
   if constexpr (NSK == 0) {

@@ -988,15 +988,16 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 
 // ---------------------------------------------------------------------------
 // Deterministic categorical-table scatter (the default; scatter_kernel's atomics add a row's contributions in
-// arrival order, so two runs of the same step differed in the last bits).  One workgroup per task (field, row kind),
-// both table families at once.  Per pass over <= kSortSeg samples:
-//   1. keys (row << 12 | sample) into LDS -- unique, so any correct sort gives the same order -- and each sample's
-//      QR partner row; 2. bitonic sort in LDS; 3. the sorted positions in chunks of kSortCh: a work item (component,
-//      chunk) walks its chunk's positions in order, summing each run of equal rows; a run that starts and ends inside
-//      the chunk is added to its row at once, a run cut by the chunk's start / end leaves its partial sum in LDS
-//      (lead / trail); 4. the chunk holding a cut run's head adds trail + the following chunks' leads in chunk
-//      order.  Every row is added by exactly one thread per pass (passes follow each other behind a barrier), in an
-//      order fixed by the sorted positions: the same bits on every run.
+// arrival order, so two runs of the same step differed in the last bits).  A task is one field and row kind, both
+// table families at once; its rows are split into nbuck buckets (row % nbuck), one workgroup each, so every row has
+// ONE owner workgroup.  Per pass over <= kSortSeg samples the owner:
+//   1. keeps its bucket's samples in sample order (a block scan) as keys (row << 12 | sample) in LDS -- unique, so any
+//      correct sort gives the same order -- with each sample's QR partner row; 2. bitonic sort in LDS; 3. walks the
+//      sorted positions in chunks of kSortCh: a work item (chunk, component) sums each run of equal rows in position
+//      order; a run that starts and ends inside the chunk is added to its row at once, a run cut by the chunk's start /
+//      end leaves its partial sum in LDS (lead / trail); 4. the chunk holding a cut run's head adds trail + the
+//      following chunks' leads in chunk order.  Every row is added by exactly one thread per pass (passes follow each
+//      other behind a barrier), in an order fixed by the sorted positions: the same bits on every run.
 // ---------------------------------------------------------------------------
 template <int NTH>
 __device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid) {
@@ -1018,31 +1019,48 @@ __device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid)
 
 __host__ __device__ inline int sort_scatter_nch() { return kSortSeg / kSortCh; }
 
-// one task (a.t[task]) by a workgroup of NTH threads, in smem (sort_scatter_lds_bytes)
-template <int NTH>
-__device__ __forceinline__ void sort_scatter_block(const SortScatterArgs& a, int task, float* smem) {
+__global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterArgs a) {
+  constexpr int NTH = kSortThreads;
   constexpr int CH = kSortCh;
+  constexpr int SPT = kSortSeg / NTH;  // samples per thread when selecting the bucket's samples
   const int NCH = sort_scatter_nch();
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int D = a.D, FD = a.F * D, ncomp = D + 1;  // components: 0..D-1 second-order row, D first order
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
   int32_t* partv = reinterpret_cast<int32_t*>(key + kSortSeg);
-  float* lead = reinterpret_cast<float*>(partv + kSortSeg);  // [NCH][ncomp]
+  int32_t* cnt_s = partv + kSortSeg;                         // [NTH] kept samples per thread, then their prefix
+  float* lead = reinterpret_cast<float*>(cnt_s + NTH);      // [NCH][ncomp]
   float* trail = lead + NCH * ncomp;
   uint8_t* cflag = reinterpret_cast<uint8_t*>(trail + NCH * ncomp);  // bit 0: first run continues from the
                                                                      // previous chunk, 1: last run continues into
                                                                      // the next, 2: one run
-  const SortScatterTask T = a.t[task];
+  __shared__ int s_total;
+  // this workgroup's task and bucket
+  int lo = 0, hi = a.ntasks - 1;
+  const int bid = blockIdx.x;
+  while (lo < hi) {  // last task whose block0 <= bid
+    const int mid = (lo + hi + 1) >> 1;
+    if (a.t[mid].block0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const SortScatterTask T = a.t[lo];
+  const int bucket = bid - T.block0, nbuck = T.nbuck;
   const FieldDev fd = a.fields[T.field];
   const int f = T.field, col = f - a.num;
   const float lwf = a.lw ? a.lw[f] : 1.f;
   for (int64_t s0 = 0; s0 < a.batch; s0 += kSortSeg) {
-    const int n = (int)((a.batch - s0) < kSortSeg ? (a.batch - s0) : kSortSeg);
-    int np = 2;
-    while (np < n) np <<= 1;
-    for (int i = tid; i < np; i += NTH) {
-      uint64_t k = ~0ull;
-      if (i < n) {
+    const int ns = (int)((a.batch - s0) < kSortSeg ? (a.batch - s0) : kSortSeg);
+    // 1. this bucket's samples of the pass, in sample order: thread t looks at samples [SPT t, SPT t + SPT)
+    int64_t rw[SPT];
+    int32_t pt[SPT];
+    int kept = 0;
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int i = tid * SPT + u;
+      rw[u] = -1;
+      pt[u] = 0;
+      if (i < ns) {
         int64_t idx = a.xi[(s0 + i) * a.xi_stride + col];
         if (idx < 0 || idx >= fd.n) idx = 0;  // the forward clamped (and flagged) it the same way
         int64_t row = idx, part = 0;
@@ -1053,99 +1071,126 @@ __device__ __forceinline__ void sort_scatter_block(const SortScatterArgs& a, int
           part = idx / T.c;
           row = idx - part * T.c;
         }
-        k = ((uint64_t)row << 12) | (uint64_t)i;
-        partv[i] = (int32_t)part;
-      }
-      key[i] = k;
-    }
-    __syncthreads();
-    bitonic_sort_lds<NTH>(key, np, tid);
-    const int nch = (n + CH - 1) / CH;
-    for (int c = tid; c < nch; c += NTH) {
-      const int p0 = c * CH, p1 = (p0 + CH < n ? p0 + CH : n) - 1;
-      const uint64_t r0 = key[p0] >> 12, r1 = key[p1] >> 12;
-      const bool cin = p0 > 0 && (key[p0 - 1] >> 12) == r0;
-      const bool cout = p1 + 1 < n && (key[p1 + 1] >> 12) == r1;
-      cflag[c] = (uint8_t)((cin ? 1 : 0) | (cout ? 2 : 0) | (r0 == r1 ? 4 : 0));
-    }
-    __syncthreads();
-    // 3. runs inside each chunk.  Items: (chunk, d) of the second-order family with d fastest -- the lanes of one
-    // chunk read one sample's 40-byte dE row per position and add one 40-byte table row per run: coalesced -- then
-    // one item per chunk for the first-order family
-    const int n2 = T.g2 ? nch * D : 0, n1 = T.g1 ? nch : 0;
-    auto item = [&](int it, int& c, int& j) {
-      if (it < n2) {
-        c = it / D;
-        j = it - c * D;
-      } else {
-        c = it - n2;
-        j = D;
-      }
-    };
-    for (int it = tid; it < n2 + n1; it += NTH) {
-      int c, j;
-      item(it, c, j);
-      const bool fam2 = j < D;
-      float* g = fam2 ? T.g2 : T.g1;
-      const int w = fam2 ? D : 1, jj = fam2 ? j : 0;
-      const float* o = fam2 ? T.o2 : T.o1;
-      const int p0 = c * CH, cnt = n - p0 < CH ? n - p0 : CH;
-      const int fl = cflag[c];
-      float v[CH];
-      uint32_t rw[CH];
-#pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        v[q] = 0.f;
-        rw[q] = 0xffffffffu;
-        if (q < cnt) {
-          const uint64_t k = key[p0 + q];
-          const int sm = (int)(k & 4095);
-          rw[q] = (uint32_t)(k >> 12);
-          const int64_t b = s0 + sm;
-          float x = fam2 ? a.sv_de[b * FD + f * D + jj] : a.dlogit[b] * lwf;
-          if (o) x *= o[(int64_t)partv[sm] * w + jj];
-          v[q] = x;
+        if ((int)(row % nbuck) == bucket) {
+          rw[u] = row;
+          pt[u] = (int32_t)part;
+          ++kept;
         }
       }
-      float s = 0.f;
-      uint32_t cur = rw[0];
-      bool first = true;
+    }
+    cnt_s[tid] = kept;
+    __syncthreads();
+    for (int o = 1; o < NTH; o <<= 1) {  // inclusive scan of the per-thread counts
+      const int x = tid >= o ? cnt_s[tid - o] : 0;
+      __syncthreads();
+      cnt_s[tid] += x;
+      __syncthreads();
+    }
+    int pos = cnt_s[tid] - kept;
+    if (tid == NTH - 1) s_total = cnt_s[NTH - 1];
 #pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        if (q < cnt) {
-          if (rw[q] != cur) {  // a run ends inside the chunk
-            if (first && (fl & 1)) lead[c * ncomp + j] = s;
-            else atomicAdd(g + (int64_t)cur * w + jj, s);  // the row's only adder in this pass
-            first = false;
-            cur = rw[q];
-            s = 0.f;
+    for (int u = 0; u < SPT; ++u) {
+      if (rw[u] >= 0) {
+        const int i = tid * SPT + u;
+        key[pos++] = ((uint64_t)rw[u] << 12) | (uint64_t)i;
+        partv[i] = pt[u];
+      }
+    }
+    __syncthreads();
+    const int n = s_total;
+    if (n > 0) {
+      int np = 2;
+      while (np < n) np <<= 1;
+      for (int i = n + tid; i < np; i += NTH) key[i] = ~0ull;
+      __syncthreads();
+      bitonic_sort_lds<NTH>(key, np, tid);
+      const int nch = (n + CH - 1) / CH;
+      for (int c = tid; c < nch; c += NTH) {
+        const int p0 = c * CH, p1 = (p0 + CH < n ? p0 + CH : n) - 1;
+        const uint64_t r0 = key[p0] >> 12, r1 = key[p1] >> 12;
+        const bool cin = p0 > 0 && (key[p0 - 1] >> 12) == r0;
+        const bool cout = p1 + 1 < n && (key[p1 + 1] >> 12) == r1;
+        cflag[c] = (uint8_t)((cin ? 1 : 0) | (cout ? 2 : 0) | (r0 == r1 ? 4 : 0));
+      }
+      __syncthreads();
+      // 3. runs inside each chunk.  Items: (chunk, d) of the second-order family with d fastest -- the lanes of one
+      // chunk read one sample's 40-byte dE row per position and add one 40-byte table row per run: coalesced --
+      // then one item per chunk for the first-order family
+      const int n2 = T.g2 ? nch * D : 0, n1 = T.g1 ? nch : 0;
+      auto item = [&](int it, int& c, int& j) {
+        if (it < n2) {
+          c = it / D;
+          j = it - c * D;
+        } else {
+          c = it - n2;
+          j = D;
+        }
+      };
+      for (int it = tid; it < n2 + n1; it += NTH) {
+        int c, j;
+        item(it, c, j);
+        const bool fam2 = j < D;
+        float* g = fam2 ? T.g2 : T.g1;
+        const int w = fam2 ? D : 1, jj = fam2 ? j : 0;
+        const float* o = fam2 ? T.o2 : T.o1;
+        const int p0 = c * CH, cnt = n - p0 < CH ? n - p0 : CH;
+        const int fl = cflag[c];
+        float v[CH];
+        uint32_t rq[CH];
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          v[q] = 0.f;
+          rq[q] = 0xffffffffu;
+          if (q < cnt) {
+            const uint64_t k = key[p0 + q];
+            const int sm = (int)(k & 4095);
+            rq[q] = (uint32_t)(k >> 12);
+            const int64_t b = s0 + sm;
+            float x = fam2 ? a.sv_de[b * FD + f * D + jj] : a.dlogit[b] * lwf;
+            if (o) x *= o[(int64_t)partv[sm] * w + jj];
+            v[q] = x;
           }
-          s += v[q];
         }
+        float sum = 0.f;
+        uint32_t cur = rq[0];
+        bool first = true;
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          if (q < cnt) {
+            if (rq[q] != cur) {  // a run ends inside the chunk
+              if (first && (fl & 1)) lead[c * ncomp + j] = sum;
+              else atomicAdd(g + (int64_t)cur * w + jj, sum);  // the row's only adder in this pass
+              first = false;
+              cur = rq[q];
+              sum = 0.f;
+            }
+            sum += v[q];
+          }
+        }
+        if (first && (fl & 1)) lead[c * ncomp + j] = sum;  // continues from the previous chunk (maybe into the next)
+        else if (fl & 2) trail[c * ncomp + j] = sum;     // its head is here, its tail in the next chunk(s)
+        else atomicAdd(g + (int64_t)cur * w + jj, sum);
       }
-      if (first && (fl & 1)) lead[c * ncomp + j] = s;  // continues from the previous chunk (maybe into the next)
-      else if (fl & 2) trail[c * ncomp + j] = s;     // its head is here, its tail in the next chunk(s)
-      else atomicAdd(g + (int64_t)cur * w + jj, s);
-    }
-    __syncthreads();
-    // 4. runs cut by chunk ends: the chunk with the head adds its trail and the following chunks' leads in order
-    for (int it = tid; it < n2 + n1; it += NTH) {
-      int c, j;
-      item(it, c, j);
-      const int fl = cflag[c];
-      if (!(fl & 2) || (fl & 5) == 5) continue;  // no run leaves this chunk, or it is not headed here
-      const bool fam2 = j < D;
-      float* g = fam2 ? T.g2 : T.g1;
-      float s = trail[c * ncomp + j];
-      int c2 = c + 1;
-      while (true) {
-        s += lead[c2 * ncomp + j];
-        if ((cflag[c2] & 6) == 6) ++c2;  // one run that continues: the whole chunk belongs to the run
-        else break;
+      __syncthreads();
+      // 4. runs cut by chunk ends: the chunk with the head adds its trail and the following chunks' leads in order
+      for (int it = tid; it < n2 + n1; it += NTH) {
+        int c, j;
+        item(it, c, j);
+        const int fl = cflag[c];
+        if (!(fl & 2) || (fl & 5) == 5) continue;  // no run leaves this chunk, or it is not headed here
+        const bool fam2 = j < D;
+        float* g = fam2 ? T.g2 : T.g1;
+        float sum = trail[c * ncomp + j];
+        int c2 = c + 1;
+        while (true) {
+          sum += lead[c2 * ncomp + j];
+          if ((cflag[c2] & 6) == 6) ++c2;  // one run that continues: the whole chunk belongs to the run
+          else break;
+        }
+        const int p1 = c * CH + CH - 1;  // a chunk with a continuing last run is full
+        const uint32_t row = (uint32_t)(key[p1] >> 12);
+        atomicAdd(g + (int64_t)row * (fam2 ? D : 1) + (fam2 ? j : 0), sum);
       }
-      const int p1 = c * CH + CH - 1;  // a chunk with a continuing last run is full
-      const uint32_t row = (uint32_t)(key[p1] >> 12);
-      atomicAdd(g + (int64_t)row * (fam2 ? D : 1) + (fam2 ? j : 0), s);
     }
     // the next pass's adds to the same rows come after these (this workgroup's own atomics, retired before the
     // barrier; no device-scope fence: nothing another workgroup reads)
@@ -1154,22 +1199,17 @@ __device__ __forceinline__ void sort_scatter_block(const SortScatterArgs& a, int
   }
 }
 
-__global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  sort_scatter_block<kSortThreads>(a, blockIdx.x, smem);
-}
-
 size_t sort_scatter_lds_bytes(int D) {
   const int NCH = sort_scatter_nch();
-  return (size_t)kSortSeg * 12 + (size_t)2 * NCH * (D + 1) * 4 + (size_t)NCH;
+  return (size_t)kSortSeg * 12 + (size_t)kSortThreads * 4 + (size_t)2 * NCH * (D + 1) * 4 + (size_t)NCH;
 }
 
-hipError_t launch_sort_scatter(const SortScatterArgs& a, hipStream_t s) {
-  if (a.ntasks <= 0 || a.batch <= 0) return hipSuccess;
+hipError_t launch_sort_scatter(const SortScatterArgs& a, int total_blocks, hipStream_t s) {
+  if (a.ntasks <= 0 || a.batch <= 0 || total_blocks <= 0) return hipSuccess;
   const size_t lds = sort_scatter_lds_bytes(a.D);
   hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(sort_scatter_kernel), lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sort_scatter_kernel, dim3(a.ntasks), dim3(kSortThreads), lds, s, a);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(total_blocks), dim3(kSortThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1391,22 +1431,6 @@ __global__ void __launch_bounds__(64 * NW) dwr_reduce_kernel(DwArgs a, RedArgs r
     dwr_block<kDwrP, NW>(a, blockIdx.x);
   else
     reduce_final_block(r, nblk, (int)blockIdx.x - dw_blocks);
-}
-
-// The backward's last launch of the one-stream step: the table scatter's tasks (one 256-thread workgroup each, first:
-// they take their CUs while the weight-gradient GEMM's one round of workgroups takes the others), the GEMM, then the
-// shallow reductions' final sums.  Independent outputs; a dependency-free way to overlap the scatter with the GEMM.
-template <int kDwrP, int NW>
-__global__ void __launch_bounds__(64 * NW) dwr_scatter_kernel(DwArgs a, RedArgs r, SortScatterArgs sa, int nblk,
-                                                              int dw_blocks) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int bid = (int)blockIdx.x;
-  if (bid < sa.ntasks)
-    sort_scatter_block<64 * NW>(sa, bid, smem);
-  else if (bid < sa.ntasks + dw_blocks)
-    dwr_block<kDwrP, NW>(a, bid - sa.ntasks);
-  else if (r.part)
-    reduce_final_block(r, nblk, bid - sa.ntasks - dw_blocks);
 }
 
 // ---------------------------------------------------------------------------
@@ -1702,31 +1726,6 @@ hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r,
   hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(total_blocks + rblocks), dim3(256), 0, s, a, r, nblk,
                      total_blocks);
   hipError_t e = hipGetLastError();
-  return e != hipSuccess ? e : launch_dw_sum(a, s);
-}
-
-hipError_t launch_dw_scatter(const DwArgs& a, int total_blocks, const RedArgs* r, const SortScatterArgs& sa,
-                             hipStream_t s) {
-  const int64_t q = a.rows_per_split / 4 + 4;
-  for (int l = 1; l <= a.H; ++l) {
-    const int64_t w = a.ldx[l] > a.N ? a.ldx[l] : a.N;
-    if (q * w * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
-  }
-  RedArgs rr;
-  int rblocks = 0, nblk = 0;
-  if (r) {
-    rr = *r;
-    nblk = (int)((r->batch + kBM - 1) / kBM);
-    rblocks = (red_outputs(r->F, r->D, r->N, r->num) + 63) / 64;
-  } else {
-    memset(&rr, 0, sizeof rr);
-  }
-  const size_t lds = sort_scatter_lds_bytes(sa.D);
-  auto k = dwr_scatter_kernel<4, 4>;
-  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(sa.ntasks + total_blocks + rblocks), dim3(256), lds, s, a, rr, sa, nblk, total_blocks);
-  e = hipGetLastError();
   return e != hipSuccess ? e : launch_dw_sum(a, s);
 }
 
