@@ -174,7 +174,6 @@ bwd_kernel(BwdArgs p) {
   //  * the FwFM dE pieces (m, nt): S dependent MFMAs each, round-robin from the last wave.
   {
     const int MT = p.MT, S = p.S;
-    constexpr bool kPair = D <= 16;  // two chains at a time (D = 32: four 64-float operand arrays would spill)
     if (red & kRedR) {
       float* gram = smem + L.gram;
       // a wave's chains all have its parity h = wave & 1 (c = wave + NW k), so the (b, d) of every step -- its LDS
@@ -189,40 +188,20 @@ bwd_kernel(BwdArgs p) {
         off[j] = b * SX + (nn - b * D);
         dlj[j] = dl[b];
       }
-      // two chains at a time, their MFMAs interleaved (each chain's own order unchanged: the same bits), so the
-      // matrix pipe is not idle for a chain's 40-cycle dependent latency at every step
-      auto gram_ops = [&](int c, float (&av)[2 * D], float (&bv)[2 * D]) {
+      for (int c = wave; c < 2 * MT * MT; c += NW) {
         const int t = c >> 1;
         const int mk = t / MT, ml = t - mk * MT;
         const int kA = 16 * mk + (lane & 15), lB = 16 * ml + (lane & 15);
         const bool va = kA < F, vb = lB < F;
         const float* ea = bufE + (va ? kA : 0) * D;
         const float* eb = bufE + (vb ? lB : 0) * D;
+        float av[2 * D], bv[2 * D];
 #pragma unroll
         for (int j = 0; j < 2 * D; ++j) {
           const float x = ea[off[j]];
           av[j] = va ? dlj[j] * x : 0.f;
           bv[j] = vb ? eb[off[j]] : 0.f;
         }
-      };
-      const int nch = 2 * MT * MT;
-      int c = wave;
-      for (; kPair && c + NW < nch; c += 2 * NW) {
-        float av0[2 * D], bv0[2 * D], av1[2 * D], bv1[2 * D];
-        gram_ops(c, av0, bv0);
-        gram_ops(c + NW, av1, bv1);
-        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-#pragma unroll
-        for (int j = 0; j < 2 * D; ++j) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[j], bv0[j], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[j], bv1[j], acc1, 0, 0, 0);
-        }
-        reinterpret_cast<f32x4*>(gram)[c * 64 + lane] = acc0;
-        reinterpret_cast<f32x4*>(gram)[(c + NW) * 64 + lane] = acc1;
-      }
-      for (; c < nch; c += NW) {
-        float av[2 * D], bv[2 * D];
-        gram_ops(c, av, bv);
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 2 * D; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
@@ -232,75 +211,44 @@ bwd_kernel(BwdArgs p) {
     stamp(p.stamps, 12, tid);
     if (second) {
       // dE[b,k,d] = dlogit_b * sum_{l != k} Rs[k,l] E[b,l,d]  (+ dfo[b,k] * Wfl[k,d] with fwlw, :344-345)
-      // two pieces at a time (it, it + NW), their MFMAs interleaved step by step (each piece's order unchanged)
-      struct Piece {
-        const float* ecol;
-        const float* ua;
-        int m, b, d;
-      };
-      auto piece = [&](int it) {
-        Piece q;
-        q.m = it / D;
-        const int nt = it - q.m * D;
+      for (int it = NW - 1 - wave; it < MT * D; it += NW) {
+        const int m = it / D, nt = it - m * D;
         const int n = nt * 16 + (lane & 15);
-        q.b = n / D;
-        q.d = n - q.b * D;
-        q.ecol = bufE + q.b * SX + q.d + (lane >> 4) * D;  // + 4 s D at step s
-        q.ua = rsk + q.m * S * 64 + lane;                  // + 64 s
-        return q;
-      };
-      auto finish = [&](const Piece& q, const f32x4& acc) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * q.m + row0 + r;
-          if (k < F) {
-            float v = dl[q.b] * acc[r];
-            if (fwlw) v = fmaf(lwp ? dl[q.b] * lw_s[k] : dl[q.b], fwlw_s[k * D + q.d], v);
-            bufD[q.b * SX + k * D + q.d] = v;
-          }
-        }
-      };
-      // steps in groups of 8 / 4 / 3 / 2 / 1; NP pieces per group call, every operand read before the MFMAs
-      auto run = [&](const Piece* q, f32x4* acc, auto NP_) {
-        constexpr int NP = decltype(NP_)::value;
+        const int b = n / D;
+        const int d = n - b * D;
+        const float* ecol = bufE + b * SX + d + (lane >> 4) * D;  // + 4 s D at step s
+        const float* ua = rsk + m * S * 64 + lane;                 // + 64 s
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         auto group = [&](int s0, auto U_) {
           constexpr int U = decltype(U_)::value;
-          float av[NP][U], bv[NP][U];
+          float av[U], bv[U];
 #pragma unroll
-          for (int i = 0; i < NP; ++i)
+          for (int u = 0; u < U; ++u) {
+            av[u] = ua[(s0 + u) * 64];
+            bv[u] = ecol[(s0 + u) * 4 * D];
+          }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-              av[i][u] = q[i].ua[(s0 + u) * 64];
-              bv[i][u] = q[i].ecol[(s0 + u) * 4 * D];
-            }
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int i = 0; i < NP; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][u], bv[i][u], acc[i], 0, 0, 0);
+          for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
         };
         int s0 = 0;
         for (; s0 + 8 <= S; s0 += 8) group(s0, std::integral_constant<int, 8>{});
-        if (S - s0 >= 4) {
+        const int rem = S - s0;
+        if (rem >= 4) {
           group(s0, std::integral_constant<int, 4>{});
           s0 += 4;
         }
         if (S - s0 == 3) group(s0, std::integral_constant<int, 3>{});
         else if (S - s0 == 2) group(s0, std::integral_constant<int, 2>{});
         else if (S - s0 == 1) group(s0, std::integral_constant<int, 1>{});
-      };
-      int it = NW - 1 - wave;
-      for (; kPair && it + NW < MT * D; it += 2 * NW) {
-        const Piece q[2] = {piece(it), piece(it + NW)};
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        run(q, acc, std::integral_constant<int, 2>{});
-        finish(q[0], acc[0]);
-        finish(q[1], acc[1]);
-      }
-      for (; it < MT * D; it += NW) {
-        const Piece q[1] = {piece(it)};
-        f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
-        run(q, acc, std::integral_constant<int, 1>{});
-        finish(q[0], acc[0]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * m + row0 + r;
+          if (k < F) {
+            float v = dl[b] * acc[r];
+            if (fwlw) v = fmaf(lwp ? dl[b] * lw_s[k] : dl[b], fwlw_s[k * D + d], v);
+            bufD[b * SX + k * D + d] = v;
+          }
+        }
       }
     }
   }
