@@ -32,7 +32,7 @@ def test_header_declares_expected_api():
         "dfwfm_forward_workspace_bytes",
         "dfwfm_forward_ws", "dfwfm_last_error", "dfwfm_model_build_fwfm_pairs", "dfwfm_model_build_sparse_mlp", "dfwfm_model_create", "dfwfm_model_destroy",
         "dfwfm_metrics_workspace_bytes", "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_prune_apply", "dfwfm_prune_threshold",
-        "dfwfm_prune_workspace_bytes", "dfwfm_read_error_flag", "dfwfm_set_step_source", "dfwfm_sparse_grads_apply", "dfwfm_sparse_grads_local", "dfwfm_sparse_grads_size",
+        "dfwfm_prune_workspace_bytes", "dfwfm_read_error_flag", "dfwfm_set_deterministic", "dfwfm_set_step_source", "dfwfm_sparse_grads_apply", "dfwfm_sparse_grads_local", "dfwfm_sparse_grads_size",
         "dfwfm_train_forward", "dfwfm_workspace_generation"])
 
 

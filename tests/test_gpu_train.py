@@ -701,7 +701,7 @@ def test_resident_inputs_graphs_equal_copied_inputs(gpu):
         m = build(cfg, params, gpu, is_deep_dropout=True)
         m.train()
         torch.manual_seed(5)
-        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, resident_inputs=resident)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, resident_inputs=resident, deterministic=True)
         for k in range(6):
             t.step(*bat[k % 3])
         torch.cuda.synchronize()
@@ -726,7 +726,7 @@ def test_step_many_equals_single_steps(gpu):
         m = build(cfg, params, gpu, is_deep_dropout=True)
         m.train()
         torch.manual_seed(5)
-        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, resident_inputs=True)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, resident_inputs=True, deterministic=True)
         t.step(*bat[0])
         for _ in range(2):
             if many:
@@ -741,8 +741,8 @@ def test_step_many_equals_single_steps(gpu):
         losses.append(float(t.loss_sum.item()))
         res.append({n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()})
         t.close()
-    # every sum of the step is formed in a fixed order (sorted scatter, split-K slices, tile-ordered reductions and
-    # loss): the same bits
+    # deterministic mode: every sum of the step is formed in a fixed order (sorted scatter, split-K slices,
+    # tile-ordered reductions and loss): the same bits
     for n in res[0]:
         assert np.array_equal(res[0][n], res[1][n]), n
     assert losses[0] == losses[1], losses
@@ -1004,11 +1004,13 @@ def _hot_case(B, seed=4):
 
 @pytest.mark.parametrize("B", [3000, 9000])  # 9000: three sorted passes of <= 4096 samples
 def test_sorted_scatter_bit_identical_and_matches_atomic(gpu, monkeypatch, B):
-    """The sorted table scatter (default): two backward passes give the same bits, and equal the atomic scatter
-    (DFWFM_SCATTER=atomic, arrival-order sums) within fp32 reassociation, hot rows and multi-pass batches included."""
+    """Deterministic mode (sorted table scatter, split-K slices): two backward passes give the same bits, and equal
+    the atomic scatter (DFWFM_SCATTER=atomic, arrival-order sums) within fp32 reassociation, hot rows and multi-pass
+    batches included."""
     m, xi, xv, y = _hot_case(B)
     m = m.to(gpu).train()
     m.init_weights()
+    m._sync_engine(gpu).set_deterministic(True)
     g1, _, _ = _sparse_step(m, gpu, xi, xv, y, sparse=False, bce_fused=True)
     g2, _, _ = _sparse_step(m, gpu, xi, xv, y, sparse=False, bce_fused=True)
     for k in g1:
@@ -1022,9 +1024,9 @@ def test_sorted_scatter_bit_identical_and_matches_atomic(gpu, monkeypatch, B):
 
 @pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult"])
 def test_fused_step_runs_are_bit_identical(gpu, name):
-    """Two FusedTrainStep instances from the same weights over the same 4 batches (dropout on, graph-replayed steps)
-    end with bit-identical parameters and loss: the sorted scatter, the split-K slices of the weight-gradient GEMM and
-    the tile-ordered reductions leave no arrival-order sum in the step."""
+    """Two FusedTrainStep(deterministic=True) instances from the same weights over the same 4 batches (dropout on,
+    graph-replayed steps) end with bit-identical parameters and loss: the sorted scatter, the split-K slices of the
+    weight-gradient GEMM and the tile-ordered reductions leave no arrival-order sum in the step."""
     from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
     cfg, params, xi, xv, y, *_ = load_train_golden(name)
     B = 64
@@ -1033,7 +1035,7 @@ def test_fused_step_runs_are_bit_identical(gpu, name):
     for _ in range(2):
         m = build(cfg, params, gpu, is_deep_dropout=True)
         torch.manual_seed(11)
-        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, deterministic=True)
         for k in range(4):
             t.step(*bat[k % 3])
         torch.cuda.synchronize()
@@ -1046,8 +1048,8 @@ def test_fused_step_runs_are_bit_identical(gpu, name):
 
 
 def test_full_size_fused_steps_bit_identical(gpu):
-    """Criteo-39 sizes at the bench's batch (4096, 3x400 MLP, dropout): two runs of 3 fused steps from the same
-    weights give bit-identical parameters (every table, the MLP's split-K weight gradients included)."""
+    """Criteo-39 sizes at the bench's batch (4096, 3x400 MLP, dropout), deterministic mode: two runs of 3 fused steps
+    from the same weights give bit-identical parameters (every table, the MLP's split-K weight gradients included)."""
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
     from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
     sizes = synth.CRITEO_FEATURE_SIZES
@@ -1064,7 +1066,7 @@ def test_full_size_fused_steps_bit_identical(gpu):
                     is_deep_dropout=True).to(gpu).train()
         m.init_weights()
         torch.manual_seed(21)
-        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, deterministic=True)
         for b in bats:
             t.step(*b)
         torch.cuda.synchronize()
@@ -1073,3 +1075,21 @@ def test_full_size_fused_steps_bit_identical(gpu):
         del m
     for n in res[0]:
         assert np.array_equal(res[0][n], res[1][n]), n
+
+
+def test_autograd_backward_deterministic_switch(gpu):
+    """DeepFMs.deterministic reaches the autograd backward (torch.ops.dfwfm.forward's registered backward): two
+    loss.backward() calls on the same batch give bit-identical gradients, at Criteo-39 table sizes."""
+    m, xi, xv, y = _hot_case(4096, seed=8)
+    m = m.to(gpu).train()
+    m.init_weights()
+    m.deterministic = True
+    got = []
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        out = m(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu))
+        F.binary_cross_entropy_with_logits(out, torch.from_numpy(y).to(gpu)).backward()
+        torch.cuda.synchronize()
+        got.append({k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()})
+    for k in got[0]:
+        assert np.array_equal(got[0][k], got[1][k]), k

@@ -104,6 +104,10 @@ class DeepFMs(nn.Module):
         # (reference :661-666) leaves at most this many (of F (F - 1) / 2); 0 (default) keeps the dense Gram
         # on MFMA, which is as fast at the reference's 73 of 741 pairs
         self.fwfm_pair_max = 0
+        # the device backward's gradient sums in a fixed order (dfwfm_set_deterministic; like
+        # torch.use_deterministic_algorithms): two runs of a training step give the same bits, at ~+16 us per step
+        # at Criteo-39 (sorted table scatter, split-K slices); off by default (float atomics)
+        self.deterministic = False
         self._defer_index_check = 0     # >0 inside a batched caller: one flag read at its end, not per batch
         self._engine = None
 

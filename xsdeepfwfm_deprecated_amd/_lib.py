@@ -147,6 +147,7 @@ SIGNATURES = {
     "dfwfm_last_error": (ctypes.c_char_p, []),
     "dfwfm_diag_stamps": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64, _P]),
     "dfwfm_abi_version": (ctypes.c_int, []),
+    "dfwfm_set_deterministic": (ctypes.c_int, [_P, ctypes.c_int32]),
 }
 
 _lib = None

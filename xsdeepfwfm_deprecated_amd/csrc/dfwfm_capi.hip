@@ -92,6 +92,7 @@ struct dfwfm_model {
   bool bwd_tables;  // the per-tile backward (sv_de) ran for the last dfwfm_train_forward
   bool bwd_fused_red;  // ... with the dense shallow reductions fused in (per-tile partials written)
   float* bwd_loss_sum; // ... and the loss gradient fused in too: the tiles' losses are partials, summed into this
+  bool deterministic;  // dfwfm_set_deterministic: fixed-order table scatter and split-K sums
   bool tables_set;
   bool dense_set;
 };
@@ -1079,7 +1080,10 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   // 3. categorical tables.  Default: the deterministic sorted scatter (one task per field and row kind, both table
   // families); DFWFM_SCATTER=atomic: the atomic scatter (privatised LDS tasks for small tables, global atomics for
   // large ones), whose sums come in arrival order (A/B only)
-  const bool atomic_scatter = getenv("DFWFM_SCATTER") && !strcmp(getenv("DFWFM_SCATTER"), "atomic");
+  // the table scatter: the atomic one (fast; sums in arrival order) unless deterministic mode, which sorts;
+  // DFWFM_SCATTER=atomic / sorted forces either (A/B)
+  const char* sc_env = getenv("DFWFM_SCATTER");
+  const bool atomic_scatter = sc_env ? strcmp(sc_env, "sorted") != 0 : !m->deterministic;
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && !atomic_scatter) {
     SortScatterArgs sa;
     memset(&sa, 0, sizeof sa);
@@ -1094,6 +1098,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     sa.sv_de = m->sv_de;
     sa.dlogit = dlogit;
     sa.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
+    if (const char* dg = getenv("DFWFM_SCATTER_DIAG")) sa.diag = atoi(dg);  // diagnostics only: results invalid
     const bool need2 = (m->flags & kNeedE) != 0, need1 = (m->flags & kFoTables) != 0;
     auto add = [&](float* g2, float* g1, const float* o2, const float* o1, int64_t c, int f, int kind,
                    int64_t rows) -> int {
@@ -1107,11 +1112,12 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
         sblocks = 0;
       }
       SortScatterTask& t = sa.t[sa.ntasks++];
-      // row buckets, one workgroup each: a few hundred samples per bucket for the large tables (4096 rows sort in
-      // 78 dependent LDS stages on one CU; eight buckets of ~512 in 45 shorter ones, on eight)
-      t.nbuck = (int8_t)(rows >= 64 ? 8 : rows >= 16 ? 4 : rows >= 4 ? 2 : 1);
+      // row buckets, one workgroup each: tables of at most 64 rows one row per bucket (no sort; a few hundred samples
+      // each), larger ones eight buckets of ~B/8 samples (sorted in 45 LDS stages at B = 4096, not 4096 keys' 78)
+      t.onerow = rows <= 64 ? 1 : 0;
+      t.nbuck = (int16_t)(rows <= 64 ? (rows > 0 ? rows : 1) : 8);
       t.block0 = sblocks;
-      t.pad = 0;
+      t.pad8 = 0;
       sblocks += t.nbuck;
       t.g2 = g2;
       t.g1 = g1;
@@ -1253,8 +1259,8 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
                     "changed after the workspace was sized?)", (long long)per_split * splits, (long long)m->dw_slices);
       d.splits = (int32_t)splits;
       d.rows_per_split = rows;
-      d.part = m->dw_part;
-      d.bpart = m->dw_bpart;
+      d.part = m->deterministic ? m->dw_part : nullptr;  // split slices (deterministic) or float atomics
+      d.bpart = m->deterministic ? m->dw_bpart : nullptr;
       d.blk0[1] = 0;
       for (int l = 1; l <= H; ++l) d.blk0[l + 1] = d.blk0[l] + d.nnb * d.nkb[l] * (int32_t)splits;
       e = red_pending ? launch_dw_reduce(d, d.blk0[H + 1], r, s) : launch_dw(d, d.blk0[H + 1], s);
@@ -1266,6 +1272,12 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     e = launch_reduce_final(r, s);
     if (e != hipSuccess) return hip_fail(e, "reduce launch");
   }
+  return DFWFM_OK;
+}
+
+int dfwfm_set_deterministic(dfwfm_model* m, int32_t on) {
+  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  m->deterministic = on != 0;
   return DFWFM_OK;
 }
 

@@ -256,7 +256,7 @@ struct ScatterArgs {
 // every row's contributions in a fixed order, so the gradients are the same bits on every run.
 constexpr int kSortSeg = 4096;      // samples sorted per pass (larger batches: passes in sample order)
 constexpr int kSortCh = 32;         // sorted positions per chunk of the segmented sums
-constexpr int kSortThreads = 256;
+constexpr int kSortThreads = 512;
 struct SortScatterTask {
   float* g2;            // second-order table grad (width D) or null
   float* g1;            // first-order table grad (width 1) or null
@@ -265,9 +265,10 @@ struct SortScatterTask {
   int32_t c;            // QR collisions (kind 1, 2)
   int16_t field;        // model field index
   int8_t kind;          // 0 plain row idx, 1 quotient row idx / c, 2 remainder row idx % c
-  int8_t nbuck;         // row buckets (row % nbuck), one workgroup each
+  int8_t pad8;
   int32_t block0;       // the task's first workgroup
-  int32_t pad;
+  int16_t nbuck;        // row buckets (row % nbuck), one workgroup each
+  int16_t onerow;       // nbuck == rows: every bucket holds one row (no sort needed)
 };
 static_assert(sizeof(SortScatterTask) == 48, "sort scatter task layout");
 constexpr int kSortScatterList = 64;  // tasks per launch (the list is a kernel argument, < 4 KiB)
@@ -282,6 +283,7 @@ struct SortScatterArgs {
   const float* sv_de;
   const float* dlogit;
   const float* lw;      // [F] or null (dfo = dlogit)
+  int32_t diag;         // diagnostics only (DFWFM_SCATTER_DIAG): 1 skip the sort, 2 skip the sums, 4 no row adds
 };
 size_t sort_scatter_lds_bytes(int D);
 

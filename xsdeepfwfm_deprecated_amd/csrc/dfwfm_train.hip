@@ -965,6 +965,83 @@ __device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid)
     }
 }
 
+// the same network with each thread's E consecutive keys in registers (np = E * NTH): stages of partner distance
+// j < E inside the thread, E <= j < 64 E across the wave (lane ^ j / E, no LDS and no barrier), and only the
+// distances past a wave through LDS -- at np = 512 on 512 threads 6 of the 45 stages take a barrier
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+template <int NTH, int E>
+__device__ __forceinline__ void bitonic_sort_reg(uint64_t* key, int tid) {
+  constexpr int np = NTH * E;
+  uint64_t x[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) x[e] = key[tid * E + e];
+  for (int k = 2; k <= np; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < E) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = tid * E + e;
+          if ((e & j) == 0) {
+            const bool asc = (i & k) == 0;
+            const uint64_t lo = x[e], hi = x[e + j];
+            if ((lo > hi) == asc) {
+              x[e] = hi;
+              x[e + j] = lo;
+            }
+          }
+        }
+      } else if (j < 64 * E) {
+        const int m = j / E;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = tid * E + e;
+          const uint64_t y = shfl_xor_u64(x[e], m);
+          const bool asc = (i & k) == 0, lower = (i & j) == 0;
+          const bool take_min = asc == lower;
+          x[e] = take_min ? (y < x[e] ? y : x[e]) : (y > x[e] ? y : x[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) key[tid * E + e] = x[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = tid * E + e;
+          const uint64_t y = key[i ^ j];
+          const bool asc = (i & k) == 0, lower = (i & j) == 0;
+          const bool take_min = asc == lower;
+          x[e] = take_min ? (y < x[e] ? y : x[e]) : (y > x[e] ? y : x[e]);
+        }
+        __syncthreads();
+      }
+    }
+#pragma unroll
+  for (int e = 0; e < E; ++e) key[tid * E + e] = x[e];
+  __syncthreads();
+}
+
+// np keys (a power of two, 2 <= np <= kSortSeg) in LDS, sorted ascending in place
+template <int NTH>
+__device__ __forceinline__ void sort_keys(uint64_t* key, int np, int tid) {
+  if (np <= NTH) {
+    // pad to NTH keys (sentinels sort last), one per thread
+    for (int i = np + tid; i < NTH; i += NTH) key[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_reg<NTH, 1>(key, tid);
+  } else if (np == 2 * NTH) {
+    bitonic_sort_reg<NTH, 2>(key, tid);
+  } else if (np == 4 * NTH) {
+    bitonic_sort_reg<NTH, 4>(key, tid);
+  } else if (np == 8 * NTH) {
+    bitonic_sort_reg<NTH, 8>(key, tid);
+  } else {
+    bitonic_sort_lds<NTH>(key, np, tid);
+  }
+}
+
 __host__ __device__ inline int sort_scatter_nch() { return kSortSeg / kSortCh; }
 
 __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterArgs a) {
@@ -994,6 +1071,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
   }
   const SortScatterTask T = a.t[lo];
   const int bucket = bid - T.block0, nbuck = T.nbuck;
+  if (a.diag & 8) return;
   const FieldDev fd = a.fields[T.field];
   const int f = T.field, col = f - a.num;
   const float lwf = a.lw ? a.lw[f] : 1.f;
@@ -1019,12 +1097,16 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
           part = idx / T.c;
           row = idx - part * T.c;
         }
-        if ((int)(row % nbuck) == bucket) {
+        if ((int)((uint32_t)row % (uint32_t)nbuck) == bucket) {  // rows < 2^31
           rw[u] = row;
           pt[u] = (int32_t)part;
           ++kept;
         }
       }
+    }
+    if (a.diag & 16) {  // diagnostics: the key loads only
+      if (kept == 99999) cnt_s[0] = (int)rw[0];
+      return;
     }
     cnt_s[tid] = kept;
     __syncthreads();
@@ -1051,7 +1133,8 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
       while (np < n) np <<= 1;
       for (int i = n + tid; i < np; i += NTH) key[i] = ~0ull;
       __syncthreads();
-      bitonic_sort_lds<NTH>(key, np, tid);
+      // one row per bucket (small tables): the keys are already in order (sample order, one run)
+      if (!(a.diag & 1) && !T.onerow) sort_keys<NTH>(key, np, tid);
       const int nch = (n + CH - 1) / CH;
       for (int c = tid; c < nch; c += NTH) {
         const int p0 = c * CH, p1 = (p0 + CH < n ? p0 + CH : n) - 1;
@@ -1064,7 +1147,8 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
       // 3. runs inside each chunk.  Items: (chunk, d) of the second-order family with d fastest -- the lanes of one
       // chunk read one sample's 40-byte dE row per position and add one 40-byte table row per run: coalesced --
       // then one item per chunk for the first-order family
-      const int n2 = T.g2 ? nch * D : 0, n1 = T.g1 ? nch : 0;
+      const int n2 = (T.g2 && !(a.diag & 2)) ? nch * D : 0, n1 = (T.g1 && !(a.diag & 2)) ? nch : 0;
+      const bool adds = !(a.diag & 4);
       auto item = [&](int it, int& c, int& j) {
         if (it < n2) {
           c = it / D;
@@ -1107,7 +1191,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
           if (q < cnt) {
             if (rq[q] != cur) {  // a run ends inside the chunk
               if (first && (fl & 1)) lead[c * ncomp + j] = sum;
-              else atomicAdd(g + (int64_t)cur * w + jj, sum);  // the row's only adder in this pass
+              else if (adds) atomicAdd(g + (int64_t)cur * w + jj, sum);  // the row's only adder in this pass
               first = false;
               cur = rq[q];
               sum = 0.f;
@@ -1117,7 +1201,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
         }
         if (first && (fl & 1)) lead[c * ncomp + j] = sum;  // continues from the previous chunk (maybe into the next)
         else if (fl & 2) trail[c * ncomp + j] = sum;     // its head is here, its tail in the next chunk(s)
-        else atomicAdd(g + (int64_t)cur * w + jj, sum);
+        else if (adds) atomicAdd(g + (int64_t)cur * w + jj, sum);
       }
       __syncthreads();
       // 4. runs cut by chunk ends: the chunk with the head adds its trail and the following chunks' leads in order
@@ -1137,7 +1221,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
         }
         const int p1 = c * CH + CH - 1;  // a chunk with a continuing last run is full
         const uint32_t row = (uint32_t)(key[p1] >> 12);
-        atomicAdd(g + (int64_t)row * (fam2 ? D : 1) + (fam2 ? j : 0), sum);
+        if (adds) atomicAdd(g + (int64_t)row * (fam2 ? D : 1) + (fam2 ? j : 0), sum);
       }
     }
     // the next pass's adds to the same rows come after these (this workgroup's own atomics, retired before the
@@ -1297,10 +1381,11 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
     }
   }
   __syncthreads();
-  // Deterministic split-K: with one split the block is added to dW (and db) directly -- one writer per element.
-  // Otherwise every split writes its block to its own slice of a.part and the next launch (dw_sum_kernel) adds the
-  // slices in split order: the same bits on every run (the split-K float atomics this replaces summed in arrival
-  // order; a last-split ticket needs device-scope fences, whose L2 write-backs cost more than the launch).
+  // Split-K: with one split the block is added to dW (and db) directly -- one writer per element.  Otherwise by
+  // default float atomics (the splits summed in arrival order: the last bits differ run to run); deterministic mode
+  // (a.part set) writes every split's block to its own slice and the next launch (dw_sum_kernel) adds the slices in
+  // split order -- the same bits on every run (+7 us at Criteo-39; a last-split ticket instead needs device-scope
+  // fences, whose L2 write-backs cost more than the launch).
   constexpr int BE = kDwrT * kDwrT;
   const int splits = a.splits;
   const int ublk = a.blk0[l] / splits + rem;  // the block's index over all layers, without the split
@@ -1310,8 +1395,19 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
 #pragma unroll
     for (int w = 1; w < NW; ++w) bsum += bred[w][tid];
   }
+  if (splits > 1 && !a.part) {
+    // the default (fast) form: float atomics, one per element per split -- the sum of the splits in arrival order
+    if (gB && tid < kDwrT && n0 + tid < N) atomicAdd(gB + n0 + tid, bsum);
+    if (!gW) return;
+    for (int e = tid; e < BE; e += 64 * NW) {  // consecutive lanes on consecutive k of a row: 256 contiguous bytes
+      const int r = e / kDwrT, c = e - r * kDwrT;
+      const int n = n0 + r, k = k0 + c;
+      if (n < N && k < K) atomicAdd(gW + (int64_t)n * K + k, red[0][r][c] + red[1][r][c]);
+    }
+    return;
+  }
   if (splits > 1) {
-    // this split's block and column sums to its slices; dw_sum_kernel adds the slices in split order
+    // deterministic: this split's block and column sums to its slices; dw_sum_kernel adds them in split order
     float* mine = a.part + ((size_t)ublk * splits + split) * BE;
     for (int e = tid; e < BE; e += 64 * NW) {
       const int r = e / kDwrT, c = e - r * kDwrT;
@@ -1639,7 +1735,7 @@ hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream
 }
 
 static hipError_t launch_dw_sum(const DwArgs& a, hipStream_t s) {
-  if (a.splits <= 1) return hipSuccess;
+  if (a.splits <= 1 || !a.part) return hipSuccess;
   int64_t total = 0;
   for (int l = 1; l <= a.H; ++l) total += (a.gW[l] ? (int64_t)a.N * a.K[l] : 0) + (a.gB[l] ? a.N : 0);
   if (total <= 0) return hipSuccess;

@@ -234,6 +234,13 @@ class ForwardEngine:
         self._token = getattr(self, "_token", 0) + 1
         return self._token
 
+    def set_deterministic(self, on: bool) -> None:
+        """dfwfm_set_deterministic: fixed-order gradient sums (table scatter, split-K) for the backwards after it."""
+        on = bool(on)
+        if getattr(self, "_deterministic", None) != on:
+            _lib.check(_lib.lib().dfwfm_set_deterministic(self.handle, int(on)), "dfwfm_set_deterministic")
+            self._deterministic = on
+
     def backward(self, token: int, dlogit, field_grads, dense):
         """field_grads: per field (emb2, emb2_r, emb1, emb1_r) grad tensors or None; dense: dict of
         field_cov, fwfm_lin, fm_1st, bias, fc_w (tensor or None), lin_w / lin_b (lists)."""
@@ -351,6 +358,9 @@ class CpuEngine:
         self._token += 1
         self._train = (xi, xv, B, float(dropout_p), int(seed) & 0xFFFFFFFF)
         return self._token
+
+    def set_deterministic(self, on: bool) -> None:
+        """The host backward's sums are in a fixed order already (per-thread partials added in thread order)."""
 
     def backward(self, token, dlogit, field_grads, dense):
         if token != self._token or self._saved is None:

@@ -185,7 +185,7 @@ class FusedTrainStep:
 
     def __init__(self, model, batch_size, lr=1e-3, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8,
                  use_graph=True, dist=None, sparse_exchange=True, resident_inputs=False, max_graph_sets=8,
-                 max_many_sets=2):
+                 max_many_sets=2, deterministic=None):
         dev = model._device()
         if dev.type != "cuda":
             raise _lib.DfwfmError("FusedTrainStep runs only on a HIP device")
@@ -201,6 +201,8 @@ class FusedTrainStep:
         self._many_sets = {}  # step_many's K-step graphs, keyed like _graph_sets (their own LRU: no evictions of step()'s)
         self.eng = model._sync_engine(dev)
         self.L = _lib.lib()
+        # fixed-order gradient sums (bit-identical runs); default: the model's `deterministic` switch
+        self.deterministic = bool(model.deterministic if deterministic is None else deterministic)
         params = [p for p in model.parameters() if p.requires_grad]
         fields, dense = model._param_layout()
         known = {id(t) for tup in fields for t in tup if t is not None}
@@ -384,6 +386,7 @@ class FusedTrainStep:
 
     def _part1(self, n, denom, phases=None):
         L, st, h = self.L, self._stream(), self.eng.handle
+        self.eng.set_deterministic(self.deterministic)  # read when the backward launches are enqueued / captured
         # the dense weights re-packed and the gradient buffer zeroed in one launch
         _lib.check(L.dfwfm_model_set_dense_zero(h, *self.dense_args, ctypes.c_void_p(self.grad.data_ptr()),
                                                 self.grad.numel(), st), "dfwfm_model_set_dense_zero")
@@ -404,12 +407,14 @@ class FusedTrainStep:
             self._sparse_lists(st)
 
     def _backward_phase(self, phases):
+        self.eng.set_deterministic(self.deterministic)
         _lib.check(self.L.dfwfm_backward_phases(self.eng.handle, ctypes.c_void_p(self.dlogit.data_ptr()),
                                                 ctypes.byref(self.grads), phases, self._stream()),
                    "dfwfm_backward_phases")
 
     def _part1b(self):
         """The MLP weight gradients (dW_l, db_l): the backward's second part under data parallelism."""
+        self.eng.set_deterministic(self.deterministic)
         _lib.check(self.L.dfwfm_backward_phases(self.eng.handle, ctypes.c_void_p(self.dlogit.data_ptr()),
                                                 ctypes.byref(self.grads), _lib.BWD_MLP_WEIGHTS, self._stream()),
                    "dfwfm_backward_phases")
