@@ -31,6 +31,8 @@ constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_table
 constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
 constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
+constexpr int kP3Pieces = 8192; // MLP-free forward: FwFM as U' E pieces (11.25 MFMAs per sample) instead of per-sample
+                                // Gram tiles (18); DFWFM_P3_FWFM=gram|pieces
 // bwd_kernel diagnostics / A/B (DFWFM_DIAG_BWD=<bits> sets them << 20; off the flag range the model itself uses):
 // no G_l stores (results invalid), no mask loads (results invalid), the generic K loop instead of the static form
 constexpr int kBwdNoGStore = 1 << 20, kBwdNoMask = 1 << 21, kBwdGeneric = 1 << 22;
@@ -138,7 +140,7 @@ __host__ __device__ inline LdsLayout lds_layout(int F, int D, int MT, int S, int
   L.red = o;   o += (deep && KS == 2) ? 4 * TPW * 64 * 4 : 0;
   L.tailr = o; o += (deep && tail) ? NG * 64 * 4 + 4 * kBM : 0;  // partials + per-(wave, row) deep sums of the tail
   L.fo = o;    o += kBM * r4(F);
-  L.part2 = o; o += p3 ? kBM : MT * D * 16;  // per FwFM piece, its 16 column sums (p3: per sample)
+  L.part2 = o; o += p3 ? kBM * D : MT * D * 16;  // per FwFM piece, its 16 column sums (p3: per sample / column)
   L.dsum = o;  o += p3 ? 0 : NG * kBM;
   L.fs = o;    o += kBM;
   L.total = r4(o);

@@ -371,7 +371,7 @@ fwd_kernel(FwdArgs p) {
       DFWFM_PRELOAD(ls);
     }
     if constexpr (!QR)  // PART 3: behind the row loads (vmcnt retires in order); QR: no room
-      if (!(flags & kPairs)) load_uu();
+      if (!(flags & (kPairs | kP3Pieces))) load_uu();
     // ... the shallow parameters go to LDS while the row loads are in flight ...
 #pragma unroll
     for (int k = 0; k < kUpkPT; ++k) {
@@ -454,6 +454,58 @@ fwd_kernel(FwdArgs p) {
 #pragma unroll
       for (int o = LPS / 2; o >= 1; o >>= 1) part += __shfl_xor(part, o);
       if (j == 0) part2[b] = part;
+    } else if ((flags & kHasSecond) && (flags & kP3Pieces)) {
+      // MLP-free forward, FwFM as pieces: Y = U' E (rows k: fields, MT tiles of 16; columns n = b*D + d of the 16
+      // samples: D tiles of 16; contraction over l: S steps of 4, from step 4m on -- U' is strictly upper), column
+      // tile nt owned by wave nt % NW for every row tile m; second[b] = sum_{k,d} E[b,k,d] Y[k, b*D + d].  180
+      // MFMAs per 16 samples against the Gram's 288: the MFMA time, not only the latency, sets this kernel's rate in
+      // batch sets (five workgroups per CU).  U' fragments (A operands) arrive with the row loads (uf).
+      constexpr int MTC = P3_MTC;
+      constexpr int SMAX = 4 * MTC;
+      const int MT = p.MT, S = p.S;
+      float uf[MTC][SMAX];
+      {
+        const float* up = p.upack;
+#pragma unroll
+        for (int m = 0; m < MTC; ++m)
+#pragma unroll
+          for (int s = 0; s < SMAX; ++s)
+            uf[m][s] = (m < MT && s >= 4 * m && s < S) ? up[(m * S + s) * 64 + lane] : 0.f;
+      }
+      for (int nt = wave; nt < D; nt += NW) {
+        const int n = nt * 16 + (lane & 15);
+        const int b = n / D;
+        const int d = n - b * D;
+        const float* ecol = bufX + b * SX + d;  // E[b][l][d] = ecol[l * D]
+        float colv = 0.f;
+#pragma unroll
+        for (int m = 0; m < MTC; ++m) {
+          if (m >= MT) break;
+          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s0 = 4 * m; s0 < SMAX; s0 += 4) {
+            float bv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int s = s0 + u;
+              bv[u] = s < S ? ecol[(4 * s + (lane >> 4)) * D] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (s0 + u < S) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[m][s0 + u], bv[u], acc, 0, 0, 0);
+          }
+          float v = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 16 * m + 4 * (lane >> 4) + r;
+            v = fmaf(k < F ? ecol[(k < F ? k : 0) * D] : 0.f, acc[r], v);
+          }
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          colv += v;
+        }
+        if (lane < 16) part2[n] = colv;  // column n's sum over k (row tiles in order)
+      }
     } else if (flags & kHasSecond) {
       // MLP-free forward: second[b] = sum_{k<l} U'[k,l] <E_bk, E_bl> from the per-sample Gram G_b = E_b E_b^T
       // on MFMA (rows k, columns l, contraction over d: ceil(D/4) steps).  A sample's MT*ceil(D/4) operand
@@ -594,7 +646,11 @@ fwd_kernel(FwdArgs p) {
     }
     if (flags & kHasSecond) {
       if constexpr (PART == 3) {
-        second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
+        if (flags & kP3Pieces) {
+          for (int d = q; d < D; d += 16) second += part2[b * D + d];  // the sample's column sums
+        } else {
+          second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
+        }
       } else {
         const int MT = p.MT;
         for (int d = q; d < D; d += 16) {  // D = 32: two terms per lane
