@@ -477,33 +477,37 @@ fwd_kernel(FwdArgs p) {
         const int b = n / D;
         const int d = n - b * D;
         const float* ecol = bufX + b * SX + d;  // E[b][l][d] = ecol[l * D]
+        // the row tiles' chains side by side: step s's B operand (E column, one LDS read) feeds every row tile m
+        // with 4m <= s, each into its own accumulator
+        f32x4 acc[MTC];
+#pragma unroll
+        for (int m = 0; m < MTC; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s0 = 0; s0 < SMAX; s0 += 4) {
+          float bv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int s = s0 + u;
+            bv[u] = s < S ? ecol[(4 * s + (lane >> 4)) * D] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int m = 0; m < MTC; ++m)
+              if (4 * m <= s0 + u && s0 + u < S && m < MT)
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[m][s0 + u], bv[u], acc[m], 0, 0, 0);
+        }
         float colv = 0.f;
 #pragma unroll
         for (int m = 0; m < MTC; ++m) {
-          if (m >= MT) break;
-          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s0 = 4 * m; s0 < SMAX; s0 += 4) {
-            float bv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int s = s0 + u;
-              bv[u] = s < S ? ecol[(4 * s + (lane >> 4)) * D] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (s0 + u < S) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[m][s0 + u], bv[u], acc, 0, 0, 0);
-          }
-          float v = 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int k = 16 * m + 4 * (lane >> 4) + r;
-            v = fmaf(k < F ? ecol[(k < F ? k : 0) * D] : 0.f, acc[r], v);
+            colv = fmaf(k < F ? ecol[(k < F ? k : 0) * D] : 0.f, acc[m][r], colv);
           }
-          v += __shfl_xor(v, 16);
-          v += __shfl_xor(v, 32);
-          colv += v;
         }
+        colv += __shfl_xor(colv, 16);
+        colv += __shfl_xor(colv, 32);
         if (lane < 16) part2[n] = colv;  // column n's sum over k (row tiles in order)
       }
     } else if (flags & kHasSecond) {
@@ -646,7 +650,7 @@ fwd_kernel(FwdArgs p) {
     }
     if (flags & kHasSecond) {
       if constexpr (PART == 3) {
-        if (flags & kP3Pieces) {
+        if ((flags & kP3Pieces) && !(flags & kPairs)) {
           for (int d = q; d < D; d += 16) second += part2[b * D + d];  // the sample's column sums
         } else {
           second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
