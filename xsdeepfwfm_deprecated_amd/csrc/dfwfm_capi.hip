@@ -510,10 +510,11 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
-  // the MLP-free forward's FwFM form (A/B: DFWFM_P3_FWFM=gram|pieces)
+  // the MLP-free forward's FwFM form: U'E pieces (default; 2.34 vs 2.59 us per batch at 2000 steps, 2.85-2.90 vs
+  // 3.05 at 20, profiles/r05/r05l_*) or per-sample Gram tiles (DFWFM_P3_FWFM=gram, A/B)
   if (!m->cfg.use_deep) {
     static const char* p3 = getenv("DFWFM_P3_FWFM");
-    if (p3 && !strcmp(p3, "pieces")) a.flags |= kP3Pieces;
+    if (!(p3 && !strcmp(p3, "gram"))) a.flags |= kP3Pieces;
   }
   // the static K loop (fwd_kernel NS = 25) when every layer is 25 chunks deep and 25 tiles wide
   a.ns = (m->NC0 == 25 && m->NT == 25 && !getenv("DFWFM_NO_STATIC_K")) ? 25 : 0;
