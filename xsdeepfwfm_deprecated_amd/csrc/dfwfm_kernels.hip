@@ -472,61 +472,45 @@ fwd_kernel(FwdArgs p) {
           for (int s = 0; s < SMAX; ++s)
             uf[m][s] = (m < MT && s >= 4 * m && s < S) ? up[(m * S + s) * 64 + lane] : 0.f;
       }
-      // a wave's column tiles two at a time: up to 2 MTC chains side by side, step s's E columns (one LDS read per
-      // tile) feeding every row tile m with 4m <= s
-      auto tiles = [&](int nt0, auto TN_) {
-        constexpr int TN = decltype(TN_)::value;
-        int n[TN];
-        const float* ecol[TN];
+      for (int nt = wave; nt < D; nt += NW) {
+        const int n = nt * 16 + (lane & 15);
+        const int b = n / D;
+        const int d = n - b * D;
+        const float* ecol = bufX + b * SX + d;  // E[b][l][d] = ecol[l * D]
+        // the row tiles' chains side by side: step s's B operand (E column, one LDS read) feeds every row tile m
+        // with 4m <= s, each into its own accumulator (two column tiles at a time measured slower: 14.2k vs 11.6k
+        // cycles for the phase, profiles/r05/r05m_stP.log)
+        f32x4 acc[MTC];
 #pragma unroll
-        for (int t = 0; t < TN; ++t) {
-          n[t] = (nt0 + t * NW) * 16 + (lane & 15);
-          const int b = n[t] / D;
-          ecol[t] = bufX + b * SX + (n[t] - b * D);  // E[b][l][d] = ecol[l * D]
-        }
-        f32x4 acc[TN][MTC];
-#pragma unroll
-        for (int t = 0; t < TN; ++t)
-#pragma unroll
-          for (int m = 0; m < MTC; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int m = 0; m < MTC; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s0 = 0; s0 < SMAX; s0 += 4) {
-          float bv[TN][4];
+          float bv[4];
 #pragma unroll
-          for (int t = 0; t < TN; ++t)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int s = s0 + u;
-              bv[t][u] = s < S ? ecol[t][(4 * s + (lane >> 4)) * D] : 0.f;
-            }
+          for (int u = 0; u < 4; ++u) {
+            const int s = s0 + u;
+            bv[u] = s < S ? ecol[(4 * s + (lane >> 4)) * D] : 0.f;
+          }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int m = 0; m < MTC; ++m)
-#pragma unroll
-              for (int t = 0; t < TN; ++t)
-                if (4 * m <= s0 + u && s0 + u < S && m < MT)
-                  acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[m][s0 + u], bv[t][u], acc[t][m], 0, 0, 0);
+              if (4 * m <= s0 + u && s0 + u < S && m < MT)
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[m][s0 + u], bv[u], acc[m], 0, 0, 0);
         }
+        float colv = 0.f;
 #pragma unroll
-        for (int t = 0; t < TN; ++t) {
-          float colv = 0.f;
+        for (int m = 0; m < MTC; ++m) {
 #pragma unroll
-          for (int m = 0; m < MTC; ++m) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int k = 16 * m + 4 * (lane >> 4) + r;
-              colv = fmaf(k < F ? ecol[t][(k < F ? k : 0) * D] : 0.f, acc[t][m][r], colv);
-            }
+          for (int r = 0; r < 4; ++r) {
+            const int k = 16 * m + 4 * (lane >> 4) + r;
+            colv = fmaf(k < F ? ecol[(k < F ? k : 0) * D] : 0.f, acc[m][r], colv);
           }
-          colv += __shfl_xor(colv, 16);
-          colv += __shfl_xor(colv, 32);
-          if (lane < 16) part2[n[t]] = colv;  // column n's sum over k (row tiles in order)
         }
-      };
-      int nt = wave;
-      for (; nt + NW < D; nt += 2 * NW) tiles(nt, std::integral_constant<int, 2>{});
-      if (nt < D) tiles(nt, std::integral_constant<int, 1>{});
+        colv += __shfl_xor(colv, 16);
+        colv += __shfl_xor(colv, 32);
+        if (lane < 16) part2[n] = colv;  // column n's sum over k (row tiles in order)
+      }
     } else if (flags & kHasSecond) {
       // MLP-free forward: second[b] = sum_{k<l} U'[k,l] <E_bk, E_bl> from the per-sample Gram G_b = E_b E_b^T
       // on MFMA (rows k, columns l, contraction over d: ceil(D/4) steps).  A sample's MT*ceil(D/4) operand
