@@ -1156,30 +1156,39 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     if (e != hipSuccess) return hip_fail(e, "scatter launch");
   }
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && atomic_scatter) {
-    ScatterArgs priv, atom;
-    memset(&priv, 0, sizeof priv);
-    priv.D = D;
-    priv.F = F;
-    priv.num = num;
-    priv.fields = m->d_fields;
-    priv.xi = m->t_xi;
-    priv.xi_stride = m->t_xs;
-    priv.batch = batch;
-    priv.sv_de = m->sv_de;
-    priv.dlogit = dlogit;
-    priv.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
-    memcpy(&atom, &priv, sizeof priv);
-    priv.chunk = 256;   // more workgroups: the privatised tasks alone would not fill the chip
-    atom.chunk = 256;
-    const int64_t pchunks = (batch + priv.chunk - 1) / priv.chunk;
-    const int64_t achunks = (batch + atom.chunk - 1) / atom.chunk;
-    int blocks[2] = {0, 0};  // [atomic, priv]
-    auto flush = [&](bool is_priv) -> int {
-      ScatterArgs& L = is_priv ? priv : atom;
-      if (L.ntasks == 0) return DFWFM_OK;
-      hipError_t er = is_priv ? launch_scatter_priv(L, blocks[1], s) : launch_scatter(L, blocks[0], s);
+    // privatised tasks (small tables: per-chunk LDS sums, one flush per touched row) and global-atomic tasks (large
+    // tables), one launch for both kinds: the privatised tasks first in the grid
+    ScatterArgs L;
+    memset(&L, 0, sizeof L);
+    L.D = D;
+    L.F = F;
+    L.num = num;
+    L.fields = m->d_fields;
+    L.xi = m->t_xi;
+    L.xi_stride = m->t_xs;
+    L.batch = batch;
+    L.sv_de = m->sv_de;
+    L.dlogit = dlogit;
+    L.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
+    L.chunk = 256;  // samples per workgroup (more workgroups: the privatised tasks alone would not fill the chip)
+    const int64_t nb = (batch + L.chunk - 1) / L.chunk;
+    ScatterTask pt[kScatterList], at[kScatterList];
+    int np = 0, na = 0;
+    auto flush = [&]() -> int {
       L.ntasks = 0;
-      blocks[is_priv] = 0;
+      int64_t blocks = 0;
+      for (int i = 0; i < np; ++i, blocks += nb) {
+        L.t[L.ntasks] = pt[i];
+        L.t[L.ntasks++].block0 = (int32_t)blocks;
+      }
+      for (int i = 0; i < na; ++i, blocks += nb) {
+        L.t[L.ntasks] = at[i];
+        L.t[L.ntasks++].block0 = (int32_t)blocks;
+      }
+      np = na = 0;
+      if (L.ntasks == 0) return DFWFM_OK;
+      if (blocks > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "scatter grid too large");
+      hipError_t er = launch_scatter(L, (int)blocks, s);
       return er == hipSuccess ? DFWFM_OK : hip_fail(er, "scatter launch");
     };
     auto add = [&](float* gt, const float* other, int64_t c, int f, int kind, int src, int64_t rows) -> int {
@@ -1190,23 +1199,19 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       // their atomics well enough (DFWFM_PRIV_ROWS: tuning only)
       static const int64_t priv_rows = getenv("DFWFM_PRIV_ROWS") ? atoll(getenv("DFWFM_PRIV_ROWS")) : kPrivRows;
       const bool is_priv = rows * (w + 1) <= kPrivFloats && rows <= priv_rows;
-      ScatterArgs& L = is_priv ? priv : atom;
-      const int64_t nb = is_priv ? pchunks : achunks;
-      if (L.ntasks == kScatterList || blocks[is_priv] + nb > 0x7fffffff) {
-        int rc = flush(is_priv);
+      if (np + na == kScatterList || (int64_t)(np + na + 1) * nb > 0x7fffffff) {
+        int rc = flush();
         if (rc != DFWFM_OK) return rc;
       }
-      ScatterTask& t = L.t[L.ntasks];
+      ScatterTask& t = is_priv ? pt[np++] : at[na++];
       t.g = gt;
       t.other = other;
       t.c = (int32_t)c;
       t.field = (int16_t)f;
-      t.kind = (int8_t)kind;
+      t.kind = (int8_t)(kind | (is_priv ? kScatterPriv : 0));
       t.src = (int8_t)src;
       t.rows = (int32_t)(rows < 0x7fffffff ? rows : 0x7fffffff);
-      t.block0 = blocks[is_priv];
-      blocks[is_priv] += (int)nb;
-      L.ntasks++;
+      t.block0 = 0;
       return DFWFM_OK;
     };
     int rc = DFWFM_OK;
@@ -1225,13 +1230,13 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
           const bool mult = fd.op == 0;
           const float* tq = src == 0 ? fd.emb2 : fd.emb1;
           const float* tr = src == 0 ? fd.emb2_r : fd.emb1_r;
-          rc = add(gq, mult ? tr : nullptr, fd.c, f, 1, src, fd.n / fd.c);
+          // quotient rows: ceil(n / c) (weight_q's rows; an index past the last full group lands in the last row)
+          rc = add(gq, mult ? tr : nullptr, fd.c, f, 1, src, (fd.n + fd.c - 1) / fd.c);
           if (rc == DFWFM_OK) rc = add(gr, mult ? tq : nullptr, fd.c, f, 2, src, fd.c);
         }
       }
     }
-    if (rc == DFWFM_OK) rc = flush(true);
-    if (rc == DFWFM_OK) rc = flush(false);
+    if (rc == DFWFM_OK) rc = flush();
     if (rc != DFWFM_OK) return rc;
   }
 

@@ -231,12 +231,13 @@ struct ScatterTask {
   const float* other;   // QR mult: the partner table whose row multiplies the gradient (else null)
   int32_t c;            // QR collisions (kind 1, 2)
   int16_t field;        // model field index
-  int8_t kind;          // 0 plain row idx, 1 quotient row idx / c, 2 remainder row idx % c
+  int8_t kind;          // 0 plain row idx, 1 quotient row idx / c, 2 remainder row idx % c; | kScatterPriv
   int8_t src;           // 0: dE[b, f, :] (row width D), 1: dfo[b, f] = dlogit * (lw[f] or 1) (width 1)
   int32_t rows;         // table rows
   int32_t block0;       // first workgroup of the task in its launch
 };
 static_assert(sizeof(ScatterTask) == 32, "scatter task layout");
+constexpr int kScatterPriv = 64;  // ScatterTask::kind flag: a privatised (LDS-accumulated) task
 constexpr int kScatterList = 96;  // tasks per launch: the list is a kernel argument (< 4 KiB)
 struct ScatterArgs {
   ScatterTask t[kScatterList];
@@ -475,8 +476,8 @@ constexpr int kDwEdge = 80;
 constexpr int kDwRows = 64;  // four waves x whole groups of four four-row k-steps
 hipError_t launch_reduce(const RedArgs& a, hipStream_t s);  // both stages
 hipError_t launch_reduce_final(const RedArgs& a, hipStream_t s);  // the second stage only (bwd_kernel red)
+// privatised (kind | kScatterPriv) and global-atomic tasks in one launch
 hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s);
-hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_sort_scatter(const SortScatterArgs& a, int total_blocks, hipStream_t s);
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
                        float eps, float wd, float bc2_sqrt, hipStream_t s);

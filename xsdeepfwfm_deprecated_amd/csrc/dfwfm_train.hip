@@ -829,22 +829,12 @@ __global__ void __launch_bounds__(256) reduce_final_kernel(RedArgs a, int nblk) 
 // lane with global atomics.
 // ---------------------------------------------------------------------------
 template <bool PRIV>
-__global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
+__device__ __forceinline__ void scatter_body(const ScatterArgs& a, const ScatterTask& T, int bid, float* acc,
+                                             int32_t* srow, int32_t* spart) {
   // Lanes walk (sample, d) elements with d fastest, so one atomic wave-instruction adds ~6 rows of
   // 4*w contiguous bytes instead of 64 lanes hitting 64 different rows (~17x slower on gfx950,
   // MI355X_MICROARCH.md, float atomics).  Each sample's row / partner row is located once into LDS.
-  extern __shared__ __attribute__((aligned(16))) float acc[];
-  __shared__ int32_t srow[4 * 256];
-  __shared__ int32_t spart[4 * 256];
   const int tid = threadIdx.x;
-  int lo = 0, hi = a.ntasks - 1;
-  const int bid = blockIdx.x;
-  while (lo < hi) {  // last task whose block0 <= bid
-    const int mid = (lo + hi + 1) >> 1;
-    if (a.t[mid].block0 <= bid) lo = mid;
-    else hi = mid - 1;
-  }
-  const ScatterTask T = a.t[lo];
   const FieldDev fd = a.fields[T.field];
   const int f = T.field, D = a.D, FD = a.F * D, w = T.src == 0 ? D : 1;
   const int col = f - a.num;
@@ -857,10 +847,11 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
     int64_t idx = a.xi[b * a.xi_stride + col];
     if (idx < 0 || idx >= fd.n) idx = 0;  // the forward clamped (and flagged) it the same way
     int64_t row = idx, part = 0;
-    if (T.kind == 1) {
+    const int kind = T.kind & 3;
+    if (kind == 1) {
       row = idx / T.c;
       part = idx - row * T.c;
-    } else if (T.kind == 2) {
+    } else if (kind == 2) {
       part = idx / T.c;
       row = idx - part * T.c;
     }
@@ -932,6 +923,24 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
         if (at[u] >= 0) atomicAdd(T.g + at[u], v[u]);
     }
   }
+}
+
+// Both kinds of scatter tasks in one launch (privatised tasks first; they are independent of the global-atomic ones):
+// the small tables' LDS accumulation runs beside the large tables' atomics instead of one launch after the other
+__global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float acc[];
+  __shared__ int32_t srow[4 * 256];
+  __shared__ int32_t spart[4 * 256];
+  int lo = 0, hi = a.ntasks - 1;
+  const int bid = blockIdx.x;
+  while (lo < hi) {  // last task whose block0 <= bid
+    const int mid = (lo + hi + 1) >> 1;
+    if (a.t[mid].block0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const ScatterTask T = a.t[lo];
+  if (T.kind & kScatterPriv) scatter_body<true>(a, T, bid, acc, srow, spart);
+  else scatter_body<false>(a, T, bid, acc, srow, spart);
 }
 
 // ---------------------------------------------------------------------------
@@ -1711,26 +1720,20 @@ hipError_t launch_reduce(const RedArgs& a, hipStream_t s) {
 
 hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s) {
   if (total_blocks <= 0 || a.ntasks <= 0) return hipSuccess;
-  if (a.chunk > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(scatter_kernel<false>, dim3(total_blocks), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_scatter_priv(const ScatterArgs& a, int total_blocks, hipStream_t s) {
-  if (total_blocks <= 0 || a.ntasks <= 0) return hipSuccess;
-  if (a.chunk > 4 * 256) return hipErrorInvalidValue;
-  // LDS for the largest table of this launch only (not kPrivFloats): more workgroups per CU
+  // LDS for the largest privatised table of this launch only (not kPrivFloats): more workgroups per CU
   size_t floats = 0;
   for (int i = 0; i < a.ntasks; ++i) {
+    if (!(a.t[i].kind & kScatterPriv)) continue;
+    if (a.chunk > 4 * 256) return hipErrorInvalidValue;
     const size_t f = (size_t)a.t[i].rows * ((a.t[i].src == 0 ? a.D : 1) + 1);
     floats = f > floats ? f : floats;
   }
   if (floats > (size_t)kPrivFloats) return hipErrorInvalidValue;
+  if (a.chunk > 256) return hipErrorInvalidValue;  // the srow / spart staging of a chunk
   const size_t lds = sizeof(float) * (floats > 0 ? floats : 1);
-  auto k = scatter_kernel<true>;
-  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(k), lds);
+  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(scatter_kernel), lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(total_blocks), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(scatter_kernel, dim3(total_blocks), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
