@@ -1093,3 +1093,41 @@ def test_autograd_backward_deterministic_switch(gpu):
         got.append({k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()})
     for k in got[0]:
         assert np.array_equal(got[0][k], got[1][k]), k
+
+
+@pytest.mark.parametrize("qr,drop,B", [(False, True, 4096), (False, False, 4000), (True, True, 1000)])
+def test_helper_wave_train_forward_bit_identical(gpu, monkeypatch, qr, drop, B):
+    """The training forward with helper waves (ftrain_kernel: the shallow part and the activation saves on four waves
+    beside the MLP's eight) against fwd_kernel<TRAIN> (DFWFM_FTRAIN=0), Criteo-39 sizes, 3x400 MLP: two deterministic
+    fused steps give the same logits and the same parameters bit for bit (every saved activation feeds the
+    backward), with and without deep dropout, QR tables, and a ragged last tile."""
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    sizes = synth.CRITEO_FEATURE_SIZES
+    bats = []
+    for i in range(2):
+        xi, xv = synth.synth_inputs(sizes, 13, B, seed=70 + i)
+        bats.append((torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu),
+                     torch.from_numpy((np.arange(B) % 3 == i).astype(np.float32)).to(gpu)))
+    res = []
+    for ft in ("0", "1"):
+        monkeypatch.setenv("DFWFM_FTRAIN", ft)
+        torch.manual_seed(5)
+        kw = dict(embedding_bag=1, qr_flag=1, qr_operation="mult", qr_collisions=4, qr_threshold=200) if qr else {}
+        m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1,
+                    is_deep_dropout=drop, **kw).to(gpu).train()
+        m.init_weights()
+        torch.manual_seed(9)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, deterministic=True)
+        outs = []
+        for b in bats:
+            t.step(*b)
+            outs.append(t.out.detach().cpu().numpy().copy())
+        torch.cuda.synchronize()
+        res.append((outs, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}))
+        t.close()
+        del m
+    for o0, o1 in zip(res[0][0], res[1][0]):
+        assert np.array_equal(o0, o1)
+    for n in res[0][1]:
+        assert np.array_equal(res[0][1][n], res[1][1][n]), n

@@ -68,6 +68,11 @@ names = ["stage (params, Xi/Xv)", "gather E + table first order", "shallow (fwlw
          "MLP layer 3", "deep reduce + combine"]
 slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (11, 7), (7, 3), (3, 4), (3, 12), (12, 13),
          (13, 4), (4, 5), (5, 6), (6, 8)]
+if int(os.environ.get("DFWFM_DIAG_FT", "0")) & 1:  # ftrain_kernel: each wave's HW_ID in slot `wave`
+    for w in range(min(4, n)):
+        print(f"workgroup {w}: wave -> SIMD", [int((st[w, k] >> 4) & 3) for k in range(12)],
+              "CU", [int((st[w, k] >> 8) & 15) for k in range(12)])
+    sys.exit(0)
 rt0, rt1 = st[:, 14], st[:, 15] & ((1 << 48) - 1)
 life = (rt1 - rt0) / 100.0
 span = (rt1.max() - rt0.min()) / 100.0
@@ -88,6 +93,12 @@ if a.fwfm:  # no MLP: stage, gather, shallow phases, then the combine (slot 8)
              "  . fwlw first order", "  . FwFM MFMA (wave 0)", "  . barrier wait", "  . sums (wave 0)",
              "  . barrier + logits out"]
     slots = [(0, 1), (1, 2), (2, 8), (2, 9), (9, 10), (10, 11), (11, 7), (7, 8)]
+elif a.train and os.environ.get("DFWFM_FTRAIN", "1") != "0":  # ftrain_kernel: helper waves beside the MLP
+    names = ["stage (params, Xi/Xv)", "gather E (+ X_0) to LDS", "  helpers W0: FwFM pieces", "  helpers W0: fwlw, E / X_0",
+             "  helpers W1: sums, fo save, X_1", "  helpers W2: X_2", "MLP layer 1", "  . K loop (wave 0)",
+             "  . epilogue (wave 0)", "  . barriers, split tile", "MLP layer 2", "MLP layer 3", "combine"]
+    slots = [(0, 1), (1, 2), (2, 10), (10, 9), (4, 11), (5, 7), (3, 4), (3, 12), (12, 13), (13, 4), (4, 5), (5, 6),
+             (6, 8)]
 elif os.environ.get("DFWFM_R32") == "1":  # fwd32 has no slot 7
     names = names[:7] + names[9:]
     slots = slots[:7] + slots[9:]

@@ -27,6 +27,7 @@ struct dfwfm_model {
   int NG, TPWI, tailI; // inference forward: tile groups (waves, 4 or 8), tiles per wave, split tail
   int r32;             // 32-sample workgroups (fwd32_kernel) usable: 0 no, 1 when the stream's CUs are covered, 2 forced
   size_t lds_r32;
+  size_t lds_ftrain;   // the training forward with helper waves (ftrain_kernel), 0: not this model's form
   void* cu_stream[8];  // streams whose CU counts are cached (hipExtStreamGetCUMask), round-robin replaced
   int cu_count[8], cu_n, cu_next;
   int dev_cus;         // CUs of the device (0 until the first stream_cu_count)
@@ -277,6 +278,9 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
     const int mode = !r32 || !*r32 ? 1 : (atoi(r32) != 0 ? 2 : 0);
     m->r32 = (c.use_deep && fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG)) ? mode : 0;
     m->lds_r32 = m->r32 ? fwd32_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
+    m->lds_ftrain = (c.use_deep && ftrain_supported(F, D, H, NT, m->NC0, m->tailI, m->NG))
+                        ? ftrain_lds_bytes(F, D, m->MT, m->S, m->SX, m->SY) : 0;
+    if (m->lds_ftrain > 160 * 1024) m->lds_ftrain = 0;
     // DFWFM_R32_LDS=<bytes>: reserve at least this much LDS per workgroup (> 80 KiB: one workgroup per CU, so two
     // batches in flight on plain streams take disjoint halves of the chip; A/B against CU-masked streams)
     if (const char* pad = getenv("DFWFM_R32_LDS"))
@@ -937,7 +941,12 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   // the eight-wave layout when the model has it (DFWFM_NG=4 keeps the four-wave kernel)
   a.tail = m->tailI;
-  hipError_t e = launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, 1, m->NG, m->lds_inf, (hipStream_t)stream);
+  // the helper-wave form when the model has it (DFWFM_FTRAIN=0: fwd_kernel<TRAIN>, bit-identical, for A/B and tests)
+  if (const char* dg = getenv("DFWFM_DIAG_FT")) a.flags |= (atoi(dg) & 3) << 23;  // diagnostics only
+  const char* ft = getenv("DFWFM_FTRAIN");
+  const bool helpers = m->lds_ftrain > 0 && !(ft && atoi(ft) == 0);
+  hipError_t e = helpers ? launch_ftrain(a, m->D, m->lds_ftrain, (hipStream_t)stream)
+                         : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, 1, m->NG, m->lds_inf, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
   m->trained = true;
   return DFWFM_OK;

@@ -452,6 +452,11 @@ hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 bool fwd32_supported(int F, int D, int H, int NT, int NC0, int tailI, int NG);
 size_t fwd32_lds_bytes(int F, int D, int MT, int S, int SX);
 hipError_t launch_fwd32(const FwdArgs& a, int D, size_t lds, hipStream_t s);
+// the training forward with helper waves (dfwfm_ftrain.hip): the static 3x400 form only (ftrain_supported); logits
+// and saved activations bit-identical to fwd_kernel<TRAIN>'s
+bool ftrain_supported(int F, int D, int H, int NT, int NC0, int tailI, int NG);
+size_t ftrain_lds_bytes(int F, int D, int MT, int S, int SX, int SY);
+hipError_t launch_ftrain(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 // per-embedding-size launchers, each compiled in its own translation unit (-DDFWFM_KD=<D>)
 #define DFWFM_PER_D_CAT2(a, b) a##b
 #define DFWFM_PER_D_CAT(a, b) DFWFM_PER_D_CAT2(a, b)
