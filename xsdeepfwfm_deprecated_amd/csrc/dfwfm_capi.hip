@@ -514,10 +514,11 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.SX = m->SX;
   a.SY = m->SY;
   a.flags = m->flags;
-  // the MLP-free forward's FwFM form on four waves (batch sets): U'E pieces (default; 2.34 vs 2.59 us per batch at
-  // 2000 steps, 2.85-2.90 vs 3.05 at 20, profiles/r05/r05l_*) or per-sample Gram tiles (DFWFM_P3_FWFM=gram, A/B);
-  // the eight-wave form (one batch per launch) keeps the Gram tiles (its lone-call latency: 7.3 vs 7.7 us)
-  if (!m->cfg.use_deep) {
+  // the MLP-free forward's FwFM form: U'E pieces (default; batch sets 2.34 vs 2.59 us per batch at 2000 steps, 2.85-2.90
+  // vs 3.05 at 20, profiles/r05/r05l_*; a lone batch on eight waves 7.7 vs 7.3 us) or per-sample Gram tiles
+  // (DFWFM_P3_FWFM=gram, A/B) -- the same form for a batch set and a lone batch, so a set's logits stay bit-identical
+  // to each batch's own forward; pieces only while the U' fragments fit the eight-wave form's registers (MT <= 3)
+  if (!m->cfg.use_deep && m->MT <= 3) {
     static const char* p3 = getenv("DFWFM_P3_FWFM");
     if (!(p3 && !strcmp(p3, "gram"))) a.flags |= kP3Pieces;
   }

@@ -256,6 +256,9 @@ fwd_kernel(FwdArgs p) {
   // G[16m + 4(lane>>4) + r][16n + (lane&15)], and U'[k][l] sits in the pack at [(k/16) S + l/4][(k%16) + 16 (l%4)]
   constexpr int P3_MTC = NS > 0 ? NS : kMaxMT;  // row tiles (PART 3 instantiates NS = MT: no idle registers)
   constexpr int P3_NTL = PART == 3 ? P3_MTC * (P3_MTC + 1) / 2 : 1;  // upper tiles (m <= n)
+  // the U'E pieces form (kP3Pieces) while its U' fragments fit the eight-wave form's 80 registers (MT <= 3; the host
+  // asks for pieces only then, so a batch set and a lone batch take the same form: the same bits)
+  constexpr bool kPieces = PART == 3 && P3_MTC <= 3;
   float uu[P3_NTL][4];
   auto load_uu = [&]() {
     if constexpr (PART == 3) {
@@ -371,7 +374,7 @@ fwd_kernel(FwdArgs p) {
       DFWFM_PRELOAD(ls);
     }
     if constexpr (!QR)  // PART 3: behind the row loads (vmcnt retires in order); QR: no room
-      if (!(flags & kPairs) && !((flags & kP3Pieces) && NW == 4)) load_uu();
+      if (!(flags & kPairs) && !(kPieces && (flags & kP3Pieces))) load_uu();
     // ... the shallow parameters go to LDS while the row loads are in flight ...
 #pragma unroll
     for (int k = 0; k < kUpkPT; ++k) {
@@ -454,8 +457,8 @@ fwd_kernel(FwdArgs p) {
 #pragma unroll
       for (int o = LPS / 2; o >= 1; o >>= 1) part += __shfl_xor(part, o);
       if (j == 0) part2[b] = part;
-    } else if ((flags & kHasSecond) && (flags & kP3Pieces) && NW == 4) {
-      // MLP-free forward on four waves (batch sets, five workgroups per CU), FwFM as pieces: Y = U' E (rows k: fields, MT tiles of 16; columns n = b*D + d of the 16
+    } else if ((flags & kHasSecond) && kPieces && (flags & kP3Pieces)) {
+      // MLP-free forward (four waves in batch sets, five workgroups per CU; eight for a lone batch), FwFM as pieces: Y = U' E (rows k: fields, MT tiles of 16; columns n = b*D + d of the 16
       // samples: D tiles of 16; contraction over l: S steps of 4, from step 4m on -- U' is strictly upper), column
       // tile nt owned by wave nt % NW for every row tile m; second[b] = sum_{k,d} E[b,k,d] Y[k, b*D + d].  180
       // MFMAs per 16 samples against the Gram's 288: the MFMA time, not only the latency, sets this kernel's rate in
@@ -651,7 +654,7 @@ fwd_kernel(FwdArgs p) {
     }
     if (flags & kHasSecond) {
       if constexpr (PART == 3) {
-        if ((flags & kP3Pieces) && NW == 4 && !(flags & kPairs)) {
+        if (kPieces && (flags & kP3Pieces) && !(flags & kPairs)) {
           for (int d = q; d < D; d += 16) second += part2[b * D + d];  // the sample's column sums
         } else {
           second = q == 0 ? part2[b] : 0.f;  // the sample's Gram sum
