@@ -1393,8 +1393,8 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
   // Split-K: with one split the block is added to dW (and db) directly -- one writer per element.  Otherwise by
   // default float atomics (the splits summed in arrival order: the last bits differ run to run); deterministic mode
   // (a.part set) writes every split's block to its own slice and the next launch (dw_sum_kernel) adds the slices in
-  // split order -- the same bits on every run (+7 us at Criteo-39; a last-split ticket instead needs device-scope
-  // fences, whose L2 write-backs cost more than the launch).
+  // split order -- the same bits on every run (a last-split ticket instead needs device-scope fences, whose L2
+  // write-backs cost more than the launch).
   constexpr int BE = kDwrT * kDwrT;
   const int splits = a.splits;
   const int ublk = a.blk0[l] / splits + rem;  // the block's index over all layers, without the split
@@ -1440,38 +1440,56 @@ __global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
 }
 
 // the split slices of every weight / bias gradient element added in split order (the GEMM's second launch when it
-// splits the batch): one thread per element of dW_l (then of db_l), layer by layer
-__global__ void __launch_bounds__(256) dw_sum_kernel(DwArgs a, int64_t total) {
+// splits the batch): kDwSumParts workgroups per 80 x 80 block (16 of its rows each), its splits' slices contiguous --
+// every slice read in flight before the adds (one thread per element walking the layers with integer divisions took
+// 7.2 us at Criteo-39; one workgroup per block 13)
+constexpr int kDwSumParts = 5;
+__global__ void __launch_bounds__(256) dw_sum_kernel(DwArgs a) {
   constexpr int BE = kDwrT * kDwrT;
+  constexpr int BP = BE / kDwSumParts;  // elements of this workgroup's part
+  constexpr int PT = (BP + 255) / 256;
+  static_assert(BE % kDwSumParts == 0, "block parts");
   const int splits = a.splits;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    int64_t i = e;
-    int l = 1;
-    // weights of layer l (N x K), then its bias (N)
-    for (; l <= a.H; ++l) {
-      const int64_t nw = a.gW[l] ? (int64_t)a.N * a.K[l] : 0, nb = a.gB[l] ? a.N : 0;
-      if (i < nw + nb) break;
-      i -= nw + nb;
+  const int ub = blockIdx.x / kDwSumParts, part = blockIdx.x - ub * kDwSumParts;
+  int l = 1;
+  while (l < a.H && ub >= a.blk0[l + 1] / splits) ++l;
+  const int rem = ub - a.blk0[l] / splits;
+  const int nb = rem / a.nkb[l], kb = rem - nb * a.nkb[l];
+  const int n0 = nb * kDwrT, k0 = kb * kDwrT;
+  const int tid = threadIdx.x;
+  float* gW = a.gW[l];
+  if (gW) {
+    const int K = a.K[l];
+    const float* sl = a.part + (size_t)ub * splits * BE + part * BP;
+    float v[PT];
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int e = tid + 256 * j;
+      v[j] = e < BP ? sl[e] : 0.f;
     }
-    if (l > a.H) return;
-    const int64_t nw = a.gW[l] ? (int64_t)a.N * a.K[l] : 0;
-    const int ub0 = a.blk0[l] / splits;
-    if (i < nw) {
-      const int n = (int)(i / a.K[l]), k = (int)(i - (int64_t)n * a.K[l]);
-      const int nb = n / kDwrT, kb = k / kDwrT;
-      const float* sl = a.part + ((size_t)(ub0 + nb * a.nkb[l] + kb) * splits) * BE + (n - nb * kDwrT) * kDwrT +
-                        (k - kb * kDwrT);
-      float v = sl[0];
-      for (int sp = 1; sp < splits; ++sp) v += sl[(size_t)sp * BE];
-      a.gW[l][i] += v;
-    } else {
-      const int n = (int)(i - nw);
-      const int nb = n / kDwrT;
-      const float* bp = a.bpart + ((size_t)(ub0 + nb * a.nkb[l]) * splits) * kDwrT + (n - nb * kDwrT);
-      float v = bp[0];
-      for (int sp = 1; sp < splits; ++sp) v += bp[(size_t)sp * kDwrT];
-      a.gB[l][n] += v;
+    for (int sp = 1; sp < splits; ++sp) {
+      float w[PT];
+#pragma unroll
+      for (int j = 0; j < PT; ++j) {
+        const int e = tid + 256 * j;
+        w[j] = e < BP ? sl[(size_t)sp * BE + e] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < PT; ++j) v[j] += w[j];
     }
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int e = part * BP + tid + 256 * j;
+      const int r = e / kDwrT, c = e - r * kDwrT;
+      const int n = n0 + r, k = k0 + c;
+      if (tid + 256 * j < BP && n < a.N && k < K) gW[(int64_t)n * K + k] += v[j];
+    }
+  }
+  if (a.gB[l] && kb == 0 && part == 0 && tid < kDwrT && n0 + tid < a.N) {
+    const float* bp = a.bpart + (size_t)ub * splits * kDwrT + tid;
+    float v = bp[0];
+    for (int sp = 1; sp < splits; ++sp) v += bp[(size_t)sp * kDwrT];
+    a.gB[l][n0 + tid] += v;
   }
 }
 
@@ -1739,11 +1757,9 @@ hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s)
 
 static hipError_t launch_dw_sum(const DwArgs& a, hipStream_t s) {
   if (a.splits <= 1 || !a.part) return hipSuccess;
-  int64_t total = 0;
-  for (int l = 1; l <= a.H; ++l) total += (a.gW[l] ? (int64_t)a.N * a.K[l] : 0) + (a.gB[l] ? a.N : 0);
-  if (total <= 0) return hipSuccess;
-  const int64_t blocks = (total + 255) / 256;
-  hipLaunchKernelGGL(dw_sum_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s, a, total);
+  const int blocks = a.blk0[a.H + 1] / a.splits;  // unsplit 80 x 80 blocks over every layer
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dw_sum_kernel, dim3((unsigned)(blocks * kDwSumParts)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
