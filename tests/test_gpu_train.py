@@ -1095,12 +1095,13 @@ def test_autograd_backward_deterministic_switch(gpu):
         assert np.array_equal(got[0][k], got[1][k]), k
 
 
-@pytest.mark.parametrize("qr,drop,B", [(False, True, 4096), (False, False, 4000), (True, True, 1000)])
-def test_helper_wave_train_forward_bit_identical(gpu, monkeypatch, qr, drop, B):
+@pytest.mark.parametrize("qr,drop,B,depth", [(False, True, 4096, 3), (False, False, 4000, 3), (True, True, 1000, 3),
+                                             (False, True, 512, 1), (False, True, 700, 2)])
+def test_helper_wave_train_forward_bit_identical(gpu, monkeypatch, qr, drop, B, depth):
     """The training forward with helper waves (ftrain_kernel: the shallow part and the activation saves on four waves
     beside the MLP's eight) against fwd_kernel<TRAIN> (DFWFM_FTRAIN=0), Criteo-39 sizes, 3x400 MLP: two deterministic
     fused steps give the same logits and the same parameters bit for bit (every saved activation feeds the
-    backward), with and without deep dropout, QR tables, and a ragged last tile."""
+    backward), with and without deep dropout, QR tables, a ragged last tile, one and two hidden layers."""
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
     from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
     sizes = synth.CRITEO_FEATURE_SIZES
@@ -1114,7 +1115,7 @@ def test_helper_wave_train_forward_bit_identical(gpu, monkeypatch, qr, drop, B):
         monkeypatch.setenv("DFWFM_FTRAIN", ft)
         torch.manual_seed(5)
         kw = dict(embedding_bag=1, qr_flag=1, qr_operation="mult", qr_collisions=4, qr_threshold=200) if qr else {}
-        m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1,
+        m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1, h_depth=depth,
                     is_deep_dropout=drop, **kw).to(gpu).train()
         m.init_weights()
         torch.manual_seed(9)
