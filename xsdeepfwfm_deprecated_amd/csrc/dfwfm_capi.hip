@@ -943,7 +943,8 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   // the eight-wave layout when the model has it (DFWFM_NG=4 keeps the four-wave kernel)
   a.tail = m->tailI;
   // the helper-wave form when the model has it (DFWFM_FTRAIN=0: fwd_kernel<TRAIN>, bit-identical, for A/B and tests)
-  if (const char* dg = getenv("DFWFM_DIAG_FT")) a.flags |= (atoi(dg) & 3) << 23;  // diagnostics only
+  if (const char* dg = getenv("DFWFM_DIAG_FT"))  // diagnostics only (results invalid)
+    a.flags |= ((atoi(dg) & 1) ? kFtDiagHwId : 0) | ((atoi(dg) & 2) ? kFtDiagNoMlp : 0);
   const char* ft = getenv("DFWFM_FTRAIN");
   const bool helpers = m->lds_ftrain > 0 && !(ft && atoi(ft) == 0);
   hipError_t e = helpers ? launch_ftrain(a, m->D, m->lds_ftrain, (hipStream_t)stream)

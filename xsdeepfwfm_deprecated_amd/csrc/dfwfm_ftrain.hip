@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(kNTH) ftrain_kernel(FwdArgs p) {
   float* part2 = smem + L.part2;
   float* dsum = smem + L.dsum;
   float* fs = smem + L.fs;
-  uint64_t* const stamps = (flags & (1 << 23)) ? nullptr : p.stamps;  // HW_ID mode: no clocks
+  uint64_t* const stamps = (flags & kFtDiagHwId) ? nullptr : p.stamps;  // HW_ID mode: no clocks
   const TileRef tr = tile_ref<kBM>(p);
   const int64_t b0 = tr.b0;
   const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
@@ -105,9 +105,8 @@ __global__ void __launch_bounds__(kNTH) ftrain_kernel(FwdArgs p) {
   stamp(stamps, 0, tid);
   stamp_start_rt(stamps, tid);
 
-  // diagnostics (DFWFM_DIAG_FT=<bits> << 23, results invalid): bit 0 -- each wave's HW_ID into stamp slot `wave`
-  // instead of clocks; bit 1 -- the MLP waves skip their K loops
-  if ((flags & (1 << 23)) && p.stamps != nullptr && lane == 0)
+  // diagnostics (kFtDiagHwId: each wave's HW_ID into stamp slot `wave` instead of clocks; kFtDiagNoMlp)
+  if ((flags & kFtDiagHwId) && p.stamps != nullptr && lane == 0)
     p.stamps[(size_t)blockIdx.x * kStampSlots + wave] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
   const bool mlpw = wave < kNG;  // wave-uniform
   const int g = wave;            // MLP output-tile group (waves 0-7)
@@ -371,7 +370,7 @@ __global__ void __launch_bounds__(kNTH) ftrain_kernel(FwdArgs p) {
       for (int j = 0; j < kTPW; ++j) acc[j] = bq[j];
       ts.init(layer_off, NC, TT, g);
       f32x4 tp;
-      if (!(flags & (1 << 24)))
+      if (!(flags & kFtDiagNoMlp))
         mlp_k_loop_s<kTPW, kNG, kNS, true>(acc, in, SA, ls, wb0, wb1, wb2, lane, ts, tp);
       else
         tp = f32x4{0.f, 0.f, 0.f, 0.f};

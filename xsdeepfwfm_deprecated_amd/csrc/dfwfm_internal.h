@@ -36,6 +36,9 @@ constexpr int kP3Pieces = 8192; // MLP-free forward: FwFM as U' E pieces (11.25 
 // bwd_kernel diagnostics / A/B (DFWFM_DIAG_BWD=<bits> sets them << 20; off the flag range the model itself uses):
 // no G_l stores (results invalid), no mask loads (results invalid), the generic K loop instead of the static form
 constexpr int kBwdNoGStore = 1 << 20, kBwdNoMask = 1 << 21, kBwdGeneric = 1 << 22;
+// ftrain_kernel diagnostics (DFWFM_DIAG_FT=<bits> sets them << 23, results invalid): each wave's HW_ID into the stamp
+// slots instead of clocks; the MLP waves skip their K loops
+constexpr int kFtDiagHwId = 1 << 23, kFtDiagNoMlp = 1 << 24;
 constexpr int kMaxH = 16;      // hidden layers
 constexpr int kMaxSet = 32;    // batches per launch of dfwfm_forward_batches (the set is a kernel argument)
 
