@@ -30,7 +30,9 @@ def _inputs(sizes, nb, B, seed):
     return [synth.synth_inputs(sizes, 13, B, seed=seed + i) for i in range(nb)]
 
 
-def _check(cfg, params, m, gpu, host, sample=64):
+def _check(cfg, params, m, gpu, host):
+    """Every batch of the set bit-identical to its own forward; the first and the last batch -- every row (the
+    float64 oracle takes ~0.3 s per 4096 rows) -- against the oracle at the north-star bar."""
     eng = m._sync_engine(gpu)
     dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
     B = host[0][0].shape[0]
@@ -39,13 +41,11 @@ def _check(cfg, params, m, gpu, host, sample=64):
         eng.forward_batches(dev, outs)
         alone = [eng.forward(xi, xv) for xi, xv in dev]
     torch.cuda.synchronize()
-    rng = np.random.default_rng(B + len(host))
     for i, ((xi, xv), o, a) in enumerate(zip(host, outs, alone)):
         got = o.cpu().numpy()
         assert np.array_equal(got, a.cpu().numpy()), f"batch {i}: set vs alone"
-        rows = np.arange(B) if B <= sample else rng.choice(B, sample, replace=False)
         if i in (0, len(host) - 1):
-            assert logit_close(got[rows], dfwfm_oracle.forward(cfg, params, xi[rows], xv[rows])) < 1e-5
+            assert logit_close(got, dfwfm_oracle.forward(cfg, params, xi, xv)) < 1e-5, f"batch {i} vs oracle"
 
 
 @pytest.mark.parametrize("qr", [0, 1])
@@ -176,7 +176,7 @@ def test_batch_set_full_size_pruned_dense(gpu):
         assert 0.89 < z < 0.91, (h, z)
     eng = m._sync_engine(gpu)
     assert not eng.sync_sparse(m.sparse_mlp_max_density)
-    _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], 3, 4096, seed=4242), sample=256)
+    _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], 3, 4096, seed=4242))
 
 
 def test_forward_rejects_column_major_inputs(gpu):
