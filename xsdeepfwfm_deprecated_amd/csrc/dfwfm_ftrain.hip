@@ -348,6 +348,11 @@ __global__ void __launch_bounds__(kNTH) ftrain_kernel(FwdArgs p) {
     };
     f32x4 bq[kTPW];
     load_bias(bq, 0, 4 * (lane >> 4));
+    // E and X_0 (== E without dropout, zero padding columns included) to the workspace before layer 1's K loop:
+    // memory instructions the MLP waves issue while the matrix pipes are still free, so the helper waves run their
+    // FwFM pieces at full issue rate meanwhile (beside the K loop they crawl)
+    store_tile(p.sv_e + b0 * SE, SE, bufE, SX, nrows, SE / 4, tid, 64 * kNG);
+    if (drop) store_tile(p.sv_x[0] + b0 * SE, SE, bufX, SX, nrows, SE / 4, tid, 64 * kNG);
     int layer_off = 0;
     for (int h = 0; h < H; ++h) {
       int lv = lane;
@@ -454,7 +459,7 @@ __global__ void __launch_bounds__(kNTH) ftrain_kernel(FwdArgs p) {
       if (stamps != nullptr && htid == 0) stamps[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();
     };
     // The helpers' work in the MLP's windows (each ends at the barrier after that layer's K loop + epilogue):
-    //   [B1, A_0)       the FwFM pieces, fwlw first order, E and X_0 -> workspace
+    //   [B1, A_0)       the FwFM pieces, fwlw first order (E and X_0 leave from the MLP waves before their K loop)
     //   [B_0, A_1)      first + second sums, the first order, X_1 (layer 3 overwrites it after B_1)
     //   [B_{h-1}, A_h)  X_h, h >= 2
     // (X_H leaves from the MLP waves' registers.)  The pieces (m, nt) are fwd_kernel PART 0's chains and sums, each
@@ -566,9 +571,6 @@ __global__ void __launch_bounds__(kNTH) ftrain_kernel(FwdArgs p) {
         fo[b * Fp + f] = s;
       }
     }
-    // E and X_0 (== E without dropout), zero padding columns included
-    store_tile(p.sv_e + b0 * SE, SE, bufE, SX, nrows, SE / 4, htid, kHTH);
-    if (drop) store_tile(p.sv_x[0] + b0 * SE, SE, bufX, SX, nrows, SE / 4, htid, kHTH);
     hstamp(9);
     __syncthreads();  // A_0
     __syncthreads();  // B_0
