@@ -435,7 +435,10 @@ bwd_kernel(BwdArgs p) {
             } else if (k < FD) {
               float gv = acc[j][r];
               if (drop) gv = dropout_keep(dseed, 0, row, k, p.drop_p) ? gv * scale : 0.f;
-              bufD[b * SX + k] += gv;
+              // the final dE of this element: to LDS (the numerical fields' reduction) and to the workspace from here
+              const float v = bufD[b * SX + k] + gv;
+              bufD[b * SX + k] = v;
+              if (row < p.batch) p.sv_de[row * FD + k] = v;
             }
           }
         }
@@ -461,7 +464,9 @@ bwd_kernel(BwdArgs p) {
           } else if (k < FD) {
             float gv = sum;
             if (drop) gv = dropout_keep(dseed, 0, b0 + b, k, p.drop_p) ? gv * scale : 0.f;
-            bufD[b * SX + k] += gv;
+            const float v = bufD[b * SX + k] + gv;
+            bufD[b * SX + k] = v;
+            if (b0 + b < p.batch) p.sv_de[(b0 + b) * FD + k] = v;
           }
         }
         __syncthreads();
@@ -471,11 +476,14 @@ bwd_kernel(BwdArgs p) {
   }
   stamp(p.stamps, 8, tid);
 
-  // ---- P3: dE -> workspace (coalesced rows) ---------------------------------------
-  for (int i = tid; i < kBM * FD; i += NTH) {
-    const int b = i / FD;
-    const int c = i - b * FD;
-    if (b0 + b < p.batch) p.sv_de[(b0 + b) * FD + c] = bufD[b * SX + c];
+  // ---- P3: dE -> workspace (coalesced rows); with the MLP its layer-1 epilogue stored every element already (the
+  // store pass after the last barrier took ~5.8k cycles) -------------------------------------------------------
+  if (!deep) {
+    for (int i = tid; i < kBM * FD; i += NTH) {
+      const int b = i / FD;
+      const int c = i - b * FD;
+      if (b0 + b < p.batch) p.sv_de[(b0 + b) * FD + c] = bufD[b * SX + c];
+    }
   }
   if (red) {
     // numerical fields' second-order tables: E_f = v_f * Xv_f (:297-299) -> sum_b dE[b, f, :] * Xv[b, f]
