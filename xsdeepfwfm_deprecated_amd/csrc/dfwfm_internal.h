@@ -406,7 +406,7 @@ inline hipError_t ensure_lds_limit(const void* fn, size_t lds) {
 
 // One packing job of set_dense (see pack_dense_kernel).
 enum PackType : int32_t { kPackPad = 0, kPackLinear = 1, kPackLinearT = 2, kPackFwfm = 3, kPackFwfmSym = 4, kPackZero = 5 };
-constexpr int kPackZeroPT = 4;  // kPackZero: float4 written per thread (a job element = kPackZeroPT float4)
+constexpr int kPackZeroPT = 16;  // kPackZero: float4 written per thread (a job element = kPackZeroPT float4)
 struct PackJob {
   const float* src;
   float* dst;
