@@ -273,7 +273,11 @@ int dfwfm_bce_grad(const float* logits, const float* labels, int64_t n, double d
  * DFWFM_BWD_TILES or DFWFM_BWD_TABLES) forms dlogit from the training forward's logits and the labels with
  * dfwfm_bce_grad's arithmetic (the same dlogit bits), writes it to `dlogit` for the later phases and adds the
  * per-sample losses to *loss_sum (when non-NULL); one launch fewer per step.  A model without embeddings (no
- * per-tile backward) runs dfwfm_bce_grad then dfwfm_backward_phases. */
+ * per-tile backward) runs dfwfm_bce_grad then dfwfm_backward_phases.
+ * The loss is summed like the dense gradients: each 16-row tile's loss is a per-tile partial that the REDUCE phase
+ * (DFWFM_BWD_REDUCE, part of DFWFM_BWD_SPREAD / DFWFM_BWD_TABLES) adds in tile order, so *loss_sum is formed when
+ * that phase runs -- in this call, or in a later dfwfm_backward_phases call on the same training forward (the
+ * TILES-then-SPREAD split).  A caller that runs DFWFM_BWD_TILES and never runs REDUCE gets no loss. */
 int dfwfm_backward_phases_bce(dfwfm_model* m, const float* logits, const float* labels, double denom, float* dlogit,
                               float* loss_sum, const dfwfm_grads* grads, int32_t phases, void* stream);
 

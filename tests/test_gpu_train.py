@@ -557,7 +557,13 @@ def _sparse_step(m, gpu, xi, xv, y, sparse, split=False, bce_fused=False, extras
     if split:  # the per-tile backward, then the weight GEMM on a side stream beside the reductions + scatter
         ph = lambda bits, s_: _lib.check(L.dfwfm_backward_phases(  # noqa: E731
             eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(grads), bits, s_), "bwd phases")
-        ph(_lib.BWD_TILES, st)
+        if bce_fused:  # the loss gradient in the per-tile backward; its loss sum is formed by the later REDUCE
+            _lib.check(L.dfwfm_backward_phases_bce(eng.handle, ctypes.c_void_p(out.data_ptr()),
+                                                   ctypes.c_void_p(y_d.data_ptr()), float(len(xi)),
+                                                   ctypes.c_void_p(dl.data_ptr()), ctypes.c_void_p(loss.data_ptr()),
+                                                   ctypes.byref(grads), _lib.BWD_TILES, st), "bwd bce tiles")
+        else:
+            ph(_lib.BWD_TILES, st)
         side = torch.cuda.Stream(gpu)
         side.wait_stream(torch.cuda.current_stream(gpu))
         ph(_lib.BWD_MLP_WEIGHTS, ctypes.c_void_p(side.cuda_stream))
@@ -963,6 +969,25 @@ def test_backward_with_fused_bce_equals_separate(gpu, name):
         assert np.abs(g1[k] - g0[k]).max() <= G_TOL * sc + 1e-12, k
 
 
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_fwfm_nolw"])
+def test_backward_bce_tiles_then_spread_forms_loss(gpu, name):
+    """with the loss gradient fused into DFWFM_BWD_TILES, the tiles' losses are partials that the REDUCE
+    phase of a LATER call (DFWFM_BWD_SPREAD) sums into loss_sum: the split form gives the whole call's loss and
+    dlogit bits (include/dfwfm.h, dfwfm_backward_phases_bce)."""
+    cfg, params, xi, xv, y, *_ = load_train_golden(name)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    e0, e1 = {}, {}
+    g0, _, o0 = _sparse_step(m, gpu, xi, xv, y, sparse=False, bce_fused=True, extras=e0)
+    g1, _, o1 = _sparse_step(m, gpu, xi, xv, y, sparse=False, bce_fused=True, split=True, extras=e1)
+    assert np.array_equal(o0, o1)
+    assert np.array_equal(e0["dlogit"], e1["dlogit"])
+    assert e1["loss"] != 0.0
+    assert abs(e0["loss"] - e1["loss"]) <= 1e-6 * max(1.0, abs(e0["loss"]))
+    for k in g0:
+        sc = np.abs(g0[k]).max()
+        assert np.abs(g1[k] - g0[k]).max() <= G_TOL * sc + 1e-12, k
+
+
 @pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult", "train_fwfm_nolw"])
 def test_backward_tiles_spread_split_equals_whole(gpu, name):
     """DFWFM_BWD_TILES, then DFWFM_BWD_MLP_WEIGHTS on a second stream beside DFWFM_BWD_SPREAD (the one-GPU step's
@@ -1132,3 +1157,45 @@ def test_helper_wave_train_forward_bit_identical(gpu, monkeypatch, qr, drop, B, 
         assert np.array_equal(o0, o1)
     for n in res[0][1]:
         assert np.array_equal(res[0][1][n], res[1][1][n]), n
+
+
+@pytest.mark.parametrize("det", [False, True])
+def test_train_step_smaller_ragged_batch_after_larger(gpu, det):
+    """the weight-gradient GEMM's split slices are sized for the workspace's batch, but a smaller
+    ragged batch can round to MORE splits (39 x 10 inputs, two 320-wide layers: 36 blocks per split, cap 7; B = 1000
+    rounds to 192-row splits = 6, B = 896 to 128-row splits = 7).  A step at 1000 rows then one at 896 must both run
+    and match the training oracle, with the float-atomic and the deterministic split-K sums."""
+    from test_gpu_parity import _sweep_case
+    from xsdeepfwfm_deprecated_amd import synth
+    cfg, params, _, _ = _sweep_case(39, 13, 10, 320, 2, 0, seed=11)
+    xi, xv = synth.synth_inputs(cfg["feature_sizes"], 13, 1000, seed=12)
+    y = (np.arange(1000) % 3 == 0).astype(np.float32)
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    m.deterministic = det
+    hip_step(m, xi, xv, y, gpu, 1e-3, 3e-7)  # sizes the workspace for 1000 rows
+    p1 = {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}
+    B = 896
+    out, loss, grads, newp = hip_step(m, xi[:B], xv[:B], y[:B], gpu, 1e-3, 3e-7)
+    o_out, o_loss, og, onew = torch_port.train_step(cfg, p1, xi[:B], xv[:B], y[:B], 1e-3, 3e-7)
+    assert logit_close(out, o_out) < 1e-5
+    for k in og:
+        sc = np.abs(og[k]).max()
+        assert np.abs(grads[k] - og[k]).max() <= G_TOL * sc + 1e-12, k
+
+
+def test_fused_step_deterministic_change_recaptures(gpu):
+    """FusedTrainStep.deterministic is read at capture; changing it between steps selects another graph
+    set (the key holds it), so the new mode takes effect instead of replaying the old graphs."""
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    cfg, params, xi, xv, y, *_ = load_train_golden("train_small_mlp")
+    B = 32
+    m = build(cfg, params, gpu, is_deep_dropout=False)
+    t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, deterministic=False)
+    bats = [tuple(torch.from_numpy(a).to(gpu) for a in b) for b in _batches(cfg, xi, xv, y, B, 2)]
+    t.step(*bats[0])
+    k0 = t._graph_key
+    t.deterministic = True
+    t.step(*bats[1])
+    torch.cuda.synchronize()
+    assert t._graph_key != k0 and t._graph_key[2] is True
+    t.close()

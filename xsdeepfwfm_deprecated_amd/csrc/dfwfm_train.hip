@@ -952,8 +952,8 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Deterministic categorical-table scatter (the default; scatter_kernel's atomics add a row's contributions in
-// arrival order, so two runs of the same step differed in the last bits).  A task is one field and row kind, both
+// Deterministic categorical-table scatter (deterministic mode, dfwfm_set_deterministic; the default scatter_kernel's
+// atomics add a row's contributions in arrival order, so two runs of the same step can differ in the last bits).  A task is one field and row kind, both
 // table families at once; its rows are split into nbuck buckets (row % nbuck), one workgroup each, so every row has
 // ONE owner workgroup.  Per pass over <= kSortSeg samples the owner:
 //   1. keeps its bucket's samples in sample order (a block scan) as keys (row << 12 | sample) in LDS -- unique, so any

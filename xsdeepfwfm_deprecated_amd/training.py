@@ -196,7 +196,7 @@ class FusedTrainStep:
         self.use_graph = use_graph
         self.resident_inputs = bool(resident_inputs)
         self.max_graph_sets = max(1, int(max_graph_sets))
-        self._graph_sets = {}  # (denom, drop, workspace generation, input pointers) -> (graphs, inputs)
+        self._graph_sets = {}  # (denom, drop, deterministic, workspace generation, input pointers) -> (graphs, inputs)
         self.max_many_sets = max(1, int(max_many_sets))
         self._many_sets = {}  # step_many's K-step graphs, keyed like _graph_sets (their own LRU: no evictions of step()'s)
         self.eng = model._sync_engine(dev)
@@ -664,7 +664,8 @@ class FusedTrainStep:
             # the input pointers: one graph set per resident input buffer set
             # (slices of one large resident array get a new key per step: each is a capture, so fit() copies
             # its batches -- resident_inputs is for a fixed ring of input buffers)
-            key = (denom, self.drop, self._ws_generation(),
+            # (deterministic too: the graphs bake in the scatter / split-K form chosen at capture)
+            key = (denom, self.drop, self.deterministic, self._ws_generation(),
                    tuple((t.data_ptr(), tuple(t.stride())) for t in inputs))
             hit = self._graph_sets.pop(key, None)
             if hit is None:
@@ -708,7 +709,7 @@ class FusedTrainStep:
             raise RuntimeError("FusedTrainStep.step_many after close()")
         self.drop = self.drop_train if self.model.training else 0.0
         denom = float(self.B)
-        key = ("many", denom, self.drop, self._ws_generation(),
+        key = ("many", denom, self.drop, self.deterministic, self._ws_generation(),
                tuple((t.data_ptr(), tuple(t.stride())) for d in direct for t in d))
         hit = self._many_sets.pop(key, None)
         if hit is None:
