@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden, logit_close, model_kwargs
+from conftest import load_golden, logit_close, logit_close_scaled, model_kwargs
 from oracle import dfwfm_oracle
 
 pytestmark = pytest.mark.gpu
@@ -30,9 +30,10 @@ def _inputs(sizes, nb, B, seed):
     return [synth.synth_inputs(sizes, 13, B, seed=seed + i) for i in range(nb)]
 
 
-def _check(cfg, params, m, gpu, host):
+def _check(cfg, params, m, gpu, host, scaled=False):
     """Every batch of the set bit-identical to its own forward; the first and the last batch -- every row (the
-    float64 oracle takes ~0.3 s per 4096 rows) -- against the oracle at the north-star bar."""
+    float64 oracle takes ~0.3 s per 4096 rows) -- against the oracle at the north-star bar (scaled: the bar widened
+    by the row's absolute term sum, conftest.logit_close_scaled, for first-order sums without lw that cancel)."""
     eng = m._sync_engine(gpu)
     dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
     B = host[0][0].shape[0]
@@ -45,7 +46,9 @@ def _check(cfg, params, m, gpu, host):
         got = o.cpu().numpy()
         assert np.array_equal(got, a.cpu().numpy()), f"batch {i}: set vs alone"
         if i in (0, len(host) - 1):
-            assert logit_close(got, dfwfm_oracle.forward(cfg, params, xi, xv)) < 1e-5, f"batch {i} vs oracle"
+            ref = dfwfm_oracle.forward(cfg, params, xi, xv)
+            err = logit_close_scaled(got, ref, cfg, params, xi, xv) if scaled else logit_close(got, ref)
+            assert err < 1e-5, f"batch {i} vs oracle"
 
 
 @pytest.mark.parametrize("qr", [0, 1])
@@ -58,9 +61,11 @@ def test_batch_set_deep_bit_identical(gpu, qr, nb, B):
     _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], nb, B, seed=100 * nb + B))
 
 
-@pytest.mark.parametrize("nb,B", [(3, 4096), (6, 1000)])
+@pytest.mark.parametrize("nb,B", [(3, 4096), (6, 1000), (35, 256), (3, 4096 + 17), (2, 5), (20, 4096)])
 def test_batch_set_fwfm_only_bit_identical(gpu, nb, B):
-    """The MLP-free forward (BASELINE configs[0]'s model at Criteo-39 sizes) as a batch set."""
+    """The MLP-free forward (BASELINE configs[0]'s model at Criteo-39 sizes) as a batch set: the persistent LDS-DMA
+    forward (dfwfm_fwfm_dma.hip; more tiles than workgroups, ragged tails, fewer tiles than workgroups, two launches)
+    bit-identical to each batch's own forward (fwd_kernel), every row of the first and last batch vs the oracle."""
     cfg, params, m = _criteo_model(gpu, 0, 0, seed=91)
     _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], nb, B, seed=7 * nb + B))
 
@@ -206,3 +211,74 @@ def test_forward_rejects_column_major_inputs(gpu):
     rf = m.eval_by_batch(np.asfortranarray(xi), np.asfortranarray(xv), y, n)
     rc = m.eval_by_batch(xi, xv, y, n)
     assert rf[:2] == rc[:2]
+
+
+def _fwfm_only_case(F, num, D, lw, fm, seed):
+    from xsdeepfwfm_deprecated_amd import DeepFMs, synth
+    sizes = [1] * num + [int(x) for x in 7 + (np.arange(F - num) * 389 + seed) % 20000]
+    cfg = dict(field_size=F, feature_sizes=sizes, embedding_size=D, use_fwfm=1 - fm, use_fm=fm, use_logit=0,
+               use_deep=0, use_lw=lw, use_fwlw=0, h_depth=1, deep_nodes=16, numerical=num, embedding_bag=0,
+               qr_flag=0, qr_operation="mult", qr_collisions=4, qr_threshold=200)
+    m = DeepFMs(**model_kwargs(cfg))
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    params = synth.synth_state(shapes, F, D, 16, True, False, seed=seed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    return cfg, params, m
+
+
+# (F, numerical, D, lw, FM): FwFM row tiles 1 / 2 / 3 and every last-tile step count (S = 4 (MT - 1) + 1..4), no
+# numerical fields, plain first-order sum, FM instead of FwFM, D 4 / 8 / 10 / 16
+@pytest.mark.parametrize("F,num,D,lw,fm", [(39, 13, 10, 1, 0), (39, 13, 16, 1, 0), (48, 16, 8, 0, 0),
+                                           (20, 5, 4, 1, 1), (30, 0, 10, 1, 0), (9, 1, 10, 0, 0),
+                                           (33, 13, 10, 1, 0), (42, 2, 4, 1, 0), (16, 3, 16, 0, 1)])
+def test_fwfm_only_set_dma_shapes_bit_identical(gpu, monkeypatch, F, num, D, lw, fm):
+    """The LDS-DMA batch-set forward over model shapes: bit-identical to each batch alone and to the same set through
+    fwd_kernel's MLP-free form (DFWFM_P3_DMA=0), and within the north-star bar of the float64 oracle."""
+    cfg, params, m = _fwfm_only_case(F, num, D, lw, fm, seed=F * 100 + D)
+    m = m.to(gpu).eval()
+    from xsdeepfwfm_deprecated_amd import synth
+    host = [synth.synth_inputs(cfg["feature_sizes"], num, 1000 + F, seed=F + D + i) for i in range(5)]
+    _check(cfg, params, m, gpu, host, scaled=not lw)
+    dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
+    res = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("DFWFM_P3_DMA", v)
+        eng = m._sync_engine(gpu)
+        outs = [torch.empty(1000 + F, device=gpu) for _ in dev]
+        with torch.no_grad():
+            eng.forward_batches(dev, outs)
+        res[v] = torch.stack(outs).cpu().numpy()
+    assert np.array_equal(res["0"], res["1"])
+
+
+def test_fwfm_only_set_strided_inputs_and_out_of_range(gpu):
+    """The LDS-DMA forward reads Xi / Xv through any row stride and clamps an out-of-range index to row 0 with the
+    sticky flag (nn.Embedding's IndexError, raised by DeepFMs.forward), like fwd_kernel."""
+    cfg, params, m = _criteo_model(gpu, 0, 0, seed=13)
+    sizes = cfg["feature_sizes"]
+    host = _inputs(sizes, 4, 700, seed=9)
+    eng = m._sync_engine(gpu)
+    wide = [(torch.zeros(700, 31, dtype=torch.int64, device=gpu), torch.zeros(700, 17, device=gpu)) for _ in host]
+    for (wi, wv), (xi, xv) in zip(wide, host):
+        wi[:, :26] = torch.from_numpy(xi).to(gpu)
+        wv[:, :13] = torch.from_numpy(xv).to(gpu)
+    dev = [(wi[:, :26], wv[:, :13]) for wi, wv in wide]
+    outs = [torch.empty(700, device=gpu) for _ in dev]
+    with torch.no_grad():
+        eng.forward_batches(dev, outs)
+        alone = [eng.forward(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
+    for o, a in zip(outs, alone):
+        assert torch.equal(o, a)
+    assert eng.read_error_flag() == 0
+    wide[2][0][123, 7] = sizes[13 + 7]  # one past the last row of field 20
+    wide[3][0][699, 0] = -1
+    with torch.no_grad():
+        eng.forward_batches(dev, outs)
+    assert eng.read_error_flag() != 0
+    clamped = [t.clone() for t, _ in wide]
+    clamped[2][123, 7] = 0
+    clamped[3][699, 0] = 0
+    with torch.no_grad():
+        ref = [eng.forward(c[:, :26], wv[:, :13]) for c, (_, wv) in zip(clamped, wide)]
+    for o, a in zip(outs, ref):
+        assert torch.equal(o, a)

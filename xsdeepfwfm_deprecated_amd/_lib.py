@@ -23,7 +23,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
 # A/B of build variants only (e.g. libdfwfm_ns4.so built with DFWFM_HIPCC_FLAGS=-DDFWFM_NSETS=4)
 LOAD_PATH = os.path.join(PKG_DIR, os.environ["DFWFM_LIB"]) if os.environ.get("DFWFM_LIB") else LIB_PATH
-SOURCES = ["dfwfm_kernels.hip", "dfwfm_fwd32.hip", "dfwfm_ftrain.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_sparse.hip",
+SOURCES = ["dfwfm_kernels.hip", "dfwfm_fwd32.hip", "dfwfm_fwfm_dma.hip", "dfwfm_ftrain.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_sparse.hip",
            "dfwfm_spmlp.hip", "dfwfm_capi.hip"]
 # the forward / backward kernel templates are instantiated once per embedding size, each size in its own
 # translation unit (-DDFWFM_KD=<D>) so they compile in parallel; the plain object holds everything else

@@ -533,13 +533,18 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
 // The weight-gradient GEMM's grid for `batch` rows: 80 x 80 blocks per layer (per_split of them over all layers) in
 // `splits` batch splits of `rows` rows.  One workgroup per CU at most (tools/ubench_dw, Criteo-39, B = 4096: 3 splits
 // = 225 workgroups 42 us; 6 splits 47 us; past one round of workgroups 60+ us), each split over >= 128 rows.
-int dw_plan(const dfwfm_model* m, int64_t batch, int* per_split, int64_t* splits, int64_t* rows) {
+// `cap` (optional) = the split count before the rows are rounded to whole k-step groups: it bounds `splits` for this
+// batch AND for every smaller one (each term that sets it is non-decreasing in the batch), so slices sized from the
+// cap of the workspace's batch serve every ragged batch after it.
+int dw_plan(const dfwfm_model* m, int64_t batch, int* per_split, int64_t* splits, int64_t* rows,
+            int64_t* cap = nullptr) {
   const int edge = kDwEdge, quantum = kDwRows;
   const int nnb = (m->N + edge - 1) / edge;
   int ps = 0;
   for (int l = 1; l <= m->H; ++l) ps += nnb * (((l == 1 ? m->F * m->D : m->N) + edge - 1) / edge);
   *per_split = ps;
   *splits = *rows = 0;
+  if (cap) *cap = 0;
   if (ps == 0 || batch <= 0) return DFWFM_OK;
   int64_t sp = 256 / ps;
   if (const char* ds = getenv("DFWFM_DW_SPLITS")) sp = atoi(ds);  // tuning only
@@ -551,6 +556,7 @@ int dw_plan(const dfwfm_model* m, int64_t batch, int* per_split, int64_t* splits
   const int64_t rows_cap = ((0x7fffffffLL / (wmax * 4)) * 4 - 4 * quantum) / quantum * quantum;
   if (rows_cap < quantum) return fail(DFWFM_ERR_UNSUPPORTED, "MLP rows of %lld floats", (long long)wmax);
   if ((batch + sp - 1) / sp > rows_cap) sp = (batch + rows_cap - 1) / rows_cap;
+  if (cap) *cap = sp;
   int64_t r = (batch + sp - 1) / sp;
   r = (r + quantum - 1) / quantum * quantum;  // whole k-step groups per wave
   *splits = (batch + r - 1) / r;
@@ -568,10 +574,11 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   const int64_t red_blocks = (batch + kBM - 1) / kBM;
   const int64_t red_floats = red_blocks * red_outputs(m->F, m->D, m->N, m->num);
   int per_split = 0;
-  int64_t splits = 0, rows = 0;
-  int rc = dw_plan(m, batch, &per_split, &splits, &rows);
+  int64_t splits = 0, rows = 0, cap = 0;
+  int rc = dw_plan(m, batch, &per_split, &splits, &rows, &cap);
   if (rc != DFWFM_OK) return rc;
-  const int64_t slices = splits > 1 ? (int64_t)per_split * splits : 0;
+  // sized from the cap, not from this batch's rounded split count: a smaller (ragged) batch can round to more splits
+  const int64_t slices = cap > 1 ? (int64_t)per_split * cap : 0;
   const int64_t dw_floats = slices * (kDwEdge * kDwEdge + kDwEdge);  // the blocks' and the bias sums' slices
   if (m->d_ws) (void)hipFree(m->d_ws);
   m->d_ws = nullptr;
@@ -747,7 +754,14 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     }
     int rc = diag_stamps_buffer(m, (int64_t)n * a.tiles * rows, 1, &a.stamps);
     if (rc != DFWFM_OK) return rc;
+    // MLP-free sets: the persistent LDS-DMA forward (DFWFM_P3_DMA=0: fwd_kernel PART 3, A/B)
+    static const char* dma_env = getenv("DFWFM_P3_DMA");
+    bool dma = n > 1 && !m->cfg.use_deep && !(dma_env && atoi(dma_env) == 0) && fwfm_dma_supported(a, m->D);
+    for (int f = m->num; f < m->F && dma; ++f) dma = m->h_fields[f].n < 0x7fffffff;  // 32-bit row indices in LDS
+    if (dma)
+      if (const char* dg = getenv("DFWFM_DIAG_DMA")) a.flags |= atoi(dg) << 25;  // diagnostics only: results invalid
     const hipError_t e = r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
+                       : dma ? launch_fwfm_dma(a, m->D, (hipStream_t)stream)
                              : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
                                               (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "batch-set forward launch");
@@ -1095,11 +1109,9 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     }
   }
 
-  // 3. categorical tables.  Default: the deterministic sorted scatter (one task per field and row kind, both table
-  // families); DFWFM_SCATTER=atomic: the atomic scatter (privatised LDS tasks for small tables, global atomics for
-  // large ones), whose sums come in arrival order (A/B only)
-  // the table scatter: the atomic one (fast; sums in arrival order) unless deterministic mode, which sorts;
-  // DFWFM_SCATTER=atomic / sorted forces either (A/B)
+  // 3. categorical tables: the atomic scatter (privatised LDS tasks for small tables, global atomics for large ones;
+  // sums in arrival order) unless deterministic mode, which runs the sorted per-row-owner scatter (one task per field
+  // and row kind, both table families); DFWFM_SCATTER=atomic / sorted forces either (A/B)
   const char* sc_env = getenv("DFWFM_SCATTER");
   const bool atomic_scatter = sc_env ? strcmp(sc_env, "sorted") != 0 : !m->deterministic;
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && !atomic_scatter) {
@@ -1279,7 +1291,8 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       int64_t splits = 0, rows = 0;
       int rc = dw_plan(m, batch, &plan_blocks, &splits, &rows);
       if (rc != DFWFM_OK) return rc;
-      if (splits > 1 && (int64_t)per_split * splits > m->dw_slices)
+      // the slices are used only by the deterministic split-K sum; the float-atomic form never reads them
+      if (m->deterministic && splits > 1 && (int64_t)per_split * splits > m->dw_slices)
         return fail(DFWFM_ERR_STATE, "weight-gradient split slices: %lld needed, %lld allocated (DFWFM_DW_SPLITS "
                     "changed after the workspace was sized?)", (long long)per_split * splits, (long long)m->dw_slices);
       d.splits = (int32_t)splits;

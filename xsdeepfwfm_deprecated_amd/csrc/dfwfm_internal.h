@@ -446,6 +446,10 @@ hipError_t launch_metrics(const float* z, const float* y, int64_t n, double* out
 
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s);
+// the MLP-free batch-set forward as one persistent launch with LDS-DMA row gathers (dfwfm_fwfm_dma.hip): models with
+// FwFM / FM second order, first-order tables, no QR / pair list / fwlw, ceil(F / 16) <= 3, D in {4, 8, 10, 16}
+bool fwfm_dma_supported(const FwdArgs& a, int D);
+hipError_t launch_fwfm_dma(const FwdArgs& a, int D, hipStream_t s);
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
 // the split forward's first launch alone (gather + shallow part -> a.part_e / a.part_fs)
 hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream_t s);
