@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--sparse-mlp", type=float, default=None,
                     help="DeepFMs.sparse_mlp_max_density for this run (pruned config: the sparse deep tower when "
                          "the hidden layers' nonzero fraction is at most this); default: the model's")
+    ap.add_argument("--pack-tables", type=int, default=1,
+                    help="MLP-free configs: gather from the tables' serving copy (second + first order in one row; "
+                         "0: the plain tables, A/B)")
     ap.add_argument("--pair-max", type=int, default=None,
                     help="DeepFMs.fwfm_pair_max for this run (fwfm_pruned: 0 runs the dense Gram FwFM)")
     ap.add_argument("--cu-mask", choices=["none", "even-odd", "lo-hi"], default=None,
@@ -327,6 +330,7 @@ def main():
         model.fwfm_pair_max = 192  # the pair path (measured level with the dense Gram: DESIGN.md section 3.3)
     if a.pair_max is not None:
         model.fwfm_pair_max = a.pair_max
+    model.pack_tables = bool(a.pack_tables)
     if a.config in ("pruned", "fwfm_pruned"):
         # reference :647-673 with sparse=0.90, emb_r=0.444, prune_r=1 (main_all.py flags of config 4); FwFM-only:
         # R keeps 73 of 741 pairs and the forward sums those (dfwfm_model_build_fwfm_pairs)
@@ -366,7 +370,7 @@ def main():
         if M > 1 else None
 
     with torch.no_grad():
-        eng = model._sync_engine(dev)
+        eng = model._sync_inference(dev)  # (MLP-free configs: the tables' serving copy, built once here)
         if a.sparse_mlp is not None:
             model.sparse_mlp_max_density = a.sparse_mlp
         sparse_on = eng.sync_sparse(model.sparse_mlp_max_density) if deep else False
@@ -597,7 +601,6 @@ def main():
               "launches_in_flight": S}
     if cfg["use_deep"]:  # 98.5 % of the arithmetic is the MLP: MFMA-bound (intensity ~690 FLOP/B)
         result["roofline"] = {**mfma, **common}
-        result["roofline_hbm"] = hbm
     else:                # gather + FwFM only: ~12 FLOP/B, below the f32 ridge -> HBM-bound
         result["roofline"] = {**hbm, **common}
         if traffic:      # the fabric rate of the PMC-counted bytes (40-B rows fetched as 128-B lines)
@@ -610,6 +613,12 @@ def main():
                 "us_per_batch": floor_us, "frac": round(floor_us / (ms_per_step * 1e3), 4),
                 "source": "tools/ubench_gather.hip 3 (profiles/r02/r02q_ubench_gather_nb3.log)"}
         result["roofline_mfma"] = mfma
+    if deep and not a.no_per_call and not (a.config == "pruned" and sparse_on):
+        # north_star: "achieved HBM GB/s on the gather" -- the gather / shallow half as its own launch
+        gl = gather_leg(eng, batches, dev, a.steps, bytes_ - 4)
+        if world > 1:
+            gl["us_per_batch"] = round(max_over_ranks(gl["us_per_batch"], world, dev), 3)
+        result["roofline_gather"] = gl
     if not a.no_per_call and not (a.config == "pruned" and sparse_on):
         pc = per_call_leg(eng, batches, dev, a.steps, flops, bytes_, a.config)
         if world > 1:
@@ -665,6 +674,68 @@ def per_call_leg(eng, batches, dev, steps, flops, bytes_, config, settle_ms=150.
     else:
         res["mfma_frac"] = round(flops * BATCH / (us / 1e6) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)
     return res
+
+
+def gather_leg(eng, batches, dev, steps, read_bytes, settle_ms=100.0, streams=4):
+    """The deep forward's gather / shallow half alone (dfwfm_forward_gather: the split forward's first launch,
+    fwd_kernel PART 1 -- the per-field rows of model/DeepFMs.py:300-367 into deep_emb (:398), first + second order)
+    over the resident batches, one batch of 4096 per call, replayed from captured graphs like per_call: on one
+    stream (`lone`: one 16-sample tile per CU, the chain's latency) and with `streams` calls in flight (the
+    headline numbers: throughput).  `achieved` = the gather's algorithmic read bytes per sample (Xi, Xv, the
+    categorical rows, the first-order weights: what the fused kernel also reads) / its time; `achieved_incl_store`
+    adds this launch's own deep_emb + first/second stores, which the fused kernel keeps in LDS."""
+    G = max(1, min(20, steps))
+    n = len(batches)
+
+    def timed(S):
+        sts = [torch.cuda.Stream(dev) for _ in range(S)]
+        for st in sts:
+            st.wait_stream(torch.cuda.current_stream(dev))
+        gs = []
+        with torch.no_grad():
+            for k, st in enumerate(sts):
+                with torch.cuda.stream(st):
+                    E = eng.forward_gather(*batches[k % n])
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=st):
+                        for i in range(G):
+                            eng.forward_gather(*batches[(k * G + i) % n], E[0], E[1])
+                    gs.append(g)
+            reps = -(-steps // G)
+            t0 = time.perf_counter()
+            while (time.perf_counter() - t0) * 1e3 < settle_ms:
+                for k, st in enumerate(sts):
+                    with torch.cuda.stream(st):
+                        gs[k].replay()
+                torch.cuda.synchronize(dev)
+            e0 = [torch.cuda.Event(enable_timing=True) for _ in sts]
+            e1 = [torch.cuda.Event(enable_timing=True) for _ in sts]
+            for k, st in enumerate(sts):
+                e0[k].record(st)
+            for r in range(reps):
+                for k, st in enumerate(sts):
+                    with torch.cuda.stream(st):
+                        gs[k].replay()
+            for k, st in enumerate(sts):
+                e1[k].record(st)
+            torch.cuda.synchronize(dev)
+        first = min(range(S), key=lambda k: e0[0].elapsed_time(e0[k]))
+        last = max(range(S), key=lambda k: e0[0].elapsed_time(e1[k]))
+        return e0[first].elapsed_time(e1[last]) * 1e3 / (reps * G * S), reps * G * S, E[0].shape[1] * 4 + 4
+
+    us1, _, store = timed(1)
+    us, nb, store = timed(streams)
+    gbs = read_bytes * BATCH / (us / 1e6) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_sample": read_bytes,
+            "achieved_incl_store": round((read_bytes + store) * BATCH / (us / 1e6) / 1e9, 1),
+            "store_bytes_per_sample": store, "us_per_batch": round(us, 3), "batches": nb,
+            "in_flight": streams,
+            "lone": {"us_per_batch": round(us1, 3),
+                     "achieved": round(read_bytes * BATCH / (us1 / 1e6) / 1e9, 1)},
+            "kernel": "dfwfm::fwd_kernel<10,1,1,false,1,4,0,true> (dfwfm_forward_gather)",
+            "what": "the deep forward's gather / shallow half as its own launch per 4096-sample batch, "
+                    f"{streams} streams in flight (lone: one stream)"}
 
 
 def pmc_traffic(kname, workload_id, batches=1):

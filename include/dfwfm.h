@@ -141,6 +141,15 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
                      int64_t xv_stride, int64_t batch, float* out, void* workspace, size_t ws_bytes,
                      void* stream);
 
+/* The gather / shallow half of a deep model's forward alone (reference model/DeepFMs.py:300-367 and the deep_emb
+ * `cat` of :398): the per-field embedding rows (numerical v_f * Xv, categorical nn.Embedding / QR rows) into
+ * deep_emb [batch][deep_emb_stride] (zero padded past F * D) and first + second order into first_second[batch] --
+ * the split forward's first launch, so that the gather has its own duration and HBM rate (bench.py
+ * roofline_gather).  deep_emb_stride must equal ceil(F * D / 16) * 16 (the MLP's K chunks).  Models without a
+ * deep tower: DFWFM_ERR_UNSUPPORTED (their whole forward is this half). */
+int dfwfm_forward_gather(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
+                         int64_t batch, float* deep_emb, int64_t deep_emb_stride, float* first_second, void* stream);
+
 /* Pruned deep tower (BASELINE configs[3]; reference masks model/DeepFMs.py:647-673, whose forward stays
  * dense): compacts every hidden layer's nonzero weights (the tensors of the last
  * dfwfm_model_set_dense) into a per-neuron (k, w) list on the device and, when the nonzero fraction
@@ -160,6 +169,19 @@ int dfwfm_model_build_sparse_mlp(dfwfm_model* m, double max_density, int32_t* en
  * update, not per forward; dfwfm_model_set_dense turns the path off until the next call; max_pairs <= 0 turns
  * it off.  Logits agree with the dense forward to fp32 summation order (1e-5 bar). */
 int dfwfm_model_build_fwfm_pairs(dfwfm_model* m, int32_t max_pairs, int32_t* enabled, void* stream);
+
+/* Serving copy of the categorical tables for the forward without a deep tower (fwd_kernel PART 3): every row of
+ * every categorical field's second-order table (emb2) with its first-order weight (emb1) appended, padded to a
+ * 64-byte row (D + 1 <= 16 floats; else D + 1 rounded up to 4), so the gather reads ONE aligned row per (sample,
+ * field) instead of a 40-B row plus a 4-B first-order word from another table (the separate 4-B reads cost the
+ * gather alone +0.5 us per 4096 samples with Infinity-Cache-resident tables and +0.8-1.3 us HBM-resident,
+ * tools/ubench_gather.hip).  The values are copied, so the logits are bit-identical with and without it.
+ * enable = 1 (re)builds the copy from the tables of the last dfwfm_model_set_tables (stream-ordered, no sync) and
+ * the inference forward reads it from then on; enable = 0 drops it.  It is a snapshot: rebuild it after any
+ * in-place update of the tables (the Python engine does, from torch's version counters), and
+ * dfwfm_model_set_tables drops it.  *enabled = 1 when the copy is in use (models with a deep tower, QR fields,
+ * no first-order tables or no second order keep the plain tables: 0). */
+int dfwfm_model_pack_tables(dfwfm_model* m, int32_t enable, int32_t* enabled, void* stream);
 
 /* ---- training step (reference model/DeepFMs.py:553-637) ---------------------------------- */
 

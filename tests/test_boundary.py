@@ -29,8 +29,8 @@ def test_header_declares_expected_api():
         "dfwfm_abi_version", "dfwfm_adam_step", "dfwfm_adam_step_dev", "dfwfm_backward", "dfwfm_backward_phases",
         "dfwfm_bce_grad", "dfwfm_backward_phases_bce", "dfwfm_model_set_dense_zero",
         "dfwfm_diag_stamps", "dfwfm_eval_metrics", "dfwfm_forward", "dfwfm_forward_batches",
-        "dfwfm_forward_workspace_bytes",
-        "dfwfm_forward_ws", "dfwfm_last_error", "dfwfm_model_build_fwfm_pairs", "dfwfm_model_build_sparse_mlp", "dfwfm_model_create", "dfwfm_model_destroy",
+        "dfwfm_forward_workspace_bytes", "dfwfm_forward_gather",
+        "dfwfm_forward_ws", "dfwfm_last_error", "dfwfm_model_build_fwfm_pairs", "dfwfm_model_build_sparse_mlp", "dfwfm_model_create", "dfwfm_model_destroy", "dfwfm_model_pack_tables",
         "dfwfm_metrics_workspace_bytes", "dfwfm_model_set_dense", "dfwfm_model_set_tables", "dfwfm_prune_apply", "dfwfm_prune_threshold",
         "dfwfm_prune_workspace_bytes", "dfwfm_read_error_flag", "dfwfm_set_deterministic", "dfwfm_set_step_source", "dfwfm_sparse_grads_apply", "dfwfm_sparse_grads_local", "dfwfm_sparse_grads_size",
         "dfwfm_train_forward", "dfwfm_workspace_generation"])

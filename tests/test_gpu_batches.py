@@ -34,7 +34,7 @@ def _check(cfg, params, m, gpu, host, scaled=False):
     """Every batch of the set bit-identical to its own forward; the first and the last batch -- every row (the
     float64 oracle takes ~0.3 s per 4096 rows) -- against the oracle at the north-star bar (scaled: the bar widened
     by the row's absolute term sum, conftest.logit_close_scaled, for first-order sums without lw that cancel)."""
-    eng = m._sync_engine(gpu)
+    eng = m._sync_inference(gpu)  # MLP-free models: the tables' serving copy (dfwfm_model_pack_tables)
     dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
     B = host[0][0].shape[0]
     with torch.no_grad():
@@ -63,9 +63,9 @@ def test_batch_set_deep_bit_identical(gpu, qr, nb, B):
 
 @pytest.mark.parametrize("nb,B", [(3, 4096), (6, 1000), (35, 256), (3, 4096 + 17), (2, 5), (20, 4096)])
 def test_batch_set_fwfm_only_bit_identical(gpu, nb, B):
-    """The MLP-free forward (BASELINE configs[0]'s model at Criteo-39 sizes) as a batch set: the persistent LDS-DMA
-    forward (dfwfm_fwfm_dma.hip; more tiles than workgroups, ragged tails, fewer tiles than workgroups, two launches)
-    bit-identical to each batch's own forward (fwd_kernel), every row of the first and last batch vs the oracle."""
+    """The MLP-free forward (BASELINE configs[0]'s model at Criteo-39 sizes) as a batch set (ragged tails, tiny
+    batches, two launches): bit-identical to each batch's own forward, every row of the first and last batch vs the
+    oracle."""
     cfg, params, m = _criteo_model(gpu, 0, 0, seed=91)
     _check(cfg, params, m, gpu, _inputs(cfg["feature_sizes"], nb, B, seed=7 * nb + B))
 
@@ -231,29 +231,19 @@ def _fwfm_only_case(F, num, D, lw, fm, seed):
 @pytest.mark.parametrize("F,num,D,lw,fm", [(39, 13, 10, 1, 0), (39, 13, 16, 1, 0), (48, 16, 8, 0, 0),
                                            (20, 5, 4, 1, 1), (30, 0, 10, 1, 0), (9, 1, 10, 0, 0),
                                            (33, 13, 10, 1, 0), (42, 2, 4, 1, 0), (16, 3, 16, 0, 1)])
-def test_fwfm_only_set_dma_shapes_bit_identical(gpu, monkeypatch, F, num, D, lw, fm):
-    """The LDS-DMA batch-set forward over model shapes: bit-identical to each batch alone and to the same set through
-    fwd_kernel's MLP-free form (DFWFM_P3_DMA=0), and within the north-star bar of the float64 oracle."""
+def test_fwfm_only_set_shapes_bit_identical(gpu, F, num, D, lw, fm):
+    """The MLP-free batch-set forward over model shapes: bit-identical to each batch alone, and within the
+    north-star bar of the float64 oracle (scaled for first-order sums without lw)."""
     cfg, params, m = _fwfm_only_case(F, num, D, lw, fm, seed=F * 100 + D)
     m = m.to(gpu).eval()
     from xsdeepfwfm_deprecated_amd import synth
     host = [synth.synth_inputs(cfg["feature_sizes"], num, 1000 + F, seed=F + D + i) for i in range(5)]
     _check(cfg, params, m, gpu, host, scaled=not lw)
-    dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
-    res = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("DFWFM_P3_DMA", v)
-        eng = m._sync_engine(gpu)
-        outs = [torch.empty(1000 + F, device=gpu) for _ in dev]
-        with torch.no_grad():
-            eng.forward_batches(dev, outs)
-        res[v] = torch.stack(outs).cpu().numpy()
-    assert np.array_equal(res["0"], res["1"])
 
 
 def test_fwfm_only_set_strided_inputs_and_out_of_range(gpu):
-    """The LDS-DMA forward reads Xi / Xv through any row stride and clamps an out-of-range index to row 0 with the
-    sticky flag (nn.Embedding's IndexError, raised by DeepFMs.forward), like fwd_kernel."""
+    """The MLP-free batch-set forward reads Xi / Xv through any row stride and clamps an out-of-range index to row 0
+    with the sticky flag (nn.Embedding's IndexError, raised by DeepFMs.forward)."""
     cfg, params, m = _criteo_model(gpu, 0, 0, seed=13)
     sizes = cfg["feature_sizes"]
     host = _inputs(sizes, 4, 700, seed=9)
@@ -282,3 +272,54 @@ def test_fwfm_only_set_strided_inputs_and_out_of_range(gpu):
         ref = [eng.forward(c[:, :26], wv[:, :13]) for c, (_, wv) in zip(clamped, wide)]
     for o, a in zip(outs, ref):
         assert torch.equal(o, a)
+
+
+def test_packed_tables_bit_identical_and_refreshed(gpu):
+    """The serving copy of the categorical tables (second-order row + first-order weight in one 64-B row) gives
+    the same bits as the plain tables, lone batch and batch set; an in-place table update re-packs it (the next
+    forward matches the oracle on the new weights); set_tables (new table tensors) drops it."""
+    cfg, params, m = _criteo_model(gpu, 0, 0, seed=17)
+    host = _inputs(cfg["feature_sizes"], 3, 1500, seed=4)
+    dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
+    outs = {}
+    for packed in (False, True):
+        m.pack_tables = packed
+        eng = m._sync_inference(gpu)
+        assert eng._packed_on == packed
+        with torch.no_grad():
+            sets = eng.forward_batches(dev, [torch.empty(1500, device=gpu) for _ in dev])
+            lone = [m(xi, xv) for xi, xv in dev]
+        outs[packed] = (torch.stack(sets).cpu().numpy(), torch.stack(lone).cpu().numpy())
+    assert np.array_equal(outs[False][0], outs[True][0]) and np.array_equal(outs[False][1], outs[True][1])
+    assert np.array_equal(outs[True][0], outs[True][1])
+    # an in-place update (torch bumps the tables' version counters) -> the next forward re-packs
+    with torch.no_grad():
+        m.fm_2nd_embeddings[20].weight.mul_(-0.5)
+        m.fm_1st_embeddings[30].weight.add_(0.25)
+        got = m(*dev[0]).cpu().numpy()
+    new = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    assert logit_close(got, dfwfm_oracle.forward(cfg, new, *host[0])) < 1e-5
+    assert m._engine._packed_on
+
+
+def test_packed_tables_after_fused_training_steps(gpu):
+    """The fused training step updates the tables inside captured graphs (no version bump): it drops the serving
+    copy's key, so the next inference forward re-packs and equals the plain-table forward bit for bit."""
+    from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
+    cfg, params, m = _criteo_model(gpu, 0, 0, seed=29)
+    host = _inputs(cfg["feature_sizes"], 3, 1024, seed=8)
+    dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
+    with torch.no_grad():
+        before = m(*dev[0]).clone()  # packs
+    m.train()
+    t = FusedTrainStep(m, 1024, lr=1e-2, weight_decay=0.0)
+    for xi, xv in dev[1:]:
+        t.step(xi, xv, (torch.arange(1024, device=gpu) % 3 == 0).float())
+    t.close()
+    m.eval()
+    with torch.no_grad():
+        packed = m(*dev[0]).cpu().numpy()
+        m.pack_tables = False
+        plain = m(*dev[0]).cpu().numpy()
+    assert not np.array_equal(packed, before.cpu().numpy())
+    assert np.array_equal(packed, plain)

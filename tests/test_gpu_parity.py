@@ -442,3 +442,28 @@ def test_fwd32_matches_reference_goldens(gpu, monkeypatch, name):
     m = make_model(cfg, params, gpu)
     got = run(m, xi, xv, gpu)
     assert logit_close(got, l32) < 1e-5 and logit_close(got, l64) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_qr_mult", "deepfwfm_fwlw_lw"])
+def test_forward_gather_matches_oracle_and_fused(gpu, name):
+    """dfwfm_forward_gather (the gather / shallow half alone, bench.py's roofline_gather): deep_emb equals the
+    oracle's embeddings (exact products of the tables' fp32 values), first + second within the north-star bar,
+    and deep_emb zero padded past F * D; a model without a deep tower is refused."""
+    from xsdeepfwfm_deprecated_amd._lib import DfwfmError
+    cfg, params, xi, xv, *_ = load_golden(name)
+    m = make_model(cfg, params, gpu)
+    B = min(len(xi), 300)
+    eng = m._sync_engine(gpu)
+    with torch.no_grad():
+        E, fs = eng.forward_gather(torch.from_numpy(xi[:B]).to(gpu), torch.from_numpy(xv[:B]).to(gpu))
+    E, fs = E.cpu().numpy(), fs.cpu().numpy()
+    _, parts = dfwfm_oracle.forward(cfg, params, xi[:B], xv[:B], return_parts=True)
+    F_, D_ = cfg["field_size"], cfg["embedding_size"]
+    ref_e = parts["E"].reshape(B, F_ * D_)
+    assert np.abs(E[:, :F_ * D_] - ref_e).max() <= 1e-6 * max(1.0, np.abs(ref_e).max())
+    assert not E[:, F_ * D_:].any()
+    assert logit_close(fs, parts["first"] + parts["second"]) < 1e-5
+    fwfm_cfg = dict(cfg, use_deep=0)
+    mf = make_model(fwfm_cfg, {k: v for k, v in params.items() if not k.startswith("net_1")}, gpu)
+    with pytest.raises(DfwfmError, match="deep tower"):
+        mf._sync_engine(gpu).forward_gather(torch.from_numpy(xi[:B]).to(gpu), torch.from_numpy(xv[:B]).to(gpu))

@@ -9,6 +9,11 @@
 //   3  one lane per row, two 16-B aligned dwordx4 + one dwordx2 placed by the row's alignment (3 loads per row)
 //   4  one lane per row of a PACKED copy: rows at a 16-float (64-B) stride, 64-B aligned -- every row one line,
 //      two dwordx4 + one dwordx2
+//   5  variant 0 plus the row's first-order weight from its own [n][1] table (one dword per row: the MLP-free
+//      forward's real pattern with lw first order, fm_1st_embeddings)
+//   6  one lane per row of a packed copy holding second AND first order: 12-float (48-B) rows, 16-B aligned,
+//      three dwordx4 (the first-order weight at float 10)
+//   7  the same at a 16-float (64-B) stride: every row one line
 // argv: [NB batches in flight] [table scale K: every table K x as many rows, e.g. 8 -> 424 MB, HBM-resident]
 // TILES: 16-sample tiles per workgroup (walked with the next tile's loads issued before this tile's
 // LDS stores: TILES > 1 is the persistent form).  Reports microseconds per 4096-sample batch with
@@ -27,6 +32,9 @@ constexpr int F = 26, D = 10, BM = 16, NTH = 512;
 struct Args {
   const float* const* tabs;  // [F] table bases
   const float* const* ptabs; // [F] packed (16-float stride) table bases
+  const float* const* ftabs; // [F] first-order tables [n][1]
+  const float* const* q12;   // [F] packed second + first order, 12-float stride
+  const float* const* q16;   // [F] packed second + first order, 16-float stride
   const int64_t* xi;         // [NB*B][F]
   float* out;                // [NB*B]
   int64_t total;             // samples
@@ -70,6 +78,27 @@ __device__ __forceinline__ void tile_loads(const Args& a, int64_t b0, int tid, f
       v1[4] = x1.x; v1[5] = x1.y; v1[6] = x1.z; v1[7] = x1.w;
       v1[8] = c.x; v1[9] = c.y;
     }
+  } else if constexpr (V == 5) {
+    const int r = tid;
+    if (r < F * BM) {
+      const int f = r >> 4;
+      const int64_t idx = a.xi[(b0 + (r & 15)) * F + f];
+      const float2* src = reinterpret_cast<const float2*>(a.tabs[f] + idx * D);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) v2[j] = src[j];
+      v1[10] = a.ftabs[f][idx];
+    }
+  } else if constexpr (V == 6 || V == 7) {
+    const int r = tid;
+    if (r < F * BM) {
+      const int f = r >> 4;
+      const int64_t idx = a.xi[(b0 + (r & 15)) * F + f];
+      const float4* src = reinterpret_cast<const float4*>((V == 6 ? a.q12[f] + idx * 12 : a.q16[f] + idx * 16));
+      const float4 x0 = src[0], x1 = src[1], x2 = src[2];
+      v1[0] = x0.x; v1[1] = x0.y; v1[2] = x0.z; v1[3] = x0.w;
+      v1[4] = x1.x; v1[5] = x1.y; v1[6] = x1.z; v1[7] = x1.w;
+      v1[8] = x2.x; v1[9] = x2.y; v1[10] = x2.z;
+    }
   } else if constexpr (V == 1) {
     const int w = tid >> 6, lane = tid & 63;
     const int rw = lane / 5, part = lane - rw * 5;  // 12 rows per wave per round
@@ -99,19 +128,21 @@ __device__ __forceinline__ void tile_loads(const Args& a, int64_t b0, int tid, f
 
 template <int V>
 __device__ __forceinline__ void tile_stores(float* E, int tid, const float2 (&v2)[8], const float (&v1)[16]) {
-  if constexpr (V == 0) {
+  if constexpr (V == 0 || V == 5) {
     const int r = tid;
     if (r < F * BM) {
       float2* dst = reinterpret_cast<float2*>(E + (r & 15) * (F * D + 2) + (r >> 4) * D);
 #pragma unroll
       for (int j = 0; j < 5; ++j) dst[j] = v2[j];
+      if constexpr (V == 5) E[BM * (F * D + 2) + r] = v1[10];
     }
-  } else if constexpr (V == 3 || V == 4) {
+  } else if constexpr (V == 3 || V == 4 || V == 6 || V == 7) {
     const int r = tid;
     if (r < F * BM) {
       float2* dst = reinterpret_cast<float2*>(E + (r & 15) * (F * D + 2) + (r >> 4) * D);
 #pragma unroll
       for (int j = 0; j < 5; ++j) dst[j] = make_float2(v1[2 * j], v1[2 * j + 1]);
+      if constexpr (V >= 6) E[BM * (F * D + 2) + r] = v1[10];
     }
   } else if constexpr (V == 1) {
     const int w = tid >> 6, lane = tid & 63;
@@ -134,7 +165,7 @@ __device__ __forceinline__ void tile_stores(float* E, int tid, const float2 (&v2
 
 template <int V, int TILES>
 __global__ void __launch_bounds__(NTH) gather_kernel(Args a) {
-  __shared__ float E[BM * (F * D + 2)];
+  __shared__ float E[BM * (F * D + 2) + F * BM];  // rows, then first order [F][BM]
   const int tid = threadIdx.x;
   float2 v2[8];
   float v1[16];
@@ -149,6 +180,7 @@ __global__ void __launch_bounds__(NTH) gather_kernel(Args a) {
       const int b = tid >> 4, q = tid & 15;
       float s = 0.f;
       for (int c = q; c < F * D; c += 16) s += E[b * (F * D + 2) + c];
+      if (V >= 5) for (int f = q; f < F; f += 16) s += E[BM * (F * D + 2) + f * BM + b];
 #pragma unroll
       for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o);
       if (q == 0) a.out[b0 + b] = s;
@@ -187,6 +219,22 @@ int main(int argc, char** argv) {
   const float** dptabs;
   CHECK(hipMalloc(&dptabs, F * sizeof(float*)));
   CHECK(hipMemcpy(dptabs, hp.data(), F * sizeof(float*), hipMemcpyHostToDevice));
+  // first-order tables and the packed second + first order copies
+  auto table_set = [&](int stride) {
+    float* t;
+    CHECK(hipMalloc(&t, rows * stride * 4));
+    CHECK(hipMemset(t, 0, rows * stride * 4));
+    std::vector<const float*> h(F);
+    int64_t o = 0;
+    for (int f = 0; f < F; ++f) { h[f] = t + o * stride; o += n[f]; }
+    const float** d;
+    CHECK(hipMalloc(&d, F * sizeof(float*)));
+    CHECK(hipMemcpy(d, h.data(), F * sizeof(float*), hipMemcpyHostToDevice));
+    return d;
+  };
+  const float** dftabs = table_set(1);
+  const float** dq12 = table_set(12);
+  const float** dq16 = table_set(16);
   printf("tables x%d: %.0f MB of 40-B rows, %.0f MB packed\n", K, rows * D * 4 / 1e6, rows * 64 / 1e6);
   const int64_t total = (int64_t)NB * B;
   std::vector<int64_t> hx(total * F);
@@ -198,7 +246,7 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&dx, hx.size() * 8));
   CHECK(hipMemcpy(dx, hx.data(), hx.size() * 8, hipMemcpyHostToDevice));
   CHECK(hipMalloc(&dout, total * 4));
-  Args a{dtabs, dptabs, dx, dout, total};
+  Args a{dtabs, dptabs, dftabs, dq12, dq16, dx, dout, total};
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -217,6 +265,10 @@ int main(int argc, char** argv) {
            tiles, grid, us_batch, alg / (us_batch * 1e-6) / 1e12);
   };
   run(gather_kernel<0, 1>, 1, "lane per row (5 x dwordx2)");
+  run(gather_kernel<5, 1>, 1, "+ first order, own tables");
+  run(gather_kernel<6, 1>, 1, "2nd+1st packed 48-B (3 x4)");
+  run(gather_kernel<7, 1>, 1, "2nd+1st packed 64-B (3 x4)");
+  if (argc > 3) return 0;
   run(gather_kernel<4, 1>, 1, "packed 64-B rows (2 x4 + x2)");
   run(gather_kernel<3, 1>, 1, "lane per row (2 x4 + 1 x2)");
   run(gather_kernel<1, 1>, 1, "5 lanes per row (dwordx2)");

@@ -104,6 +104,10 @@ class DeepFMs(nn.Module):
         # (reference :661-666) leaves at most this many (of F (F - 1) / 2); 0 (default) keeps the dense Gram
         # on MFMA, which is as fast at the reference's 73 of 741 pairs
         self.fwfm_pair_max = 0
+        # the forward without a deep tower gathers from a serving copy of the categorical tables (second-order row
+        # and first-order weight in one aligned row, dfwfm_model_pack_tables), rebuilt after weight updates; the
+        # values are copied, so the logits are the same bits either way
+        self.pack_tables = True
         # the device backward's gradient sums in a fixed order (dfwfm_set_deterministic; like
         # torch.use_deterministic_algorithms): two runs of a training step give the same bits, at ~+16 us per step
         # at Criteo-39 (sorted table scatter, split-K slices); off by default (float atomics)
@@ -248,6 +252,20 @@ class DeepFMs(nn.Module):
                        self.bias.detach(), lin_w, lin_b, w("net_1_fc") if self.use_deep else None)
         return eng
 
+    def _sync_inference(self, device):
+        """_sync_engine plus the inference-only derived state: the serving copy of the categorical tables for the
+        forward without a deep tower (re-packed when a table changed; the training forward reads the tables)."""
+        eng = self._sync_engine(device)
+        if device.type == "cuda" and not self.use_deep:
+            first = getattr(self, "fm_1st_embeddings", None)
+            second = getattr(self, "fm_2nd_embeddings", None)
+            tabs = []
+            for f in range(self.num, self.field_size):
+                d = self._field_desc(None if second is None else second[f], None if first is None else first[f])
+                tabs.append((d["emb2"], d["emb1"]))
+            eng.sync_packed(tabs, self.pack_tables)
+        return eng
+
     def _sync_cpu_engine(self):
         """The host kernels' engine (libdfwfm_cpu.so), re-described on every call (pointers, no copies)."""
         if not isinstance(self._engine, CpuEngine):
@@ -330,8 +348,10 @@ class DeepFMs(nn.Module):
             # magnitude-pruned hidden layers (fit(prune=1), reference :647-673) run as a sparse MLP when
             # at most sparse_mlp_max_density of their weights are nonzero (checked once per weight update)
             eng.sync_sparse(self.sparse_mlp_max_density)
-        elif self.use_fwfm:
-            eng.sync_pairs(self.fwfm_pair_max)
+        else:
+            self._sync_inference(device)
+            if self.use_fwfm:
+                eng.sync_pairs(self.fwfm_pair_max)
         params = [q for q in self.parameters() if q.requires_grad]
         out, _ = torch.ops.dfwfm.forward(torch_ops.register(self), xi, xv, params, False, 0.0, 0)
         if self.strict_index_check and not self._defer_index_check:
@@ -423,7 +443,7 @@ class DeepFMs(nn.Module):
             if dev.type == "cuda" and self.eval_batch_sets and x_size >= 2 * bs:
                 # the full batches as batch sets (dfwfm_forward_batches: up to 32 resident batches per launch, the
                 # same logits as one forward each); the sparse-MLP / pair-list variants keep one forward per batch
-                eng = self._sync_engine(dev)
+                eng = self._sync_inference(dev)
                 alt = eng.sync_sparse(self.sparse_mlp_max_density) if self.use_deep else (
                     eng.sync_pairs(self.fwfm_pair_max) if self.use_fwfm else False)
                 if not alt:

@@ -23,7 +23,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdfwfm.so")
 # A/B of build variants only (e.g. libdfwfm_ns4.so built with DFWFM_HIPCC_FLAGS=-DDFWFM_NSETS=4)
 LOAD_PATH = os.path.join(PKG_DIR, os.environ["DFWFM_LIB"]) if os.environ.get("DFWFM_LIB") else LIB_PATH
-SOURCES = ["dfwfm_kernels.hip", "dfwfm_fwd32.hip", "dfwfm_fwfm_dma.hip", "dfwfm_ftrain.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_sparse.hip",
+SOURCES = ["dfwfm_kernels.hip", "dfwfm_fwd32.hip", "dfwfm_ftrain.hip", "dfwfm_train.hip", "dfwfm_prune.hip", "dfwfm_metrics.hip", "dfwfm_sparse.hip",
            "dfwfm_spmlp.hip", "dfwfm_capi.hip"]
 # the forward / backward kernel templates are instantiated once per embedding size, each size in its own
 # translation unit (-DDFWFM_KD=<D>) so they compile in parallel; the plain object holds everything else
@@ -117,6 +117,9 @@ SIGNATURES = {
                                         ctypes.c_size_t, _P]),
     "dfwfm_model_build_sparse_mlp": (ctypes.c_int, [_P, ctypes.c_double, ctypes.POINTER(ctypes.c_int32), _P]),
     "dfwfm_model_build_fwfm_pairs": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), _P]),
+    "dfwfm_model_pack_tables": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), _P]),
+    "dfwfm_forward_gather": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P,
+                                            ctypes.c_int64, _P, _P]),
     "dfwfm_train_forward": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P,
                                            ctypes.c_float, ctypes.c_uint32, _P]),
     "dfwfm_backward": (ctypes.c_int, [_P, _P, ctypes.POINTER(dfwfm_grads), _P]),

@@ -48,6 +48,10 @@ struct dfwfm_model {
   FieldDev* d_fields;
   float* d_upack;  // FwFM A-operand fragments [MT][S][64]
   int2* d_pairs;   // build_fwfm_pairs: nonzero pairs of a pruned R (F (F - 1) / 2 capacity)
+  float* d_pkrows;       // dfwfm_model_pack_tables: the serving rows of every categorical field
+  size_t pkrows_floats;  // capacity
+  const float** d_pk;    // [64] per-field row bases (device)
+  int pkw;               // row stride in floats while the copy is in use, else 0
   int32_t npairs;
   int32_t* d_err;
   float4* d_wpack;
@@ -135,7 +139,7 @@ void free_model(dfwfm_model* m) {
   if (!m) return;
   void* ptrs[] = {m->d_fields, m->d_upack, m->d_err,     m->d_wpack, m->d_mlp_b,   m->d_fc,  m->d_fwlw,
                   m->d_lw,     m->d_bias,  m->d_stamps,  m->d_wtpack, m->d_rsk,   m->d_ws,
-                  m->d_ell,    m->d_cnt,   m->d_spstat, m->d_pairs};
+                  m->d_ell,    m->d_cnt,   m->d_spstat, m->d_pairs, m->d_pkrows, m->d_pk};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -368,6 +372,7 @@ int dfwfm_model_set_tables(dfwfm_model* m, const dfwfm_field_tables* t, int32_t 
   for (int f = 0; f < n; ++f)
     if (host[f].c > 0) host[f].n = (host[f].n + host[f].c - 1) / host[f].c * host[f].c;
   memcpy(m->h_fields, host, sizeof(FieldDev) * n);
+  m->pkw = 0;  // the serving copy was built from the old tables
   m->flags &= ~kHasQR;
   for (int f = 0; f < n; ++f)
     if (host[f].c > 0) m->flags |= kHasQR;
@@ -492,6 +497,8 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.out = out;
   a.err = m->d_err;
   a.upack = m->d_upack;
+  a.pk = m->pkw ? m->d_pk : nullptr;
+  a.pkw = m->pkw;
   a.pairs = m->d_pairs;
   a.npairs = m->npairs;
   a.fwlw = m->d_fwlw;
@@ -754,14 +761,7 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     }
     int rc = diag_stamps_buffer(m, (int64_t)n * a.tiles * rows, 1, &a.stamps);
     if (rc != DFWFM_OK) return rc;
-    // MLP-free sets: the persistent LDS-DMA forward (DFWFM_P3_DMA=0: fwd_kernel PART 3, A/B)
-    static const char* dma_env = getenv("DFWFM_P3_DMA");
-    bool dma = n > 1 && !m->cfg.use_deep && !(dma_env && atoi(dma_env) == 0) && fwfm_dma_supported(a, m->D);
-    for (int f = m->num; f < m->F && dma; ++f) dma = m->h_fields[f].n < 0x7fffffff;  // 32-bit row indices in LDS
-    if (dma)
-      if (const char* dg = getenv("DFWFM_DIAG_DMA")) a.flags |= atoi(dg) << 25;  // diagnostics only: results invalid
     const hipError_t e = r32 ? launch_fwd32(a, m->D, m->lds_r32, (hipStream_t)stream)
-                       : dma ? launch_fwfm_dma(a, m->D, (hipStream_t)stream)
                              : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->KS, m->NG, m->lds_inf,
                                               (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "batch-set forward launch");
@@ -824,6 +824,76 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
   hipError_t e = launch_forward_split(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->NG, m->lds_gather, m->lds_inf,
                                       (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "forward launch");
+  return DFWFM_OK;
+}
+
+int dfwfm_forward_gather(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
+                         int64_t batch, float* deep_emb, int64_t deep_emb_stride, float* first_second, void* stream) {
+  if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
+  if (!m->cfg.use_deep) return fail(DFWFM_ERR_UNSUPPORTED, "forward_gather: the model has no deep tower");
+  int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, first_second);
+  if (rc != DFWFM_OK || batch == 0) return rc;
+  if (!deep_emb || deep_emb_stride != (int64_t)m->NC0 * 16)
+    return fail(DFWFM_ERR_INVALID_ARG, "deep_emb stride %lld, need %d", (long long)deep_emb_stride, m->NC0 * 16);
+  if (reinterpret_cast<uintptr_t>(deep_emb) % 16) return fail(DFWFM_ERR_INVALID_ARG, "deep_emb not 16-byte aligned");
+  FwdArgs a;
+  fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, nullptr);
+  a.part_stride = m->NC0 * 16;
+  a.part_e = deep_emb;
+  a.part_fs = first_second;
+  a.tail = m->tailI;
+  hipError_t e = launch_forward_gather(a, m->D, m->lds_gather, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "gather launch");
+  return DFWFM_OK;
+}
+
+int dfwfm_model_pack_tables(dfwfm_model* m, int32_t enable, int32_t* enabled, void* stream) {
+  if (!m || !enabled) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
+  *enabled = 0;
+  m->pkw = 0;
+  if (!enable) return DFWFM_OK;
+  if (!m->tables_set) return fail(DFWFM_ERR_STATE, "set_tables must precede pack_tables");
+  const int need = kHasSecond | kNeedE | kFoTables;
+  if (m->cfg.use_deep || (m->flags & need) != need || (m->flags & kHasQR) || m->F - m->num < 1) return DFWFM_OK;
+  const int D = m->D;
+  const int pkw = D + 1 <= 16 ? 16 : (D + 4) & ~3;
+  PackTabList L;
+  memset(&L, 0, sizeof L);
+  L.D = D;
+  L.pkw = pkw;
+  size_t rows = 0;
+  for (int f = m->num; f < m->F; ++f) rows += (size_t)m->h_fields[f].n;
+  if (rows * pkw > m->pkrows_floats) {
+    if (m->d_pkrows) (void)hipFree(m->d_pkrows);
+    m->d_pkrows = nullptr;
+    m->pkrows_floats = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_pkrows), rows * pkw * sizeof(float)));
+    m->pkrows_floats = rows * pkw;
+  }
+  if (!m->d_pk) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_pk), 64 * sizeof(float*)));
+  const float* bases[64] = {};
+  size_t off = 0;
+  for (int f = m->num; f < m->F; ++f) {
+    const int j = f - m->num;
+    const int64_t n = m->h_fields[f].n;
+    bases[f] = m->d_pkrows + off;
+    L.emb2[j] = m->h_fields[f].emb2;
+    L.emb1[j] = m->h_fields[f].emb1;
+    L.dst[j] = m->d_pkrows + off;
+    L.n[j] = n;
+    const int64_t nb = (n + 255) / 256;
+    if ((int64_t)L.blk0[j] + nb > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "tables too large to pack");
+    L.blk0[j + 1] = L.blk0[j] + (int32_t)nb;
+    off += (size_t)n * pkw;
+  }
+  L.nf = m->F - m->num;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(m->d_pk, bases, sizeof bases, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));  // `bases` is a stack buffer (once per weight update)
+  hipError_t e = launch_pack_tables(L, s);
+  if (e != hipSuccess) return hip_fail(e, "pack tables launch");
+  m->pkw = pkw;
+  *enabled = 1;
   return DFWFM_OK;
 }
 

@@ -102,6 +102,19 @@ __device__ __forceinline__ void store_row(float* dst, const float (&v)[D]) {
   }
 }
 
+// one row of the tables' serving copy (dfwfm_model_pack_tables): D floats of second order, then the first-order
+// weight, from a 16-byte aligned row: ceil((D + 1) / 4) dwordx4 loads
+template <int D>
+__device__ __forceinline__ void load_row_fo(float (&v)[D], float& fo, const float* __restrict__ src) {
+  constexpr int NQ = (D + 4) / 4;
+  f32x4 x[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) x[q] = reinterpret_cast<const f32x4*>(src)[q];
+#pragma unroll
+  for (int d = 0; d < D; ++d) v[d] = x[d / 4][d % 4];
+  fo = x[D / 4][D % 4];
+}
+
 // row combine modes: 0 = a * scale (numerical / plain, scale 1), 1 = a * b (QR mult), 2 = a + b (QR add)
 __device__ __forceinline__ float combine(int mode, float a, float b, float scale) {
   return mode == 1 ? a * b : (mode == 2 ? a + b : a * scale);

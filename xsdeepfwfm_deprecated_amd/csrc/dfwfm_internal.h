@@ -66,6 +66,8 @@ struct FwdArgs {
   int64_t batch;
   float* out;
   int32_t* err;
+  const float* const* pk;  // dfwfm_model_pack_tables: per field, rows of pkw floats (emb2 row, emb1 weight, zero
+  int32_t pkw;             // pad) for the categorical fields; pkw = 0: the plain tables (PART 3 reads it)
   const float* upack;  // FwFM A-operand fragments [MT][S][64]: strictly-upper (R + R^T)/2
   const int2* pairs;   // kPairs: the nonzero strictly-upper entries of (R + R^T)/2, (k | l << 16, w bits), k-major
   int32_t npairs;
@@ -446,10 +448,18 @@ hipError_t launch_metrics(const float* z, const float* y, int64_t n, double* out
 
 bool supported_embedding_size(int D);
 hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size_t lds, hipStream_t s);
-// the MLP-free batch-set forward as one persistent launch with LDS-DMA row gathers (dfwfm_fwfm_dma.hip): models with
-// FwFM / FM second order, first-order tables, no QR / pair list / fwlw, ceil(F / 16) <= 3, D in {4, 8, 10, 16}
-bool fwfm_dma_supported(const FwdArgs& a, int D);
-hipError_t launch_fwfm_dma(const FwdArgs& a, int D, hipStream_t s);
+
+// dfwfm_model_pack_tables: the categorical fields' (emb2 row | emb1 weight | zero pad) serving rows, one launch
+constexpr int kPackTabList = 64;
+struct PackTabList {
+  const float* emb2[kPackTabList];
+  const float* emb1[kPackTabList];
+  float* dst[kPackTabList];
+  int64_t n[kPackTabList];
+  int32_t blk0[kPackTabList + 1];  // first workgroup of each field (256 rows per workgroup)
+  int32_t nf, D, pkw;
+};
+hipError_t launch_pack_tables(const PackTabList& L, hipStream_t s);
 hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
 // the split forward's first launch alone (gather + shallow part -> a.part_e / a.part_fs)
 hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream_t s);

@@ -193,14 +193,19 @@ fwd_kernel(FwdArgs p) {
   const float* rd_emb2[kDirectDesc ? RPT : 1];
   const float* rd_emb1[kDirectDesc ? RPT : 1];
   int64_t rd_n[kDirectDesc ? RPT : 1];
+  // PART 3 with the serving copy (dfwfm_model_pack_tables): a categorical row and its first-order weight are ONE
+  // row of pkw floats
+  constexpr bool kPackable = PART == 3 && !QR && kDirectDesc;
+  bool pkrow[kPackable ? RPT : 1];
   if constexpr (kDirectDesc) {
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int f = (tid + k * NTH) >> 4;
       rd_emb2[k] = rd_emb1[k] = nullptr;
       rd_n[k] = 0;
+      if constexpr (kPackable) pkrow[k] = p.pkw != 0 && f >= num && f < F;
       if (f < F) {
-        rd_emb2[k] = p.fields[f].emb2;
+        rd_emb2[k] = (kPackable && pkrow[kPackable ? k : 0]) ? p.pk[f] : p.fields[f].emb2;
         rd_emb1[k] = p.fields[f].emb1;
         rd_n[k] = p.fields[f].n;
       }
@@ -311,8 +316,12 @@ fwd_kernel(FwdArgs p) {
             atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
             idx = 0;
           }
-          pa[k] = rd_emb2[kDirectDesc ? k : 0] + idx * D;
-          if (fo_tab) qa[k] = rd_emb1[kDirectDesc ? k : 0] + idx;
+          if (kPackable && pkrow[kPackable ? k : 0]) {
+            pa[k] = rd_emb2[kDirectDesc ? k : 0] + idx * p.pkw;
+          } else {
+            pa[k] = rd_emb2[kDirectDesc ? k : 0] + idx * D;
+            if (fo_tab) qa[k] = rd_emb1[kDirectDesc ? k : 0] + idx;
+          }
         }
       } else if (live[k]) {
         const FieldDev fd = desc[f];
@@ -355,15 +364,19 @@ fwd_kernel(FwdArgs p) {
 #pragma unroll
         for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
       }
-      if (live[k] && needE) {
-        load_row<D>(va[k], pa[k]);
-        if constexpr (QR)
-          if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
-      }
-      if (live[k] && fo_tab) {
-        fa[k] = *qa[k];
-        if constexpr (QR)
-          if (mode[k] != 0) fb[k] = *qb[k];
+      if (kPackable && live[k] && pkrow[kPackable ? k : 0]) {  // second and first order in one aligned row
+        load_row_fo<D>(va[k], fa[k], pa[k]);
+      } else {
+        if (live[k] && needE) {
+          load_row<D>(va[k], pa[k]);
+          if constexpr (QR)
+            if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
+        }
+        if (live[k] && fo_tab) {
+          fa[k] = *qa[k];
+          if constexpr (QR)
+            if (mode[k] != 0) fb[k] = *qb[k];
+        }
       }
     }
     // layer-0 weights: the first two chunks go out behind the row loads (vmcnt retires in issue order, so
@@ -1130,6 +1143,33 @@ hipError_t launch_forward(const FwdArgs& a, int D, int tpw, int ks, int ng, size
     case 32: return launch_forward_d32(a, tpw, ks, ng, lds, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// dfwfm_model_pack_tables: thread = one row of one categorical field, written as pkw / 4 float4:
+// [emb2 row (D floats) | emb1 weight | zeros]
+__global__ void __launch_bounds__(256) pack_tables_kernel(const PackTabList L) {
+  int j = 0;
+  while (j + 1 < L.nf && (int)blockIdx.x >= L.blk0[j + 1]) ++j;  // this workgroup's field (wave-uniform)
+  const int64_t r = (int64_t)((int)blockIdx.x - L.blk0[j]) * 256 + threadIdx.x;
+  if (r >= L.n[j]) return;
+  const float* e2 = L.emb2[j] + r * L.D;
+  const float e1 = L.emb1[j][r];
+  f32x4* dst = reinterpret_cast<f32x4*>(L.dst[j] + r * L.pkw);
+  for (int q = 0; q < L.pkw / 4; ++q) {
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = 4 * q + i;
+      v[i] = e < L.D ? e2[e] : (e == L.D ? e1 : 0.f);
+    }
+    dst[q] = v;
+  }
+}
+
+hipError_t launch_pack_tables(const PackTabList& L, hipStream_t s) {
+  if (L.nf <= 0 || L.blk0[L.nf] <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_tables_kernel, dim3(L.blk0[L.nf]), dim3(256), 0, s, L);
+  return hipGetLastError();
 }
 
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s) {

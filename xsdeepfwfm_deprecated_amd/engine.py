@@ -97,6 +97,7 @@ class ForwardEngine:
                 int(f["n"]), int(f["c"]), int(f["op"]), 0)
         _lib.check(_lib.lib().dfwfm_model_set_tables(self.handle, arr, len(fields),
                                                      _stream_handle(self.device)), "dfwfm_model_set_tables")
+        self._packed_key = None  # set_tables drops the serving copy
         self._keep = arr
         self._tables_key = key
 
@@ -125,6 +126,21 @@ class ForwardEngine:
         sync_pairs / sync_sparse must rebuild them rather than report the cached state."""
         self._pairs_key = None
         self._sparse_key = None
+
+    def sync_packed(self, tables, enable: bool = True) -> bool:
+        """dfwfm_model_pack_tables: the serving copy of the categorical tables (second-order row + first-order
+        weight in one aligned row) for the forward without a deep tower, rebuilt whenever a table tensor moved or
+        changed (torch's version counters; the fused training step resets the key, its updates bypass them).
+        tables: the categorical fields' (emb2, emb1) tensors.  Returns whether the copy is in use."""
+        key = (bool(enable),) + tuple((t.data_ptr(), t._version) for pair in tables for t in pair if t is not None)
+        if key == getattr(self, "_packed_key", None):
+            return self._packed_on
+        en = ctypes.c_int32(0)
+        _lib.check(_lib.lib().dfwfm_model_pack_tables(self.handle, int(bool(enable)), ctypes.byref(en),
+                                                      _stream_handle(self.device)), "dfwfm_model_pack_tables")
+        self._packed_on = bool(en.value)
+        self._packed_key = key
+        return self._packed_on
 
     def sync_pairs(self, max_pairs: int) -> bool:
         """(Re)build the pruned FwFM's nonzero pair list after a weight update (syncs the stream once per
@@ -208,6 +224,28 @@ class ForwardEngine:
         rc = _lib.lib().dfwfm_forward_batches(self.handle, nb, pxi, xs, pxv, vs, B, pout, _stream_handle(self.device))
         _lib.check(rc, "dfwfm_forward_batches")
         return outs
+
+    def forward_gather(self, xi: torch.Tensor, xv: torch.Tensor, deep_emb: torch.Tensor | None = None,
+                       first_second: torch.Tensor | None = None):
+        """dfwfm_forward_gather: the gather / shallow half of a deep model's forward alone -- deep_emb
+        [B, ceil(F D / 16) 16] (zero padded) and first + second order [B]."""
+        B = xi.shape[0]
+        ncat = self.cfg["field_size"] - self.cfg["numerical"]
+        num = self.cfg["numerical"]
+        _require_rows(xi, "Xi", torch.int64, self.device, ncat)
+        _require_rows(xv, "Xv", torch.float32, self.device, num)
+        W = -(-self.cfg["field_size"] * self.cfg["embedding_size"] // 16) * 16
+        if deep_emb is None:
+            deep_emb = torch.empty(B, W, dtype=torch.float32, device=self.device)
+        if first_second is None:
+            first_second = torch.empty(B, dtype=torch.float32, device=self.device)
+        rc = _lib.lib().dfwfm_forward_gather(self.handle, ctypes.c_void_p(xi.data_ptr()),
+                                             xi.stride(0) if ncat > 0 else 0, ctypes.c_void_p(xv.data_ptr()),
+                                             xv.stride(0) if num > 0 else 0, B, ctypes.c_void_p(deep_emb.data_ptr()),
+                                             deep_emb.stride(0), ctypes.c_void_p(first_second.data_ptr()),
+                                             _stream_handle(self.device))
+        _lib.check(rc, "dfwfm_forward_gather")
+        return deep_emb, first_second
 
     def _ws_bytes(self, B: int) -> int:
         cache = self.__dict__.setdefault("_ws_cache", {})

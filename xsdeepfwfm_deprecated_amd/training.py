@@ -687,6 +687,7 @@ class FusedTrainStep:
             self._part2()
         self.steps += 1
         self.eng._dense_key = None  # weights changed behind torch's version counters: re-pack on next use
+        self.eng._packed_key = None  # (the tables' serving copy too)
         self.eng.invalidate_derived()  # and the pair list / sparse tower built from the old weights are stale
         return self.loss_sum
 
@@ -730,6 +731,7 @@ class FusedTrainStep:
         hit[0][0].replay()
         self.steps += len(batches)
         self.eng._dense_key = None
+        self.eng._packed_key = None
         self.eng.invalidate_derived()
         return self.loss_sum
 
