@@ -691,11 +691,12 @@ def gather_leg(eng, batches, dev, steps, read_bytes, settle_ms=100.0, streams=4)
         sts = [torch.cuda.Stream(dev) for _ in range(S)]
         for st in sts:
             st.wait_stream(torch.cuda.current_stream(dev))
-        gs = []
+        gs, bufs = [], []  # every stream's graph and the output buffers its graph writes (kept alive here)
         with torch.no_grad():
             for k, st in enumerate(sts):
                 with torch.cuda.stream(st):
                     E = eng.forward_gather(*batches[k % n])
+                    bufs.append(E)
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=st):
                         for i in range(G):
@@ -721,7 +722,10 @@ def gather_leg(eng, batches, dev, steps, read_bytes, settle_ms=100.0, streams=4)
             torch.cuda.synchronize(dev)
         first = min(range(S), key=lambda k: e0[0].elapsed_time(e0[k]))
         last = max(range(S), key=lambda k: e0[0].elapsed_time(e1[k]))
-        return e0[first].elapsed_time(e1[last]) * 1e3 / (reps * G * S), reps * G * S, E[0].shape[1] * 4 + 4
+        us = e0[first].elapsed_time(e1[last]) * 1e3 / (reps * G * S)
+        del gs  # the graphs go before the buffers they write
+        torch.cuda.synchronize(dev)
+        return us, reps * G * S, bufs[0][0].shape[1] * 4 + 4
 
     us1, _, store = timed(1)
     us, nb, store = timed(streams)

@@ -170,7 +170,8 @@ int dfwfm_model_build_sparse_mlp(dfwfm_model* m, double max_density, int32_t* en
  * it off.  Logits agree with the dense forward to fp32 summation order (1e-5 bar). */
 int dfwfm_model_build_fwfm_pairs(dfwfm_model* m, int32_t max_pairs, int32_t* enabled, void* stream);
 
-/* Serving copy of the categorical tables for the forward without a deep tower (fwd_kernel PART 3): every row of
+/* Serving copy of the categorical tables for the inference forward (dfwfm_forward / _batches; not the training
+ * forward, which reads the tables the optimizer updates): every row of
  * every categorical field's second-order table (emb2) with its first-order weight (emb1) appended, padded to a
  * 64-byte row (D + 1 <= 16 floats; else D + 1 rounded up to 4), so the gather reads ONE aligned row per (sample,
  * field) instead of a 40-B row plus a 4-B first-order word from another table (the separate 4-B reads cost the
@@ -179,8 +180,8 @@ int dfwfm_model_build_fwfm_pairs(dfwfm_model* m, int32_t max_pairs, int32_t* ena
  * enable = 1 (re)builds the copy from the tables of the last dfwfm_model_set_tables (stream-ordered, no sync) and
  * the inference forward reads it from then on; enable = 0 drops it.  It is a snapshot: rebuild it after any
  * in-place update of the tables (the Python engine does, from torch's version counters), and
- * dfwfm_model_set_tables drops it.  *enabled = 1 when the copy is in use (models with a deep tower, QR fields,
- * no first-order tables or no second order keep the plain tables: 0). */
+ * dfwfm_model_set_tables drops it.  *enabled = 1 when the copy is in use (models with QR fields, no first-order
+ * tables or no second order keep the plain tables: 0). */
 int dfwfm_model_pack_tables(dfwfm_model* m, int32_t enable, int32_t* enabled, void* stream);
 
 /* ---- training step (reference model/DeepFMs.py:553-637) ---------------------------------- */

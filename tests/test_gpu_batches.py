@@ -274,12 +274,14 @@ def test_fwfm_only_set_strided_inputs_and_out_of_range(gpu):
         assert torch.equal(o, a)
 
 
-def test_packed_tables_bit_identical_and_refreshed(gpu):
+@pytest.mark.parametrize("deep", [0, 1])
+def test_packed_tables_bit_identical_and_refreshed(gpu, deep):
     """The serving copy of the categorical tables (second-order row + first-order weight in one 64-B row) gives
-    the same bits as the plain tables, lone batch and batch set; an in-place table update re-packs it (the next
-    forward matches the oracle on the new weights); set_tables (new table tensors) drops it."""
-    cfg, params, m = _criteo_model(gpu, 0, 0, seed=17)
-    host = _inputs(cfg["feature_sizes"], 3, 1500, seed=4)
+    the same bits as the plain tables, lone batch and batch set (MLP-free kernel; deep: the 32-sample set kernel
+    and the 16-sample lone one); an in-place table update re-packs it (the next forward matches the oracle on the
+    new weights)."""
+    cfg, params, m = _criteo_model(gpu, deep, 0, seed=17)
+    host = _inputs(cfg["feature_sizes"], 3, 4096 + 3, seed=4)
     dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
     outs = {}
     for packed in (False, True):
@@ -287,7 +289,7 @@ def test_packed_tables_bit_identical_and_refreshed(gpu):
         eng = m._sync_inference(gpu)
         assert eng._packed_on == packed
         with torch.no_grad():
-            sets = eng.forward_batches(dev, [torch.empty(1500, device=gpu) for _ in dev])
+            sets = eng.forward_batches(dev, [torch.empty(4096 + 3, device=gpu) for _ in dev])
             lone = [m(xi, xv) for xi, xv in dev]
         outs[packed] = (torch.stack(sets).cpu().numpy(), torch.stack(lone).cpu().numpy())
     assert np.array_equal(outs[False][0], outs[True][0]) and np.array_equal(outs[False][1], outs[True][1])

@@ -104,9 +104,9 @@ class DeepFMs(nn.Module):
         # (reference :661-666) leaves at most this many (of F (F - 1) / 2); 0 (default) keeps the dense Gram
         # on MFMA, which is as fast at the reference's 73 of 741 pairs
         self.fwfm_pair_max = 0
-        # the forward without a deep tower gathers from a serving copy of the categorical tables (second-order row
-        # and first-order weight in one aligned row, dfwfm_model_pack_tables), rebuilt after weight updates; the
-        # values are copied, so the logits are the same bits either way
+        # the inference forward gathers from a serving copy of the categorical tables (second-order row and
+        # first-order weight in one aligned row, dfwfm_model_pack_tables), rebuilt after weight updates; the values
+        # are copied, so the logits are the same bits either way
         self.pack_tables = True
         # the device backward's gradient sums in a fixed order (dfwfm_set_deterministic; like
         # torch.use_deterministic_algorithms): two runs of a training step give the same bits, at ~+16 us per step
@@ -253,10 +253,10 @@ class DeepFMs(nn.Module):
         return eng
 
     def _sync_inference(self, device):
-        """_sync_engine plus the inference-only derived state: the serving copy of the categorical tables for the
-        forward without a deep tower (re-packed when a table changed; the training forward reads the tables)."""
+        """_sync_engine plus the inference-only derived state: the serving copy of the categorical tables
+        (re-packed when a table changed; the training forward reads the tables themselves)."""
         eng = self._sync_engine(device)
-        if device.type == "cuda" and not self.use_deep:
+        if device.type == "cuda":
             first = getattr(self, "fm_1st_embeddings", None)
             second = getattr(self, "fm_2nd_embeddings", None)
             tabs = []
@@ -342,15 +342,13 @@ class DeepFMs(nn.Module):
             from .training import train_forward
             return train_forward(self, eng, xi, xv)
         from . import torch_ops  # torch.ops.dfwfm.forward (the registered custom op)
-        if device.type == "cpu":
-            pass  # the host kernel has no pruned-layout variants
-        elif self.use_deep:
-            # magnitude-pruned hidden layers (fit(prune=1), reference :647-673) run as a sparse MLP when
-            # at most sparse_mlp_max_density of their weights are nonzero (checked once per weight update)
-            eng.sync_sparse(self.sparse_mlp_max_density)
-        else:
-            self._sync_inference(device)
-            if self.use_fwfm:
+        if device.type != "cpu":  # (the host kernel has no serving copy or pruned-layout variants)
+            self._sync_inference(device)  # the tables' serving copy, re-packed after weight updates
+            if self.use_deep:
+                # magnitude-pruned hidden layers (fit(prune=1), reference :647-673) run as a sparse MLP when
+                # at most sparse_mlp_max_density of their weights are nonzero (checked once per weight update)
+                eng.sync_sparse(self.sparse_mlp_max_density)
+            elif self.use_fwfm:
                 eng.sync_pairs(self.fwfm_pair_max)
         params = [q for q in self.parameters() if q.requires_grad]
         out, _ = torch.ops.dfwfm.forward(torch_ops.register(self), xi, xv, params, False, 0.0, 0)

@@ -854,7 +854,7 @@ int dfwfm_model_pack_tables(dfwfm_model* m, int32_t enable, int32_t* enabled, vo
   if (!enable) return DFWFM_OK;
   if (!m->tables_set) return fail(DFWFM_ERR_STATE, "set_tables must precede pack_tables");
   const int need = kHasSecond | kNeedE | kFoTables;
-  if (m->cfg.use_deep || (m->flags & need) != need || (m->flags & kHasQR) || m->F - m->num < 1) return DFWFM_OK;
+  if ((m->flags & need) != need || (m->flags & kHasQR) || m->F - m->num < 1) return DFWFM_OK;
   const int D = m->D;
   const int pkw = D + 1 <= 16 ? 16 : (D + 4) & ~3;
   PackTabList L;
@@ -1013,6 +1013,8 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   }
   FwdArgs a;
   fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, out);
+  a.pk = nullptr;  // the training forward reads the tables the optimizer updates, never the serving copy
+  a.pkw = 0;
   a.flags |= kTrain | ((m->H > 0 && dropout_p > 0.f) ? kDrop : 0);
   a.sv_e = m->sv_e;
   a.sv_fo = m->sv_fo;

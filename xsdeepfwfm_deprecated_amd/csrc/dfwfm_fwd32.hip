@@ -191,14 +191,17 @@ fwd32_kernel(FwdArgs p) {
   const float* rd_emb2[QR ? 1 : RPT];
   const float* rd_emb1[QR ? 1 : RPT];
   int64_t rd_n[QR ? 1 : RPT];
+  // the tables' serving copy (dfwfm_model_pack_tables): a categorical row and its first-order weight in one row
+  bool pkrow[QR ? 1 : RPT];
   if constexpr (!QR) {
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int f = (tid + k * kNTH) >> 5;
       rd_emb2[k] = rd_emb1[k] = nullptr;
       rd_n[k] = 0;
+      pkrow[k] = p.pkw != 0 && f >= num && f < F;
       if (f < F) {
-        rd_emb2[k] = p.fields[f].emb2;
+        rd_emb2[k] = pkrow[k] ? p.pk[f] : p.fields[f].emb2;
         rd_emb1[k] = p.fields[f].emb1;
         rd_n[k] = p.fields[f].n;
       }
@@ -282,8 +285,12 @@ fwd32_kernel(FwdArgs p) {
             atomicOr(p.err, DFWFM_FLAG_INDEX_OUT_OF_RANGE);
             idx = 0;
           }
-          pa[k] = rd_emb2[k] + idx * D;
-          if (fo_tab) qa[k] = rd_emb1[k] + idx;
+          if (pkrow[k]) {
+            pa[k] = rd_emb2[k] + idx * p.pkw;
+          } else {
+            pa[k] = rd_emb2[k] + idx * D;
+            if (fo_tab) qa[k] = rd_emb1[k] + idx;
+          }
         }
       } else {
         const FieldDev fd = desc[f];
@@ -325,15 +332,19 @@ fwd32_kernel(FwdArgs p) {
 #pragma unroll
         for (int d = 0; d < D; ++d) vb[k][d] = 0.f;
       }
-      if (live[k] && needE) {
-        load_row<D>(va[k], pa[k]);
-        if constexpr (QR)
-          if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
-      }
-      if (live[k] && fo_tab) {
-        fa[k] = *qa[k];
-        if constexpr (QR)
-          if (mode[k] != 0) fb[k] = *qb[k];
+      if (!QR && live[k] && pkrow[QR ? 0 : k]) {  // second and first order in one aligned row
+        load_row_fo<D>(va[k], fa[k], pa[k]);
+      } else {
+        if (live[k] && needE) {
+          load_row<D>(va[k], pa[k]);
+          if constexpr (QR)
+            if (mode[k] != 0) load_row<D>(vb[k], pb[k]);
+        }
+        if (live[k] && fo_tab) {
+          fa[k] = *qa[k];
+          if constexpr (QR)
+            if (mode[k] != 0) fb[k] = *qb[k];
+        }
       }
     }
     // layer-0 weights behind the row loads (vmcnt retires in issue order)

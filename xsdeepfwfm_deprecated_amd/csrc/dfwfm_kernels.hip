@@ -193,9 +193,9 @@ fwd_kernel(FwdArgs p) {
   const float* rd_emb2[kDirectDesc ? RPT : 1];
   const float* rd_emb1[kDirectDesc ? RPT : 1];
   int64_t rd_n[kDirectDesc ? RPT : 1];
-  // PART 3 with the serving copy (dfwfm_model_pack_tables): a categorical row and its first-order weight are ONE
-  // row of pkw floats
-  constexpr bool kPackable = PART == 3 && !QR && kDirectDesc;
+  // the inference forward with the serving copy (dfwfm_model_pack_tables): a categorical row and its first-order
+  // weight are ONE row of pkw floats
+  constexpr bool kPackable = (PART == 3 || (PART == 0 && !TRAIN)) && !QR && kDirectDesc;
   bool pkrow[kPackable ? RPT : 1];
   if constexpr (kDirectDesc) {
 #pragma unroll
