@@ -150,11 +150,20 @@ class _HostGate:
 def r32_on(config="deepfwfm", cu_mask="even-odd", batch_set=1):
     """The library runs the 32-sample-workgroup forward (fwd32_kernel) for the bench's deep configs when the
     launch's 32-sample workgroups give every CU of its stream two (a batch set of >= 4 batches of 4096 on the whole
-    chip), or one on a CU-masked stream (one batch on half of the chip); DFWFM_R32=1 forces it, DFWFM_R32=0 never."""
-    env = os.environ.get("DFWFM_R32", "")
+    chip), or one on a CU-masked stream (one batch on half of the chip); DFWFM_DIAG r32=1 forces it, r32=0 never."""
+    env = diag_opt("r32")
     if config in ("fwfm", "fwfm_pruned") or env == "0":
         return False
-    return env not in ("",) or cu_mask not in (None, "none") or batch_set >= 4
+    return env is not None or cu_mask not in (None, "none") or batch_set >= 4
+
+
+def diag_opt(key):
+    """The library's DFWFM_DIAG test / diagnostics option `key` (a "key=value,..." list), or None."""
+    for kv in os.environ.get("DFWFM_DIAG", "").split(","):
+        k, _, v = kv.partition("=")
+        if k == key:
+            return v
+    return None
 
 
 def masked_streams(dev, S, how):
@@ -186,21 +195,19 @@ def masked_streams(dev, S, how):
 
 def kernel_name(config="deepfwfm", cu_mask="none", batch_set=1):
     """The forward kernel instantiation the library picks for Criteo-39 / 3x400 (D, tiles per wave, K split,
-    train, part, tile groups); DFWFM_NG / DFWFM_SPLIT / DFWFM_R32 select the A/B variants."""
+    train, part, tile groups); DFWFM_DIAG ng / r32 / part3 / p3ng select the test variants."""
     if r32_on(config, cu_mask, batch_set):
         qr = 'true' if config == 'qr' else 'false'
         return f"dfwfm::fwd32_kernel<10,{qr}>"
     if config in ("fwfm", "fwfm_pruned"):
-        if os.environ.get("DFWFM_NO_PART3"):
+        if diag_opt("part3") == "0":
             return "dfwfm::fwd_kernel<10,1,1,false,0,4,0>"
-        png = os.environ.get("DFWFM_P3_NG")
+        png = diag_opt("p3ng")
         ng = 4 if png == "4" or (png is None and batch_set > 1) else 8  # batch sets: four waves (DESIGN.md 3.5)
         return f"dfwfm::fwd_kernel<10,1,1,false,3,{ng},3,false>"  # MLP-free, 3 FwFM row tiles, no QR field
-    ng = 4 if os.environ.get("DFWFM_NG") == "4" else 8
+    ng = 4 if diag_opt("ng") == "4" else 8
     tpw = 6 if ng == 4 else 3
-    if os.environ.get("DFWFM_SPLIT", "0") not in ("", "0"):
-        return f"dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::fwd_kernel<10,{tpw},1,false,2,{ng}>"
-    ns = 25 if ng == 8 and tpw == 3 and not os.environ.get("DFWFM_NO_STATIC_K") else 0  # static 25-chunk K loop
+    ns = 25 if ng == 8 and tpw == 3 else 0  # static 25-chunk K loop
     qr = "true" if (config == "qr" or ns != 25) else "false"  # the static form without QR fields: QR=false
     return f"dfwfm::fwd_kernel<10,{tpw},1,false,0,{ng},{ns},{qr}>"  # as rocprofv3 names it (QR argument last)
 
@@ -343,14 +350,14 @@ def main():
     # CU); the FwFM-only forward is latency-bound and gains from a third (three eight-wave workgroups per CU)
     # deep configs: four batches in flight on CU-masked stream pairs (even / odd CU ids): a 4096-row batch is 128
     # 32-sample workgroups, which cover a half, so the library runs fwd32_kernel and every CU holds two batches
-    # (DESIGN.md section 3); DFWFM_R32=0: the 16-sample kernel on two plain streams
+    # (DESIGN.md section 3); DFWFM_DIAG=r32=0: the 16-sample kernel on two plain streams
     # batch sets (default): every launch is one grid over up to M resident batches on the whole chip (the
     # 32-sample forward for the deep configs: a set's workgroups cover every CU twice over); when the K steps
     # fit one set they are ONE launch, else two streams, so that the next set's workgroups take the CU slots
     # the current one frees while it drains.  --batch-set 1: one launch per batch from captured graphs; the deep
     # configs then run four batches in flight on CU-masked stream pairs
     M = max(1, a.batch_set)
-    r32_default = deep and os.environ.get("DFWFM_R32", "") != "0"
+    r32_default = deep and diag_opt("r32") != "0"
     cu_mask = a.cu_mask if a.cu_mask is not None else ("even-odd" if r32_default and M == 1 else "none")
     S = max(1, a.streams if a.streams is not None else
             ((1 if a.steps <= M else 2) if M > 1 else (3 if not deep else (4 if r32_default else 2))))
@@ -677,8 +684,8 @@ def per_call_leg(eng, batches, dev, steps, flops, bytes_, config, settle_ms=150.
 
 
 def gather_leg(eng, batches, dev, steps, read_bytes, settle_ms=100.0, streams=4):
-    """The deep forward's gather / shallow half alone (dfwfm_forward_gather: the split forward's first launch,
-    fwd_kernel PART 1 -- the per-field rows of model/DeepFMs.py:300-367 into deep_emb (:398), first + second order)
+    """The deep forward's gather / shallow half alone (dfwfm_forward_gather: the MLP-free kernel, fwd_kernel PART 3,
+    storing deep_emb -- the per-field rows of model/DeepFMs.py:300-367 into deep_emb (:398), first + second order)
     over the resident batches, one batch of 4096 per call, replayed from captured graphs like per_call: on one
     stream (`lone`: one 16-sample tile per CU, the chain's latency) and with `streams` calls in flight (the
     headline numbers: throughput).  `achieved` = the gather's algorithmic read bytes per sample (Xi, Xv, the
@@ -737,7 +744,7 @@ def gather_leg(eng, batches, dev, steps, read_bytes, settle_ms=100.0, streams=4)
             "in_flight": streams,
             "lone": {"us_per_batch": round(us1, 3),
                      "achieved": round(read_bytes * BATCH / (us1 / 1e6) / 1e9, 1)},
-            "kernel": "dfwfm::fwd_kernel<10,1,1,false,1,4,0,true> (dfwfm_forward_gather)",
+            "kernel": "dfwfm::fwd_kernel<10,1,1,false,3,8,3,false> (dfwfm_forward_gather)",
             "what": "the deep forward's gather / shallow half as its own launch per 4096-sample batch, "
                     f"{streams} streams in flight (lone: one stream)"}
 

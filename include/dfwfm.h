@@ -144,9 +144,10 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
 /* The gather / shallow half of a deep model's forward alone (reference model/DeepFMs.py:300-367 and the deep_emb
  * `cat` of :398): the per-field embedding rows (numerical v_f * Xv, categorical nn.Embedding / QR rows) into
  * deep_emb [batch][deep_emb_stride] (zero padded past F * D) and first + second order into first_second[batch] --
- * the split forward's first launch, so that the gather has its own duration and HBM rate (bench.py
- * roofline_gather).  deep_emb_stride must equal ceil(F * D / 16) * 16 (the MLP's K chunks).  Models without a
- * deep tower: DFWFM_ERR_UNSUPPORTED (their whole forward is this half). */
+ * the forward without its MLP (the MLP-free forward's kernel storing deep_emb), so that the gather has its own
+ * duration and HBM rate (bench.py roofline_gather); first_second agrees with the fused forward's shallow part to
+ * fp32 summation order.  deep_emb_stride must equal ceil(F * D / 16) * 16 (the MLP's K chunks).  Models without
+ * a deep tower: DFWFM_ERR_UNSUPPORTED (their whole forward is this half). */
 int dfwfm_forward_gather(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
                          int64_t batch, float* deep_emb, int64_t deep_emb_stride, float* first_second, void* stream);
 
@@ -383,7 +384,7 @@ int dfwfm_read_error_flag(dfwfm_model* m, int32_t* flag, void* stream);
 
 /* Diagnostics. */
 const char* dfwfm_last_error(void);
-/* With DFWFM_DIAG_STAMPS=1 in the environment, each forward records 16 shader-clock stamps per
+/* With DFWFM_DIAG=stamps=1 in the environment, each forward records 16 shader-clock stamps per
  * 16-sample workgroup at its phase boundaries; copies up to n of them (synchronising `stream`)
  * and returns the number of workgroups copied, or a negative status. */
 int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream);

@@ -123,24 +123,6 @@ def test_batch_set_strided_inputs_and_errors(gpu):
     assert eng.forward_batches([], []) == []
 
 
-@pytest.mark.parametrize("env", ["DFWFM_DEFER_TAIL", "DFWFM_PRIO_EPI"])
-def test_batch_set_fwd32_schedule_variants_bit_identical(gpu, monkeypatch, env):
-    """fwd32 schedule switches (the split tile's barrier inside the next K loop; raised priority in the MLP
-    epilogues) change when work issues, not the arithmetic: same bits as the default schedule."""
-    cfg, params, m = _criteo_model(gpu, 1, 0, seed=19)
-    host = _inputs(cfg["feature_sizes"], 3, 4096 + 5, seed=23)
-    dev = [(torch.from_numpy(xi).to(gpu), torch.from_numpy(xv).to(gpu)) for xi, xv in host]
-    res = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv(env, v)
-        eng = m._sync_engine(gpu)
-        outs = [torch.empty(4096 + 5, device=gpu) for _ in dev]
-        with torch.no_grad():
-            eng.forward_batches(dev, outs)
-        res[v] = torch.stack(outs).cpu().numpy()
-    assert np.array_equal(res["0"], res["1"])
-
-
 @pytest.mark.parametrize("deep", [1, 0])
 def test_eval_by_batch_batch_sets_identical(gpu, deep):
     """eval_by_batch's full 8192-row batches as batch sets give the same loss and metrics as one forward per batch

@@ -261,40 +261,6 @@ def test_device_metrics_exact_on_separated_logits(gpu):
     assert abs(m["prauc"] - auc(rec, prec)) < 1e-12
 
 
-@pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_qr_mult", "deepfwfm_fwlw_lw", "deepfwfm_small_mlp"])
-@pytest.mark.parametrize("B", [1, 17, 256])
-def test_split_forward_is_bit_identical_to_fused(gpu, name, B, monkeypatch):
-    # dfwfm_forward_ws (gather launch + MLP launch, opt-in DFWFM_SPLIT=1, read at model creation)
-    # against dfwfm_forward (one fused launch)
-    import ctypes
-    from xsdeepfwfm_deprecated_amd import _lib
-    monkeypatch.setenv("DFWFM_SPLIT", "1")
-    cfg, params, xi, xv, *_ = load_golden(name)
-    m = make_model(cfg, params, gpu)
-    xi_t = torch.from_numpy(xi[:B]).to(gpu)
-    xv_t = torch.from_numpy(xv[:B]).to(gpu)
-    with torch.no_grad():
-        split = m(xi_t, xv_t)
-        eng = m._engine
-        n = ctypes.c_size_t(0)
-        _lib.check(_lib.lib().dfwfm_forward_workspace_bytes(eng.handle, B, ctypes.byref(n)), "ws bytes")
-        assert n.value > 0  # deep models run split
-        fused = torch.empty(B, device=gpu)
-        s = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
-        _lib.check(_lib.lib().dfwfm_forward(eng.handle, ctypes.c_void_p(xi_t.data_ptr()), xi_t.stride(0),
-                                            ctypes.c_void_p(xv_t.data_ptr()), xv_t.stride(0), B,
-                                            ctypes.c_void_p(fused.data_ptr()), s), "fused forward")
-        # a too-small workspace is refused
-        ws = torch.empty(n.value, dtype=torch.uint8, device=gpu)
-        rc = _lib.lib().dfwfm_forward_ws(eng.handle, ctypes.c_void_p(xi_t.data_ptr()), xi_t.stride(0),
-                                         ctypes.c_void_p(xv_t.data_ptr()), xv_t.stride(0), B,
-                                         ctypes.c_void_p(fused.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                                         n.value - 4, s)
-        assert rc == -1
-    torch.cuda.synchronize()
-    assert torch.equal(split.cpu(), fused.cpu())
-
-
 def _sweep_case(F, num, D, N, H, fwlw, seed):
     """A synthetic DeepFwFM config (small tables) and its params / inputs, for shape sweeps."""
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
@@ -316,7 +282,7 @@ def _sweep_case(F, num, D, N, H, fwlw, seed):
 @pytest.mark.parametrize("D,N,H,fwlw", [(10, 400, 3, 0), (10, 144, 2, 1), (4, 256, 1, 0), (16, 512, 2, 0),
                                         (8, 96, 3, 1), (32, 400, 1, 0), (10, 340, 2, 0)])
 def test_forward_shape_sweep_matches_oracle(gpu, monkeypatch, ng, D, N, H, fwlw):
-    monkeypatch.setenv("DFWFM_NG", ng)
+    monkeypatch.setenv("DFWFM_DIAG", f"ng={ng}")
     cfg, params, xi, xv = _sweep_case(39, 13, D, N, H, fwlw, seed=D * 1000 + N + H)
     m = make_model(cfg, params, gpu)
     got = run(m, xi, xv, gpu)
@@ -412,7 +378,7 @@ def test_forward_extreme_shapes_match_oracle(gpu, F, num, D, N, H):
 @pytest.mark.parametrize("qr", [0, 1])
 @pytest.mark.parametrize("B", [1, 31, 33, 4096 + 17])
 def test_fwd32_bit_identical_to_fwd_kernel(gpu, monkeypatch, qr, B):
-    """The 32-sample-workgroup forward (fwd32_kernel, DFWFM_R32=1: both 16-row tiles per wave in the MLP) gives the
+    """The 32-sample-workgroup forward (fwd32_kernel, DFWFM_DIAG=r32=1: both 16-row tiles per wave in the MLP) gives the
     same bits as fwd_kernel's static 3x400 form at Criteo-39 sizes (ragged tails, QR fields) and the oracle's
     logits at the north-star bar."""
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
@@ -426,7 +392,7 @@ def test_fwd32_bit_identical_to_fwd_kernel(gpu, monkeypatch, qr, B):
     xi, xv = synth.synth_inputs(sizes, 13, B, seed=B)
     outs = {}
     for r32 in ("0", "1"):
-        monkeypatch.setenv("DFWFM_R32", r32)
+        monkeypatch.setenv("DFWFM_DIAG", f"r32={r32}")
         mm = make_model(cfg, params, gpu)
         outs[r32] = run(mm, xi, xv, gpu)
     assert np.array_equal(outs["0"], outs["1"])
@@ -437,7 +403,7 @@ def test_fwd32_bit_identical_to_fwd_kernel(gpu, monkeypatch, qr, B):
 @pytest.mark.parametrize("name", ["deepfwfm_lw", "deepfwfm_fwlw_lw", "deepfwfm_qr_mult", "deepfwfm_qr_add_fwlw",
                                   "deepfwfm_embbag", "deepfwfm_pruned", "fm_deep"])
 def test_fwd32_matches_reference_goldens(gpu, monkeypatch, name):
-    monkeypatch.setenv("DFWFM_R32", "1")
+    monkeypatch.setenv("DFWFM_DIAG", "r32=1")
     cfg, params, xi, xv, y, l32, l64, auc = load_golden(name)
     m = make_model(cfg, params, gpu)
     got = run(m, xi, xv, gpu)

@@ -1,5 +1,5 @@
 """GPU: the forward without a deep tower -- the FwFM-only config of BASELINE configs[0]: the default
-MLP-free fwd_kernel (PART 3, per-sample Gram FwFM) and the generic fused kernel (DFWFM_NO_PART3=1) against the
+MLP-free fwd_kernel (PART 3, per-sample Gram FwFM) and the generic fused kernel (DFWFM_DIAG=part3=0) against the
 oracle."""
 import numpy as np
 import pytest
@@ -76,15 +76,15 @@ CASES = [
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_mlp_free_kernels_match_oracle(gpu, monkeypatch, case):
-    """The default MLP-free kernel (per-sample Gram FwFM) and the generic fused kernel (DFWFM_NO_PART3: the
+    """The default MLP-free kernel (per-sample Gram FwFM) and the generic fused kernel (DFWFM_DIAG part3=0: the
     piece-wise FwFM) against the oracle over the configs without a deep tower."""
     cfg, params, xi, xv = _case(**case, seed=len(str(case)))
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
     part3 = _run(_model(cfg, params, gpu, monkeypatch), xi, xv, gpu)
     assert _err(part3, ref, cfg, params, xi, xv) < 1e-5
-    monkeypatch.setenv("DFWFM_NO_PART3", "1")
+    monkeypatch.setenv("DFWFM_DIAG", "part3=0")
     fused = _run(_model(cfg, params, gpu, monkeypatch), xi, xv, gpu)
-    monkeypatch.delenv("DFWFM_NO_PART3")
+    monkeypatch.delenv("DFWFM_DIAG")
     assert _err(fused, ref, cfg, params, xi, xv) < 1e-5
 
 
@@ -105,13 +105,13 @@ def test_default_mlp_free_kernel_ragged_and_full_size(gpu, monkeypatch, B):
                                   dict(F=64, num=0, D=16), dict(F=5, num=2, D=4), dict(F=39, num=13, D=32)],
                          ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_mlp_free_four_and_eight_waves_bit_identical(gpu, monkeypatch, case):
-    """PART 3 on eight waves (the default) and on four (DFWFM_P3_NG=4, no QR operands): each sample's Gram sum
+    """PART 3 on eight waves (the default) and on four (DFWFM_DIAG p3ng=4, no QR operands): each sample's Gram sum
     is formed by one wave in the same order, so the logits are bit-identical."""
     cfg, params, xi, xv = _case(**case, B=4096 + 5, seed=11)
     got8 = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
-    monkeypatch.setenv("DFWFM_P3_NG", "4")
+    monkeypatch.setenv("DFWFM_DIAG", "p3ng=4")
     got4 = _run(_model(cfg, params, gpu, monkeypatch, False), xi, xv, gpu)
-    monkeypatch.delenv("DFWFM_P3_NG")
+    monkeypatch.delenv("DFWFM_DIAG")
     assert np.array_equal(got4, got8)
     ref = dfwfm_oracle.forward(cfg, params, xi, xv)
     assert _err(got4, ref, cfg, params, xi, xv) < 1e-5

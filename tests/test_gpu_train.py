@@ -1030,8 +1030,8 @@ def _hot_case(B, seed=4):
 @pytest.mark.parametrize("B", [3000, 9000])  # 9000: three sorted passes of <= 4096 samples
 def test_sorted_scatter_bit_identical_and_matches_atomic(gpu, monkeypatch, B):
     """Deterministic mode (sorted table scatter, split-K slices): two backward passes give the same bits, and equal
-    the atomic scatter (DFWFM_SCATTER=atomic, arrival-order sums) within fp32 reassociation, hot rows and multi-pass
-    batches included."""
+    the atomic scatter (the default, arrival-order sums) within fp32 reassociation, hot rows and multi-pass batches
+    included."""
     m, xi, xv, y = _hot_case(B)
     m = m.to(gpu).train()
     m.init_weights()
@@ -1040,7 +1040,7 @@ def test_sorted_scatter_bit_identical_and_matches_atomic(gpu, monkeypatch, B):
     g2, _, _ = _sparse_step(m, gpu, xi, xv, y, sparse=False, bce_fused=True)
     for k in g1:
         assert np.array_equal(g1[k], g2[k]), k
-    monkeypatch.setenv("DFWFM_SCATTER", "atomic")
+    m._sync_engine(gpu).set_deterministic(False)
     ga, _, _ = _sparse_step(m, gpu, xi, xv, y, sparse=False, bce_fused=True)
     for k in g1:
         sc = np.abs(ga[k]).max()
@@ -1124,7 +1124,7 @@ def test_autograd_backward_deterministic_switch(gpu):
                                              (False, True, 512, 1), (False, True, 700, 2)])
 def test_helper_wave_train_forward_bit_identical(gpu, monkeypatch, qr, drop, B, depth):
     """The training forward with helper waves (ftrain_kernel: the shallow part and the activation saves on four waves
-    beside the MLP's eight) against fwd_kernel<TRAIN> (DFWFM_FTRAIN=0), Criteo-39 sizes, 3x400 MLP: two deterministic
+    beside the MLP's eight) against fwd_kernel<TRAIN> (DFWFM_DIAG=ftrain=0), Criteo-39 sizes, 3x400 MLP: two deterministic
     fused steps give the same logits and the same parameters bit for bit (every saved activation feeds the
     backward), with and without deep dropout, QR tables, a ragged last tile, one and two hidden layers."""
     from xsdeepfwfm_deprecated_amd import DeepFMs, synth
@@ -1137,7 +1137,7 @@ def test_helper_wave_train_forward_bit_identical(gpu, monkeypatch, qr, drop, B, 
                      torch.from_numpy((np.arange(B) % 3 == i).astype(np.float32)).to(gpu)))
     res = []
     for ft in ("0", "1"):
-        monkeypatch.setenv("DFWFM_FTRAIN", ft)
+        monkeypatch.setenv("DFWFM_DIAG", f"ftrain={ft}")
         torch.manual_seed(5)
         kw = dict(embedding_bag=1, qr_flag=1, qr_operation="mult", qr_collisions=4, qr_threshold=200) if qr else {}
         m = DeepFMs(field_size=39, feature_sizes=sizes, use_fwfm=1, use_fm=0, use_deep=1, use_lw=1, h_depth=depth,

@@ -11,8 +11,8 @@ while read -r env st; do
 done <<LIST
 ${VARIANTS:-X=0 2
 X=0 3
-DFWFM_DIAG_DROP_FLAGS=1 2
-DFWFM_DIAG_DROP_FLAGS=33 2
-DFWFM_DIAG_DROP_FLAGS=49 2}
+DFWFM_DIAG=drop_flags=1 2
+DFWFM_DIAG=drop_flags=33 2
+DFWFM_DIAG=drop_flags=49 2}
 LIST
 if [ -n "${STAMPS:-}" ]; then timeout -k 10 120 python tools/phase_stamps.py; fi

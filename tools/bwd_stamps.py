@@ -1,8 +1,8 @@
 """Per-phase cycle breakdown of the fused backward from in-kernel s_memtime stamps (diagnostic).
 
-    [DFWFM_DIAG_BWD=<bits>] python tools/bwd_stamps.py [--batch 4096] [--iters 5]     (sets DFWFM_DIAG_STAMPS=2)
+    [DFWFM_DIAG=bwd=<bits>] python tools/bwd_stamps.py [--batch 4096] [--iters 5]     (adds stamps=2)
 
-DFWFM_DIAG_BWD (diagnostics, results invalid for 1 and 2): 1 no G_l stores, 2 no mask loads, 4 the generic K loop
+DFWFM_DIAG bwd= (diagnostics, results invalid for 1 and 2): 1 no G_l stores, 2 no mask loads, 4 the generic K loop
 """
 import argparse
 import ctypes
@@ -14,7 +14,8 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["DFWFM_DIAG_STAMPS"] = "2"
+from _diag import diag_set  # noqa: E402
+diag_set("stamps", 2)
 
 from xsdeepfwfm_deprecated_amd import DeepFMs, _lib, synth  # noqa: E402
 

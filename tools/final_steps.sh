@@ -20,7 +20,7 @@ bash tools/gpu_steps.sh "$T" \
  'train|200|python tools/bench_train.py --steps 500 --warmup 20' \
  'train4|200|python tools/bench_train.py --steps 500 --warmup 20 --steps-per-graph 4' \
  'traindet|200|python tools/bench_train.py --steps 500 --warmup 20 --deterministic' \
- 'train0|200|DFWFM_FTRAIN=0 python tools/bench_train.py --steps 500 --warmup 20' \
+ 'train0|200|DFWFM_DIAG=ftrain=0 python tools/bench_train.py --steps 500 --warmup 20' \
  "proftrain|200|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_proftrain -o run --output-format csv -- python3 tools/bench_train.py --steps 50" \
- 'st-train|120|DFWFM_DIAG_STAMPS=1 python tools/phase_stamps.py --train --batch 4096 --iters 10' \
+ 'st-train|120|python tools/phase_stamps.py --train --batch 4096 --iters 10' \
  'latency|300|python tools/latency.py --calls 300'

@@ -33,7 +33,6 @@ for s in $STEPS; do
     bench_fwlw) step bench_fwlw 300 python bench.py --steps 200 --warmup 20 --first-order fwlw --no-cpu-baseline ;;
     prof)   step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     prof1)  step prof1 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1_$TAG -o run --output-format csv -- python3 bench.py --no-cpu-baseline --streams 1 ;;
-    profsplit) DFWFM_SPLIT=1 step profsplit 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profsplit_$TAG -o run --output-format csv -- python3 bench.py --no-cpu-baseline --streams 1 ;;
     pmc)    step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-graph &&
             step pmc_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-graph ;;
   esac

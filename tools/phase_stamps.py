@@ -1,6 +1,6 @@
 """Per-phase cycle breakdown of the fused forward from in-kernel s_memtime stamps (diagnostic).
 
-    DFWFM_DIAG_STAMPS=1 [DFWFM_R32=1] python tools/phase_stamps.py [--batch 4096] [--iters 20] [--fwfm] [--batches N]
+    [DFWFM_DIAG=r32=1] python tools/phase_stamps.py [--batch 4096] [--iters 20] [--fwfm] [--batches N]
 
 --fwfm: the MLP-free FwFM-only model (fwd_kernel PART 3); --batches N: N distinct resident batches as one batch set
 (dfwfm_forward_batches), with the launch's workgroup lifetimes and concurrency from the 100 MHz stamps.
@@ -14,7 +14,8 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("DFWFM_DIAG_STAMPS", "1")
+from _diag import diag_get, diag_set  # noqa: E402
+diag_set("stamps", 1, overwrite=False)
 
 from xsdeepfwfm_deprecated_amd import DeepFMs, _lib, synth  # noqa: E402
 
@@ -55,7 +56,7 @@ else:
             else:
                 m(xi, xv)
 torch.cuda.synchronize()
-rows = 32 if os.environ.get("DFWFM_R32") == "1" else 16  # DFWFM_R32=1: fwd32_kernel's 32-sample workgroups
+rows = 32 if diag_get("r32") == "1" else 16  # r32=1: fwd32_kernel's 32-sample workgroups
 grid = a.batches * ((a.batch + rows - 1) // rows)
 buf = (ctypes.c_uint64 * (grid * 16))()
 n = _lib.lib().dfwfm_diag_stamps(m._engine.handle, buf, grid * 16,
@@ -68,7 +69,7 @@ names = ["stage (params, Xi/Xv)", "gather E + table first order", "shallow (fwlw
          "MLP layer 3", "deep reduce + combine"]
 slots = [(0, 1), (1, 2), (2, 3), (2, 9), (9, 10), (10, 11), (11, 3), (11, 7), (7, 3), (3, 4), (3, 12), (12, 13),
          (13, 4), (4, 5), (5, 6), (6, 8)]
-if int(os.environ.get("DFWFM_DIAG_FT", "0")) & 1:  # ftrain_kernel: each wave's HW_ID in slot `wave`
+if int(diag_get("ft", "0")) & 1:  # ftrain_kernel: each wave's HW_ID in slot `wave`
     for w in range(min(4, n)):
         print(f"workgroup {w}: wave -> SIMD", [int((st[w, k] >> 4) & 3) for k in range(12)],
               "CU", [int((st[w, k] >> 8) & 15) for k in range(12)])
@@ -93,13 +94,13 @@ if a.fwfm:  # no MLP: stage, gather, shallow phases, then the combine (slot 8)
              "  . fwlw first order", "  . FwFM MFMA (wave 0)", "  . barrier wait", "  . sums (wave 0)",
              "  . barrier + logits out"]
     slots = [(0, 1), (1, 2), (2, 8), (2, 9), (9, 10), (10, 11), (11, 7), (7, 8)]
-elif a.train and os.environ.get("DFWFM_FTRAIN", "1") != "0":  # ftrain_kernel: helper waves beside the MLP
+elif a.train and diag_get("ftrain", "1") != "0":  # ftrain_kernel: helper waves beside the MLP
     names = ["stage (params, Xi/Xv)", "gather E (+ X_0) to LDS", "  helpers W0: FwFM pieces", "  helpers W0: fwlw, E / X_0",
              "  helpers W1: sums, fo save, X_1", "  helpers W2: X_2", "MLP layer 1", "  . K loop (wave 0)",
              "  . epilogue (wave 0)", "  . barriers, split tile", "MLP layer 2", "MLP layer 3", "combine"]
     slots = [(0, 1), (1, 2), (2, 10), (10, 9), (4, 11), (5, 7), (3, 4), (3, 12), (12, 13), (13, 4), (4, 5), (5, 6),
              (6, 8)]
-elif os.environ.get("DFWFM_R32") == "1":  # fwd32 has no slot 7
+elif diag_get("r32") == "1":  # fwd32 has no slot 7
     names = names[:7] + names[9:]
     slots = slots[:7] + slots[9:]
 for nm, sl in zip(names, slots):

@@ -1,5 +1,5 @@
 """Time the backward's table scatter alone (DFWFM_BWD_SCATTER after one train forward + per-tile backward) at
-Criteo-39 sizes, B = 4096, with the diagnostic phase switches DFWFM_SCATTER_DIAG (results invalid when set).
+Criteo-39 sizes, B = 4096, with the diagnostic phase switches DFWFM_DIAG scatter= (results invalid when set).
 
     python tools/scatter_diag.py [--iters 50]
 """
@@ -26,6 +26,7 @@ def one(iters):
     xi, xv = synth.synth_inputs(sizes, 13, B, seed=3)
     xi_d, xv_d = torch.from_numpy(xi).to(dev), torch.from_numpy(xv).to(dev)
     eng = m._sync_engine(dev)
+    eng.set_deterministic(os.environ.get("SCATTER_MODE", "sorted") == "sorted")  # the sorted scatter is deterministic mode's
     out = torch.empty(B, device=dev)
     eng.train_forward(xi_d, xv_d, out, 0.0, 0)
     fields, dense = m._param_layout()
@@ -64,10 +65,10 @@ if __name__ == "__main__":
         print(json.dumps({"us": one(a.iters)}))
         sys.exit(0)
     res = {}
-    for name, env in [("atomic", {"DFWFM_SCATTER": "atomic"}), ("sorted", {}), ("nosort", {"DFWFM_SCATTER_DIAG": "1"}),
-                      ("nosums", {"DFWFM_SCATTER_DIAG": "2"}), ("noadds", {"DFWFM_SCATTER_DIAG": "4"}),
-                      ("keys_only", {"DFWFM_SCATTER_DIAG": "3"}), ("empty", {"DFWFM_SCATTER_DIAG": "8"}),
-                      ("loads_only", {"DFWFM_SCATTER_DIAG": "16"})]:
+    for name, env in [("atomic", {"SCATTER_MODE": "atomic"}), ("sorted", {}), ("nosort", {"DFWFM_DIAG": "scatter=1"}),
+                      ("nosums", {"DFWFM_DIAG": "scatter=2"}), ("noadds", {"DFWFM_DIAG": "scatter=4"}),
+                      ("keys_only", {"DFWFM_DIAG": "scatter=3"}), ("empty", {"DFWFM_DIAG": "scatter=8"}),
+                      ("loads_only", {"DFWFM_DIAG": "scatter=16"})]:
         e = dict(os.environ)
         e.update(env)
         p = subprocess.run([sys.executable, __file__, "--child", "--iters", str(a.iters)], env=e, capture_output=True,

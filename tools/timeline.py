@@ -2,7 +2,7 @@
 every workgroup's start / end on the 100 MHz clock, its CU, and its phase boundaries (shader clock,
 mapped onto the workgroup's own start..end).  Shows how the streams' workgroups share the CUs.
 
-    DFWFM_DIAG_STAMPS=1 DFWFM_DIAG_RING=40 python tools/timeline.py [--streams 2] [--graph-steps 20]
+    python tools/timeline.py [--streams 2] [--graph-steps 20]
 """
 import argparse
 import ctypes
@@ -19,8 +19,9 @@ ap.add_argument("--graph-steps", type=int, default=20)
 ap.add_argument("--replays", type=int, default=5)
 ap.add_argument("--fwfm", action="store_true", help="FwFM-only model (use_deep=0)")
 a = ap.parse_args()
-os.environ["DFWFM_DIAG_STAMPS"] = "1"
-os.environ["DFWFM_DIAG_RING"] = str(a.streams * a.graph_steps)
+from _diag import diag_set  # noqa: E402
+diag_set("stamps", 1)
+diag_set("ring", a.streams * a.graph_steps)
 
 from xsdeepfwfm_deprecated_amd import DeepFMs, _lib, synth  # noqa: E402
 

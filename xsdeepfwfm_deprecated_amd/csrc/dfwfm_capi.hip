@@ -32,7 +32,6 @@ struct dfwfm_model {
   int cu_count[8], cu_n, cu_next;
   int dev_cus;         // CUs of the device (0 until the first stream_cu_count)
   size_t lds_inf;      // inference forward LDS (lds_bytes: the training forward's, NG = 4)
-  int split;           // forward as two launches (gather, MLP) when the caller supplies a workspace
   // sparse deep tower (dfwfm_model_build_sparse_mlp): ELL of the pruned weights, used by dfwfm_forward_ws
   int sp;                          // enabled (cleared by set_dense: the ELL is then stale)
   const float* lin_w[kMaxH];       // the caller's weights from the last set_dense
@@ -61,9 +60,9 @@ struct dfwfm_model {
   float* d_fwlw;   // [F*D]
   float* d_lw;     // [F]
   float* d_bias;   // [1]
-  uint64_t* d_stamps;  // diagnostics (DFWFM_DIAG_STAMPS)
+  uint64_t* d_stamps;  // diagnostics (DFWFM_DIAG stamps=)
   size_t stamps_cap;   // workgroups the stamp buffer holds
-  size_t stamps_ring;  // launches kept (DFWFM_DIAG_RING), each its own slice of the buffer
+  size_t stamps_ring;  // launches kept (DFWFM_DIAG ring=), each its own slice of the buffer
   size_t stamps_next;  // next slice
   // training
   float4* d_wtpack;    // transposed MLP packs for dX_{l-1} = G_l W_l
@@ -234,15 +233,14 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   const int kx = m->W0 > NT * 16 ? m->W0 : NT * 16;
   m->SX = r4(kx) + 4;
   m->SY = c.use_deep ? NT * 16 + 4 : 0;
-  // one wave per SIMD; DFWFM_KSPLIT=2 runs two per SIMD splitting K (measured slower, kept for A/B)
+  // one wave per SIMD (two per SIMD splitting K measured slower, removed in round 6)
   m->KS = 1;
-  if (const char* ks = getenv("DFWFM_KSPLIT")) m->KS = atoi(ks) == 2 ? 2 : 1;
   // 4k+1 output tiles (N = 400: 25): the last tile is split by K over the four waves instead of
-  // giving one SIMD an extra whole tile (DFWFM_NO_TAIL=1 disables it, for A/B)
+  // giving one SIMD an extra whole tile
   m->TPWF = TPW;
   m->tail = 0;
   if (c.use_deep && m->KS == 1 && NT % 4 == 1 && NT >= 5 && m->NC0 >= 4 && m->NC0 <= 4 * kTailC &&
-      NT <= 4 * kTailC && !getenv("DFWFM_NO_TAIL")) {
+      NT <= 4 * kTailC) {
     m->TPWF = NT / 4;
     m->tail = 1;
   }
@@ -256,7 +254,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   m->lds_gather = sizeof(float) * (size_t)lds_layout(F, D, m->MT, m->S, m->SX, m->SY, m->TPWF > 0 ? m->TPWF : 1,
                                                      1, false, false).total;
   // inference: eight tile groups (two waves per SIMD at <= 128 registers) when the layer fits them
-  // (<= 32 output tiles); DFWFM_NG=4 selects the four-wave kernel the training forward uses
+  // (<= 32 output tiles); DFWFM_DIAG ng=4 selects the four-wave kernel the training forward uses
   m->NG = 4;
   m->TPWI = m->TPWF;
   m->tailI = m->tail;
@@ -264,10 +262,9 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   if (!c.use_deep)  // the MLP-free forward runs on eight waves (fwd_kernel PART 3): its layout's per-wave slots
     m->lds_inf = sizeof(float) * (size_t)lds_layout(F, D, m->MT, m->S, m->SX, m->SY, 1, 1, false, false, 8).total;
   if (c.use_deep && m->KS == 1 && NT <= 32 && m->NC0 <= 32) {
-    const char* ng = getenv("DFWFM_NG");
-    if (!ng || atoi(ng) == 8) {
+    if (diag_opt("ng", 8) == 8) {  // (DFWFM_DIAG ng=4: the four-wave kernel, tests)
       m->NG = 8;
-      m->tailI = (NT % 8 == 1 && NT >= 9 && m->NC0 >= 8 && !getenv("DFWFM_NO_TAIL")) ? 1 : 0;
+      m->tailI = (NT % 8 == 1 && NT >= 9 && m->NC0 >= 8) ? 1 : 0;
       m->TPWI = m->tailI ? NT / 8 : (NT + 7) / 8;
       m->lds_inf = sizeof(float) * (size_t)lds_layout(F, D, m->MT, m->S, m->SX, m->SY, m->TPWI, 1, true,
                                                       m->tailI != 0, 8).total;
@@ -276,27 +273,18 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   // 32-sample workgroups (fwd32_kernel: every weight fragment feeds both 16-row tiles) for the static 3x400 form,
   // chosen per launch when the batch's 32-sample workgroups still cover every CU the stream may use (a stream
   // masked to half of the chip, or a batch of >= 32 x CUs rows; else the 16-sample kernel keeps all CUs busy);
-  // DFWFM_R32=0 never, =1 always (tests)
+  // DFWFM_DIAG r32=0 never, r32=1 always (tests)
   {
-    const char* r32 = getenv("DFWFM_R32");
-    const int mode = !r32 || !*r32 ? 1 : (atoi(r32) != 0 ? 2 : 0);
+    const int r32 = diag_opt("r32", -1);
+    const int mode = r32 < 0 ? 1 : (r32 != 0 ? 2 : 0);
     m->r32 = (c.use_deep && fwd32_supported(F, D, H, NT, m->NC0, m->tailI, m->NG)) ? mode : 0;
     m->lds_r32 = m->r32 ? fwd32_lds_bytes(F, D, m->MT, m->S, m->SX) : 0;
     m->lds_ftrain = (c.use_deep && ftrain_supported(F, D, H, NT, m->NC0, m->tailI, m->NG))
                         ? ftrain_lds_bytes(F, D, m->MT, m->S, m->SX, m->SY) : 0;
     if (m->lds_ftrain > 160 * 1024) m->lds_ftrain = 0;
-    // DFWFM_R32_LDS=<bytes>: reserve at least this much LDS per workgroup (> 80 KiB: one workgroup per CU, so two
-    // batches in flight on plain streams take disjoint halves of the chip; A/B against CU-masked streams)
-    if (const char* pad = getenv("DFWFM_R32_LDS"))
-      if (m->r32 && (size_t)atol(pad) > m->lds_r32 && atol(pad) <= 160 * 1024) m->lds_r32 = (size_t)atol(pad);
   }
-  // split forward (opt-in, DFWFM_SPLIT=1): the gather / shallow part and the MLP as two launches, each
-  // with its own roofline (HBM-bound gather, MFMA-bound MLP) for profiling.  Measured slower than the
-  // fused launch (50.4 vs 43.0 us per batch alone, 43.4 vs 35.5 with two batches in flight): under a
-  // co-resident MLP's weight stream the gather launch's dependent loads wait ~3x longer, and in the
-  // fused kernel that wait is hidden behind the other workgroup's MLP instead of serialised
-  const char* sp = getenv("DFWFM_SPLIT");
-  m->split = (c.use_deep && m->KS == 1 && sp && atoi(sp) != 0) ? 1 : 0;
+  // (the split forward -- gather / shallow part and MLP as two launches -- measured slower than the fused launch
+  // and was removed in round 6; dfwfm_forward_gather gives the gather its own launch for measurement)
   if (m->lds_bytes > 160 * 1024 || m->lds_inf > 160 * 1024) {
     free_model(m);
     return fail(DFWFM_ERR_UNSUPPORTED, "LDS tile of %zu bytes exceeds 160 KiB", m->lds_bytes);
@@ -523,14 +511,11 @@ void fill_forward_args(const dfwfm_model* m, FwdArgs& a, const int64_t* xi, int6
   a.flags = m->flags;
   // the MLP-free forward's FwFM form: U'E pieces (default; batch sets 2.34 vs 2.59 us per batch at 2000 steps, 2.85-2.90
   // vs 3.05 at 20, profiles/r05/r05l_*; a lone batch on eight waves 7.7 vs 7.3 us) or per-sample Gram tiles
-  // (DFWFM_P3_FWFM=gram, A/B) -- the same form for a batch set and a lone batch, so a set's logits stay bit-identical
+  // (the Gram form remains for MT > 3) -- the same form for a batch set and a lone batch, so a set's logits stay bit-identical
   // to each batch's own forward; pieces only while the U' fragments fit the eight-wave form's registers (MT <= 3)
-  if (!m->cfg.use_deep && m->MT <= 3) {
-    static const char* p3 = getenv("DFWFM_P3_FWFM");
-    if (!(p3 && !strcmp(p3, "gram"))) a.flags |= kP3Pieces;
-  }
+  if (!m->cfg.use_deep && m->MT <= 3) a.flags |= kP3Pieces;
   // the static K loop (fwd_kernel NS = 25) when every layer is 25 chunks deep and 25 tiles wide
-  a.ns = (m->NC0 == 25 && m->NT == 25 && !getenv("DFWFM_NO_STATIC_K")) ? 25 : 0;
+  a.ns = (m->NC0 == 25 && m->NT == 25) ? 25 : 0;
   memcpy(a.fw_list4, m->fw_list4, sizeof a.fw_list4);
   memcpy(a.fw_list8, m->fw_list8, sizeof a.fw_list8);
   memcpy(a.fw_off4, m->fw_off4, sizeof a.fw_off4);
@@ -554,7 +539,6 @@ int dw_plan(const dfwfm_model* m, int64_t batch, int* per_split, int64_t* splits
   if (cap) *cap = 0;
   if (ps == 0 || batch <= 0) return DFWFM_OK;
   int64_t sp = 256 / ps;
-  if (const char* ds = getenv("DFWFM_DW_SPLITS")) sp = atoi(ds);  // tuning only
   const int64_t max_splits = (batch + 127) / 128;
   if (sp > max_splits) sp = max_splits;
   if (sp < 1) sp = 1;
@@ -621,16 +605,14 @@ size_t split_ws_bytes(const dfwfm_model* m, int64_t batch) {
   return sizeof(float) * (split_e_floats(m, batch) + (size_t)batch);
 }
 
-// diagnostics only: with DFWFM_DIAG_STAMPS=<which> the launch records per-workgroup phase clocks
+// diagnostics only: with DFWFM_DIAG stamps=<which> the launch records per-workgroup phase clocks
 int diag_stamps_buffer(dfwfm_model* m, int64_t batch, int which, uint64_t** out) {
   *out = nullptr;
-  const char* stv = getenv("DFWFM_DIAG_STAMPS");
-  if (!stv || atoi(stv) != which) return DFWFM_OK;
+  if (diag_opt("stamps", 0) != which) return DFWFM_OK;
   const size_t grid = (size_t)((batch + kBM - 1) / kBM);
-  // DFWFM_DIAG_RING=R: R launches in a row (e.g. captured into graphs on several streams) each get
+  // DFWFM_DIAG ring=R: R launches in a row (e.g. captured into graphs on several streams) each get
   // their own slice, for a cross-launch timeline (tools/timeline.py)
-  const char* rv = getenv("DFWFM_DIAG_RING");
-  const size_t ring = rv && atoi(rv) > 1 ? (size_t)atoi(rv) : 1;
+  const size_t ring = diag_opt("ring", 1) > 1 ? (size_t)diag_opt("ring", 1) : 1;
   if (grid > m->stamps_cap || ring != m->stamps_ring) {
     if (m->d_stamps) (void)hipFree(m->d_stamps);
     m->d_stamps = nullptr;
@@ -697,17 +679,13 @@ int dfwfm_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const fl
   if (rc != DFWFM_OK || batch == 0) return rc;
   FwdArgs a;
   fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, out);
-  // diagnostics only (phase timing): DFWFM_DIAG_DROP_FLAGS clears flag bits, results become invalid
-  if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
-  // gather / shallow phases at raised wave priority (default; DFWFM_PRIO=0 turns it off): beside the other
-  // batch's MLP on the same CU they otherwise lose the issue arbitration -- 33.71 -> 33.38 us per batch
-  {
-    const char* pr = getenv("DFWFM_PRIO");
-    if (!pr || atoi(pr) != 0) a.flags |= kPrio;
-    if (const char* pe = getenv("DFWFM_PRIO_EPI"); !pe || atoi(pe) != 0) a.flags |= kPrioEpi;
-    if (const char* dt = getenv("DFWFM_DEFER_TAIL"); !dt || atoi(dt) != 0) a.flags |= kDeferTail;
-  }
-  // diagnostics only: DFWFM_DIAG_STAMPS=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
+  // diagnostics only (phase timing): DFWFM_DIAG drop_flags clears flag bits, results become invalid
+  a.flags &= ~diag_opt("drop_flags", 0);
+  // gather / shallow phases at raised wave priority: beside the other batch's MLP on the same CU they otherwise lose
+  // the issue arbitration -- 33.71 -> 33.38 us per batch; the fwd32 epilogue priority and the deferred split-tile
+  // barrier (set kernel only)
+  a.flags |= kPrio | kPrioEpi | kDeferTail;
+  // diagnostics only: DFWFM_DIAG stamps=1 records per-workgroup phase clocks (dfwfm_diag_stamps)
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
   const bool r32 = (a.flags & kHasDeep) && use_fwd32(m, batch, stream);
@@ -744,11 +722,9 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
     const int32_t n = nb - i0 < kMaxSet ? nb - i0 : kMaxSet;
     FwdArgs a;
     fill_forward_args(m, a, xi[i0], xi_stride, xv[i0], xv_stride, batch, out[i0]);
-    if (const char* pr = getenv("DFWFM_PRIO"); !pr || atoi(pr) != 0) a.flags |= kPrio;
-    // fwd32 schedule (default on; =0 for A/B): raised priority in the MLP epilogues, the split tile's barrier inside
-    // the next K loop -- 30.33 -> 30.08 us per batch at 2000 steps, 31.3 -> 31.05 on a 20-batch set (r03be)
-    if (const char* pe = getenv("DFWFM_PRIO_EPI"); !pe || atoi(pe) != 0) a.flags |= kPrioEpi;
-    if (const char* dt = getenv("DFWFM_DEFER_TAIL"); !dt || atoi(dt) != 0) a.flags |= kDeferTail;
+    // fwd32 schedule: raised priority in the MLP epilogues, the split tile's barrier inside the next K loop --
+    // 30.33 -> 30.08 us per batch at 2000 steps, 31.3 -> 31.05 on a 20-batch set (r03be)
+    a.flags |= kPrio | kPrioEpi | kDeferTail;
     a.tail = m->tailI;
     if (n > 1) {
       a.nb = n;
@@ -771,14 +747,14 @@ int dfwfm_forward_batches(dfwfm_model* m, int32_t nb, const int64_t* const* xi, 
 
 int dfwfm_forward_workspace_bytes(dfwfm_model* m, int64_t batch, size_t* bytes) {
   if (!m || !bytes || batch < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
-  *bytes = (m->split || m->sp) ? split_ws_bytes(m, batch) : 0;
+  *bytes = m->sp ? split_ws_bytes(m, batch) : 0;
   return DFWFM_OK;
 }
 
 int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
                      int64_t batch, float* out, void* workspace, size_t ws_bytes, void* stream) {
   if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
-  if ((!m->split && !m->sp) || !workspace) return dfwfm_forward(m, xi, xi_stride, xv, xv_stride, batch, out, stream);
+  if (!m->sp || !workspace) return dfwfm_forward(m, xi, xi_stride, xv, xv_stride, batch, out, stream);
   int rc = check_inputs(m, xi, xi_stride, xv, xv_stride, batch, out);
   if (rc != DFWFM_OK || batch == 0) return rc;
   if (ws_bytes < split_ws_bytes(m, batch))
@@ -787,13 +763,12 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
   if (reinterpret_cast<uintptr_t>(workspace) % 16) return fail(DFWFM_ERR_INVALID_ARG, "workspace not 16-byte aligned");
   FwdArgs a;
   fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, out);
-  if (const char* drop = getenv("DFWFM_DIAG_DROP_FLAGS")) a.flags &= ~atoi(drop);
   a.part_stride = m->NC0 * 16;
   a.part_e = static_cast<float*>(workspace);
   a.part_fs = a.part_e + split_e_floats(m, batch);
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
   a.tail = m->tailI;
-  if (m->sp) {
+  {
     // pruned deep tower: the gather launch, then the sparse MLP over the ELL (dfwfm_spmlp.hip)
     hipError_t e = launch_forward_gather(a, m->D, m->lds_gather, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gather launch");
@@ -821,10 +796,6 @@ int dfwfm_forward_ws(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const
     if (e != hipSuccess) return hip_fail(e, "sparse MLP launch");
     return DFWFM_OK;
   }
-  hipError_t e = launch_forward_split(a, m->D, m->TPWI > 0 ? m->TPWI : 1, m->NG, m->lds_gather, m->lds_inf,
-                                      (hipStream_t)stream);
-  if (e != hipSuccess) return hip_fail(e, "forward launch");
-  return DFWFM_OK;
 }
 
 int dfwfm_forward_gather(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, const float* xv, int64_t xv_stride,
@@ -836,13 +807,16 @@ int dfwfm_forward_gather(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, c
   if (!deep_emb || deep_emb_stride != (int64_t)m->NC0 * 16)
     return fail(DFWFM_ERR_INVALID_ARG, "deep_emb stride %lld, need %d", (long long)deep_emb_stride, m->NC0 * 16);
   if (reinterpret_cast<uintptr_t>(deep_emb) % 16) return fail(DFWFM_ERR_INVALID_ARG, "deep_emb not 16-byte aligned");
+  // the MLP-free forward's kernel (fwd_kernel PART 3: the serving copy, the U'E FwFM pieces) storing the E tile and
+  // first + second instead of the logit
   FwdArgs a;
   fill_forward_args(m, a, xi, xi_stride, xv, xv_stride, batch, nullptr);
+  a.flags &= ~kHasDeep;
+  if (m->MT <= 3) a.flags |= kP3Pieces;
   a.part_stride = m->NC0 * 16;
   a.part_e = deep_emb;
   a.part_fs = first_second;
-  a.tail = m->tailI;
-  hipError_t e = launch_forward_gather(a, m->D, m->lds_gather, (hipStream_t)stream);
+  hipError_t e = launch_forward(a, m->D, 1, 1, 8, m->lds_inf, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "gather launch");
   return DFWFM_OK;
 }
@@ -996,7 +970,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(DFWFM_ERR_INVALID_ARG, "dropout_p outside [0, 1)");
   if (m->H > 0 && m->N % 4 != 0)
     return fail(DFWFM_ERR_UNSUPPORTED, "training needs deep_nodes %% 4 == 0 (got %d)", m->N);
-  if (m->KS != 1) return fail(DFWFM_ERR_UNSUPPORTED, "training runs with DFWFM_KSPLIT=1 only");
+  if (m->KS != 1) return fail(DFWFM_ERR_UNSUPPORTED, "training runs with one K half per wave only");
   if (backward_lds_bytes(m->F, m->D, m->MT, m->S, m->SX, m->SY) > 160 * 1024)
     return fail(DFWFM_ERR_UNSUPPORTED, "backward LDS tile exceeds 160 KiB");
   if ((rc = ensure_workspace(m, batch)) != DFWFM_OK) return rc;
@@ -1026,13 +1000,12 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   a.seed = seed;
   a.seed_src = m->step_src;
   if ((rc = diag_stamps_buffer(m, batch, 1, &a.stamps)) != DFWFM_OK) return rc;
-  // the eight-wave layout when the model has it (DFWFM_NG=4 keeps the four-wave kernel)
+  // the eight-wave layout when the model has it (DFWFM_DIAG ng=4 keeps the four-wave kernel)
   a.tail = m->tailI;
-  // the helper-wave form when the model has it (DFWFM_FTRAIN=0: fwd_kernel<TRAIN>, bit-identical, for A/B and tests)
-  if (const char* dg = getenv("DFWFM_DIAG_FT"))  // diagnostics only (results invalid)
-    a.flags |= ((atoi(dg) & 1) ? kFtDiagHwId : 0) | ((atoi(dg) & 2) ? kFtDiagNoMlp : 0);
-  const char* ft = getenv("DFWFM_FTRAIN");
-  const bool helpers = m->lds_ftrain > 0 && !(ft && atoi(ft) == 0);
+  // the helper-wave form when the model has it (DFWFM_DIAG ftrain=0: fwd_kernel<TRAIN>, bit-identical, tests)
+  const int dg = diag_opt("ft", 0);  // diagnostics only (results invalid)
+  a.flags |= ((dg & 1) ? kFtDiagHwId : 0) | ((dg & 2) ? kFtDiagNoMlp : 0);
+  const bool helpers = m->lds_ftrain > 0 && diag_opt("ftrain", 1) != 0;
   hipError_t e = helpers ? launch_ftrain(a, m->D, m->lds_ftrain, (hipStream_t)stream)
                          : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, 1, m->NG, m->lds_inf, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
@@ -1106,15 +1079,14 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     a.SY = m->SY;
     a.W0 = m->W0;
     a.flags = m->flags | (drop ? kDrop : 0);
-    // diagnostics only (backward phase costs): DFWFM_DIAG_BWD ORs in kDiagBwd* bits, results invalid
-    if (const char* db = getenv("DFWFM_DIAG_BWD")) a.flags |= atoi(db) << 20;
+    // diagnostics only (backward phase costs): DFWFM_DIAG bwd= ORs in kDiagBwd* bits, results invalid
+    a.flags |= diag_opt("bwd", 0) << 20;
     a.drop_p = m->t_drop;
     a.drop_scale = 1.f / (1.f - m->t_drop);
     a.seed = m->t_seed;
     a.seed_src = m->step_src;
-    // the dense shallow reductions ride along (reduce_kernel's re-read of E / fo / X_H / dE is skipped;
-    // DFWFM_NO_FUSED_RED=1 keeps the separate kernel, for A/B)
-    if (!getenv("DFWFM_NO_FUSED_RED")) {
+    // the dense shallow reductions ride along (reduce_kernel's re-read of E / fo / X_H / dE is skipped)
+    {
       a.part = m->red_part;
       a.sv_fo = m->sv_fo;
       a.xv = m->t_xv;
@@ -1125,14 +1097,13 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
               (H > 0 && g->fc_w ? kRedFc : 0) | kRedNum2 | kRedNum1;
       fused_red = true;
     }
-    // diagnostics only: DFWFM_DIAG_STAMPS=2 records the backward's phase clocks instead of the forward's
+    // diagnostics only: DFWFM_DIAG stamps=2 records the backward's phase clocks instead of the forward's
     int src = diag_stamps_buffer(m, batch, 2, &a.stamps);
     if (src != DFWFM_OK) return src;
     const size_t lds = backward_lds_bytes(F, D, m->MT, m->S, m->SX, m->SY);
-    // eight waves (the 8*TPW+1-th tile split by K, like the forward) unless DFWFM_NG=4
-    const char* ngs = getenv("DFWFM_NG");
+    // eight waves (the 8*TPW+1-th tile split by K, like the forward) unless DFWFM_DIAG ng=4
     const int NT = m->NT;
-    const bool ng8 = H > 0 && NT <= 32 && !(ngs && atoi(ngs) == 4);
+    const bool ng8 = H > 0 && NT <= 32 && diag_opt("ng", 8) != 4;
     const int tpw = ng8 ? (NT % 8 == 1 && NT >= 9 ? NT / 8 : (NT + 7) / 8) : (m->TPW > 0 ? m->TPW : 1);
     e = launch_backward(a, D, tpw > 0 ? tpw : 1, ng8 ? 8 : 4, lds, s);
     if (e != hipSuccess) return hip_fail(e, "backward launch");
@@ -1142,7 +1113,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
   }
 
   // 2. dense shallow reductions: per 16-row tile, then summed over tiles.  When this call also runs the
-  // weight-gradient GEMM, the final sums ride in its launch (launch_dw_reduce; DFWFM_NO_DW_RED=1: separate, A/B)
+  // weight-gradient GEMM, the final sums ride in its launch (launch_dw_reduce)
   RedArgs r;
   bool red_pending = false;
   if (phases & DFWFM_BWD_REDUCE) {
@@ -1173,8 +1144,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     r.MT = m->MT;
     r.flags = m->flags;
     r.loss_sum = fused_red ? m->bwd_loss_sum : nullptr;
-    red_pending = fused_red && (phases & DFWFM_BWD_MLP_WEIGHTS) && H > 0 && (g->lin_w || g->lin_b) &&
-                  !getenv("DFWFM_NO_DW_RED");
+    red_pending = fused_red && (phases & DFWFM_BWD_MLP_WEIGHTS) && H > 0 && (g->lin_w || g->lin_b);
     if (!red_pending) {
       e = fused_red ? launch_reduce_final(r, s) : launch_reduce(r, s);
       if (e != hipSuccess) return hip_fail(e, "reduce launch");
@@ -1183,9 +1153,8 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
 
   // 3. categorical tables: the atomic scatter (privatised LDS tasks for small tables, global atomics for large ones;
   // sums in arrival order) unless deterministic mode, which runs the sorted per-row-owner scatter (one task per field
-  // and row kind, both table families); DFWFM_SCATTER=atomic / sorted forces either (A/B)
-  const char* sc_env = getenv("DFWFM_SCATTER");
-  const bool atomic_scatter = sc_env ? strcmp(sc_env, "sorted") != 0 : !m->deterministic;
+  // and row kind, both table families)
+  const bool atomic_scatter = !m->deterministic;
   if ((phases & DFWFM_BWD_SCATTER) && g->fields && !atomic_scatter) {
     SortScatterArgs sa;
     memset(&sa, 0, sizeof sa);
@@ -1200,7 +1169,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     sa.sv_de = m->sv_de;
     sa.dlogit = dlogit;
     sa.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
-    if (const char* dg = getenv("DFWFM_SCATTER_DIAG")) sa.diag = atoi(dg);  // diagnostics only: results invalid
+    sa.diag = diag_opt("scatter", 0);  // diagnostics only: results invalid
     const bool need2 = (m->flags & kNeedE) != 0, need1 = (m->flags & kFoTables) != 0;
     auto add = [&](float* g2, float* g1, const float* o2, const float* o1, int64_t c, int f, int kind,
                    int64_t rows) -> int {
@@ -1293,9 +1262,8 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       if (rows > 0x7fffffff) return fail(DFWFM_ERR_UNSUPPORTED, "field %d: table of more than 2^31 rows", f);
       const int w = src == 0 ? D : 1;
       // tables up to kPrivRows rows (and kPrivFloats of LDS) accumulate privately; bigger ones spread
-      // their atomics well enough (DFWFM_PRIV_ROWS: tuning only)
-      static const int64_t priv_rows = getenv("DFWFM_PRIV_ROWS") ? atoll(getenv("DFWFM_PRIV_ROWS")) : kPrivRows;
-      const bool is_priv = rows * (w + 1) <= kPrivFloats && rows <= priv_rows;
+      // their atomics well enough (64 / 512 / 2000 rows measured slower)
+      const bool is_priv = rows * (w + 1) <= kPrivFloats && rows <= kPrivRows;
       if (np + na == kScatterList || (int64_t)(np + na + 1) * nb > 0x7fffffff) {
         int rc = flush();
         if (rc != DFWFM_OK) return rc;
@@ -1365,8 +1333,7 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       if (rc != DFWFM_OK) return rc;
       // the slices are used only by the deterministic split-K sum; the float-atomic form never reads them
       if (m->deterministic && splits > 1 && (int64_t)per_split * splits > m->dw_slices)
-        return fail(DFWFM_ERR_STATE, "weight-gradient split slices: %lld needed, %lld allocated (DFWFM_DW_SPLITS "
-                    "changed after the workspace was sized?)", (long long)per_split * splits, (long long)m->dw_slices);
+        return fail(DFWFM_ERR_STATE, "weight-gradient split slices: %lld needed, %lld allocated", (long long)per_split * splits, (long long)m->dw_slices);
       d.splits = (int32_t)splits;
       d.rows_per_split = rows;
       d.part = m->deterministic ? m->dw_part : nullptr;  // split slices (deterministic) or float atomics
@@ -1689,7 +1656,7 @@ int dfwfm_eval_metrics(const float* z, const float* y, int64_t n, double* out, v
 
 int dfwfm_diag_stamps(dfwfm_model* m, uint64_t* host, int64_t n, void* stream) {
   if (!m || !host || n < 0) return fail(DFWFM_ERR_INVALID_ARG, "null argument");
-  if (!m->d_stamps) return fail(DFWFM_ERR_STATE, "no stamps recorded (set DFWFM_DIAG_STAMPS=1)");
+  if (!m->d_stamps) return fail(DFWFM_ERR_STATE, "no stamps recorded (set DFWFM_DIAG=stamps=1)");
   const size_t cap = m->stamps_cap * kStampSlots * (m->stamps_ring ? m->stamps_ring : 1);
   const size_t cnt = (size_t)n < cap ? (size_t)n : cap;
   HIP_TRY(hipMemcpyAsync(host, m->d_stamps, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, (hipStream_t)stream));

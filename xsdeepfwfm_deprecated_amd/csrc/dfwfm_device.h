@@ -11,7 +11,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float relu_keep_nan(float v) { return v < 0.f ? 0.f : v; }
 
-// Diagnostic phase stamps (p.stamps != nullptr only in DFWFM_DIAG_STAMPS runs; in production the
+// Diagnostic phase stamps (p.stamps != nullptr only in DFWFM_DIAG stamps= runs; in production the
 // branch is never taken): wave 0 lane 0 records the shader clock at phase boundaries.
 __device__ __forceinline__ void stamp(uint64_t* st, int slot, int tid) {
   if (st != nullptr && tid == 0) st[(size_t)blockIdx.x * kStampSlots + slot] = __builtin_amdgcn_s_memtime();

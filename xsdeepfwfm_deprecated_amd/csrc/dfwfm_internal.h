@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include <mutex>
 #include <unordered_map>
@@ -26,17 +28,17 @@ constexpr int kFoLw = 16;      // project first order with fm_1st.weight
 constexpr int kNeedE = 32;     // second-order / deep embeddings are gathered
 constexpr int kTrain = 64;     // save the activations the backward needs (FwdArgs::sv_*)
 constexpr int kDrop = 128;     // dropout on the deep tower (train only)
-constexpr int kPrio = 256;     // raise the wave priority for the phases before the MLP (A/B: DFWFM_PRIO)
+constexpr int kPrio = 256;     // raise the wave priority for the phases before the MLP (always on)
 constexpr int kHasQR = 512;    // some field is a QR embedding (set by set_tables)
-constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (default; A/B: DFWFM_PRIO_EPI=0)
-constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (default; A/B: DFWFM_DEFER_TAIL=0)
+constexpr int kPrioEpi = 2048; // fwd32: raise the wave priority in the MLP epilogues too (set kernel)
+constexpr int kDeferTail = 4096; // fwd32: the split tile's barrier moved into the next K loop (set kernel)
 constexpr int kPairs = 1024;   // FwFM over the nonzero pairs of a pruned R (build_fwfm_pairs; MLP-free forward)
 constexpr int kP3Pieces = 8192; // MLP-free forward: FwFM as U' E pieces (11.25 MFMAs per sample) instead of per-sample
-                                // Gram tiles (18); DFWFM_P3_FWFM=gram|pieces
-// bwd_kernel diagnostics / A/B (DFWFM_DIAG_BWD=<bits> sets them << 20; off the flag range the model itself uses):
+                                // Gram tiles (18); set when MT <= 3
+// bwd_kernel diagnostics / A/B (DFWFM_DIAG bwd=<bits> sets them << 20; off the flag range the model itself uses):
 // no G_l stores (results invalid), no mask loads (results invalid), the generic K loop instead of the static form
 constexpr int kBwdNoGStore = 1 << 20, kBwdNoMask = 1 << 21, kBwdGeneric = 1 << 22;
-// ftrain_kernel diagnostics (DFWFM_DIAG_FT=<bits> sets them << 23, results invalid): each wave's HW_ID into the stamp
+// ftrain_kernel diagnostics (DFWFM_DIAG ft=<bits> sets them << 23, results invalid): each wave's HW_ID into the stamp
 // slots instead of clocks; the MLP waves skip their K loops
 constexpr int kFtDiagHwId = 1 << 23, kFtDiagNoMlp = 1 << 24;
 constexpr int kMaxH = 16;      // hidden layers
@@ -96,7 +98,7 @@ struct FwdArgs {
   float drop_scale;         // 1 / (1 - p)
   uint32_t seed;            // dropout hash seed of this step
   const int64_t* seed_src;  // device step counter mixed into the seed (graph replay), or null
-  // split forward (launch_forward_split): the gather launch writes, the MLP launch reads
+  // gather launch (PART 1; the sparse deep tower reads them) or dfwfm_forward_gather (PART 3)
   float* part_e;            // [B][part_stride] E tile rows (W0 columns, zero padded past F*D)
   float* part_fs;           // [B] first + second order
   int32_t part_stride;      // floats per row (W0, a multiple of 4)
@@ -120,6 +122,22 @@ struct FwdArgs {
 inline unsigned fwd_grid(const FwdArgs& a, int rows) {
   const unsigned tiles = (unsigned)((a.batch + rows - 1) / rows);
   return a.nb > 1 ? (unsigned)a.nb * tiles : tiles;
+}
+
+// Test and diagnostics options, all in ONE environment variable: DFWFM_DIAG="key=value,key=value", read where
+// they apply (product runs set none).  Keys: r32 (0 never / 1 always the 32-sample set kernel), ng (4: four-wave
+// forward / backward), ftrain (0: fwd_kernel<TRAIN> instead of the helper-wave training forward), part3 (0: the
+// generic kernel for MLP-free models), p3ng (4 / 8: MLP-free waves), stamps / ring / ft / bwd / scatter /
+// drop_flags (phase stamps and phase-skip bits; results invalid).  dflt when the key is absent.
+inline int diag_opt(const char* key, int dflt) {
+  const char* s = getenv("DFWFM_DIAG");
+  const size_t kl = strlen(key);
+  while (s && *s) {
+    if (!strncmp(s, key, kl) && s[kl] == '=') return atoi(s + kl + 1);
+    s = strchr(s, ',');
+    if (s) ++s;
+  }
+  return dflt;
 }
 
 // LDS carve-up, in floats; every region starts 16-byte aligned.
@@ -183,7 +201,7 @@ struct BwdArgs {
   float drop_p, drop_scale;
   uint32_t seed;
   const int64_t* seed_src;       // as FwdArgs::seed_src
-  uint64_t* stamps;              // diagnostics only (DFWFM_DIAG_STAMPS=2): phase clocks per workgroup
+  uint64_t* stamps;              // diagnostics only (DFWFM_DIAG stamps=2): phase clocks per workgroup
   // the dense shallow reductions fused in (red != 0): the tile's partial sums to part[blockIdx.x] in
   // reduce_kernel's layout (red_outputs), from the E / X_H / dE tiles already in LDS; reduce_final_kernel
   // adds them.  red: kRed* bits of the gradients wanted
@@ -291,7 +309,7 @@ struct SortScatterArgs {
   const float* sv_de;
   const float* dlogit;
   const float* lw;      // [F] or null (dfo = dlogit)
-  int32_t diag;         // diagnostics only (DFWFM_SCATTER_DIAG): 1 skip the sort, 2 skip the sums, 4 no row adds
+  int32_t diag;         // diagnostics only (DFWFM_DIAG scatter=): 1 skip the sort, 2 skip the sums, 4 no row adds
 };
 size_t sort_scatter_lds_bytes(int D);
 
@@ -460,8 +478,7 @@ struct PackTabList {
   int32_t nf, D, pkw;
 };
 hipError_t launch_pack_tables(const PackTabList& L, hipStream_t s);
-hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s);
-// the split forward's first launch alone (gather + shallow part -> a.part_e / a.part_fs)
+// the gather + shallow part alone (-> a.part_e / a.part_fs): the sparse deep tower's first launch
 hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream_t s);
 hipError_t launch_pack_list(const PackList& L, int total_blocks, hipStream_t s);
 // the fused inference forward on 32-sample workgroups (dfwfm_fwd32.hip): both 16-row tiles per wave in the MLP;
@@ -480,7 +497,6 @@ hipError_t launch_ftrain(const FwdArgs& a, int D, size_t lds, hipStream_t s);
 #define DFWFM_PER_D(name) DFWFM_PER_D_CAT(name, DFWFM_KD)
 #define DFWFM_DECL_PER_D(D)                                                                                   \
   hipError_t launch_forward_d##D(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s);        \
-  hipError_t launch_forward_split_d##D(const FwdArgs& a, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s); \
   hipError_t launch_forward_gather_d##D(const FwdArgs& a, size_t lds1, hipStream_t s);                      \
   hipError_t launch_backward_d##D(const BwdArgs& a, int tpw, int ng, size_t lds, hipStream_t s);
 DFWFM_DECL_PER_D(4)

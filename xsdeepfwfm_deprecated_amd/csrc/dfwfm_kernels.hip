@@ -59,9 +59,10 @@ namespace dfwfm {
                          // per CU (LDS 30.7 KB each at Criteo-39)
 #endif
 // PART: 0 = the whole forward in one launch; 1 = stage, gather and shallow part only, E tile and
-// first + second to p.part_e / p.part_fs; 2 = MLP and combine from p.part_e / p.part_fs (the split
-// forward: two launches per batch, see launch_forward_split); 3 = a model without deep tower (no MLP
-// code, trimmed LDS, FwFM fragments read from global memory: 70 registers on eight waves)
+// first + second to p.part_e / p.part_fs (the sparse deep tower's first launch); 3 = a model without deep tower
+// (no MLP code, trimmed LDS, FwFM fragments read from global memory: 70 registers on eight waves; with
+// p.part_e set, dfwfm_forward_gather: E tile and first + second out instead of the logit).  (PART 2, the MLP
+// half of the split forward, was removed in round 6 with that forward.)
 // NG: MLP output-tile groups = waves (4: one wave per SIMD, <= 256 registers; 8: two per SIMD, <= 128
 // registers, so one workgroup issues MFMAs from two waves per SIMD while a second batch's workgroup
 // on the same CU runs its gather; the training variant, one batch in flight, keeps 256 registers)
@@ -139,43 +140,7 @@ fwd_kernel(FwdArgs p) {
   const int SE = r4(FD);  // row stride of the saved E / X_0 tiles
   const int nrows = (int)((p.batch - b0) < kBM ? (p.batch - b0) : kBM);
   const bool drop0 = train && deep && (flags & kDrop) != 0;
-  if constexpr (PART == 2) {
-    // ---- the E tile and first + second of the gather launch; layer-0 weights behind them ----------
-    constexpr int kEPT = (kBM * 128 + NTH - 1) / NTH;  // float4 of the tile per thread (<= 512 columns)
-    const int PS4 = p.part_stride >> 2;
-    const int n4 = kBM * PS4;
-    f32x4 ev[kEPT];
-#pragma unroll
-    for (int k = 0; k < kEPT; ++k) {
-      const int i = tid + k * NTH;
-      const int b = i / PS4;
-      ev[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (i < n4 && b < nrows) ev[k] = reinterpret_cast<const f32x4*>(p.part_e + (b0 + b) * p.part_stride)[i - b * PS4];
-    }
-    const float fsv = tid < nrows ? p.part_fs[b0 + tid] : 0.f;
-    ls.init(wrsrc, 0, p.NC0, p.NT, g, kh);
-    DFWFM_PRELOAD(ls);
-    if constexpr (NSK == 0) {
-      if (tail) {
-        ts.init(0, p.NC0, TT, g);
-        ts.load(wrsrc, tw, lane * 16);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kEPT; ++k) {
-      const int i = tid + k * NTH;
-      const int b = i / PS4;
-      if (i < n4) reinterpret_cast<f32x4*>(bufX + b * SX)[i - b * PS4] = ev[k];
-    }
-    for (int i = tid + kEPT * NTH; i < n4; i += NTH) {  // rows wider than 512 columns
-      const int b = i / PS4;
-      reinterpret_cast<float4*>(bufX + b * SX)[i - b * PS4] =
-          b < nrows ? reinterpret_cast<const float4*>(p.part_e + (b0 + b) * p.part_stride)[i - b * PS4]
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (tid < kBM) fs[tid] = fsv;
-    __syncthreads();
-  } else {
+  {
   // ---- phase 0: field descriptors -> LDS; this thread's Xi / Xv; shallow parameters in flight --
   // Every load is issued before any is consumed (a load-then-store loop waits one round trip per
   // iteration).  Only the descriptors and the tile's Xi / Xv gate the gather; the FwFM fragments,
@@ -425,9 +390,11 @@ fwd_kernel(FwdArgs p) {
   }
   __syncthreads();
   stamp(p.stamps, 2, tid);
-  if constexpr (PART == 1) {
-    // the E tile (W0 columns, zero padded past F*D) for the MLP launch, behind the shallow part
-    store_tile(p.part_e + b0 * p.part_stride, p.part_stride, bufX, SX, nrows, p.part_stride >> 2, tid, NTH);
+  if constexpr (PART == 1 || PART == 3) {
+    // the E tile (W0 columns, zero padded past F*D) for the MLP launch, behind the shallow part (PART 3: only for
+    // dfwfm_forward_gather, the deep model's gather half as the MLP-free kernel)
+    if (PART == 1 || p.part_e)
+      store_tile(p.part_e + b0 * p.part_stride, p.part_stride, bufX, SX, nrows, p.part_stride >> 2, tid, NTH);
   }
   if constexpr (train) {
     // E for the shallow backward.  Without deep-tower dropout E is also X_0 and is saved after
@@ -694,7 +661,7 @@ fwd_kernel(FwdArgs p) {
 
   if (!deep) {
     __syncthreads();
-    if constexpr (PART == 1) {
+    if (PART == 1 || (PART == 3 && p.part_fs)) {
       if (tid < kBM && b0 + tid < p.batch) p.part_fs[b0 + tid] = fs[tid];
     } else {
       if (tid < kBM && b0 + tid < p.batch) tr.out[b0 + tid] = fs[tid] + p.bias[0];
@@ -703,7 +670,7 @@ fwd_kernel(FwdArgs p) {
     stamp_end_rt(p.stamps, tid);
     return;
   }
-  }  // PART != 2
+  }
 
   stamp(p.stamps, 3, tid);
   if (flags & kPrio) __builtin_amdgcn_s_setprio(0);
@@ -1034,19 +1001,19 @@ static hipError_t launch_fwd_8(const FwdArgs& a, int tpw, size_t lds, hipStream_
 template <int D>
 static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
   // no deep tower: the MLP-free instantiation on eight waves (105 registers, no scratch): 4.92 us per batch
-  // at three batches in flight against 5.19 for the generic four-wave one (DFWFM_NO_PART3=1) and 6.0 for a
+  // at three batches in flight against 5.19 for the generic four-wave one (DFWFM_DIAG part3=0) and 6.0 for a
   // four-wave MLP-free one (128 registers + spills)
-  if (!(a.flags & (kHasDeep | kTrain)) && !getenv("DFWFM_NO_PART3")) {
+  if (!(a.flags & (kHasDeep | kTrain)) && diag_opt("part3", 1) != 0) {
     // one instantiation per FwFM row-tile count (NS = MT): the Gram tiles' registers sized to the model.  Eight
-    // waves (70 registers, three workgroups per CU: 3.55 us per batch at three batches in flight); DFWFM_P3_NG=4
-    // selects four waves without QR operands (94 registers, five workgroups per CU by the trimmed LDS: 3.74 us
-    // at three or six in flight, profiles/r02/r02r_*); a model with a QR field always takes eight (four would
-    // spill the QR rows' second operands)
-    const char* png = getenv("DFWFM_P3_NG");
+    // waves (70 registers, three workgroups per CU: 3.55 us per batch at three batches in flight); four waves without
+    // QR operands (94 registers, five workgroups per CU by the trimmed LDS: 3.74 us at three or six in flight,
+    // profiles/r02/r02r_*); a model with a QR field always takes eight (four would spill the QR rows' second
+    // operands).  DFWFM_DIAG p3ng=4 / 8 forces either (tests)
+    const int png = diag_opt("p3ng", 0);
     const bool qr = (a.flags & kHasQR) != 0;
     // batch sets (a.nb > 1): four waves -- with the CU slots refilled across batch boundaries, five four-wave
     // workgroups per CU beat three eight-wave ones (2.52 vs 2.92 us per batch, profiles/r03/r03be_*)
-    const bool w8 = qr || (png ? atoi(png) != 4 : a.nb <= 1);
+    const bool w8 = qr || (png ? png != 4 : a.nb <= 1);
     auto pick = [&](auto ng_, auto qr_) {
       constexpr int NG = decltype(ng_)::value;
       constexpr bool Q = decltype(qr_)::value;
@@ -1069,32 +1036,7 @@ static hipError_t launch_fwd_d(const FwdArgs& a, int tpw, int ks, int ng, size_t
   }
   if (a.flags & kTrain) return ng == 8 ? launch_fwd_8<D, 0, true>(a, tpw, lds, s) : launch_fwd_k<D, 1, true>(a, tpw, lds, s);
   if (ng == 8) return launch_fwd_8<D, 0>(a, tpw, lds, s);
-  return ks == 2 ? launch_fwd_k<D, 2, false>(a, tpw, lds, s) : launch_fwd_k<D, 1, false>(a, tpw, lds, s);
-}
-
-// the split forward: gather launch (PART 1; no MLP, so one instantiation per D) then MLP launch
-// (PART 2) on the same stream
-template <int D, int TPW>
-static hipError_t launch_mlp4(const FwdArgs& a, size_t lds2, hipStream_t s) {
-  return launch_fwd_t<D, TPW, 1, false, 2, 4>(a, lds2, s);
-}
-
-template <int D>
-static hipError_t launch_split_d(const FwdArgs& a, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s) {
-  hipError_t e = launch_fwd_t<D, 1, 1, false, 1, 4>(a, lds1, s);
-  if (e != hipSuccess) return e;
-  if (ng == 8) return launch_fwd_8<D, 2>(a, tpw, lds2, s);
-  switch (tpw) {
-    case 1: return launch_mlp4<D, 1>(a, lds2, s);
-    case 2: return launch_mlp4<D, 2>(a, lds2, s);
-    case 3: return launch_mlp4<D, 3>(a, lds2, s);
-    case 4: return launch_mlp4<D, 4>(a, lds2, s);
-    case 5: return launch_mlp4<D, 5>(a, lds2, s);
-    case 6: return launch_mlp4<D, 6>(a, lds2, s);
-    case 7: return launch_mlp4<D, 7>(a, lds2, s);
-    case 8: return launch_mlp4<D, 8>(a, lds2, s);
-    default: return hipErrorInvalidValue;
-  }
+  return launch_fwd_k<D, 1, false>(a, tpw, lds, s);  // (one K half per wave: the K split was removed in round 6)
 }
 
 #ifdef DFWFM_KD
@@ -1102,25 +1044,10 @@ static hipError_t launch_split_d(const FwdArgs& a, int tpw, int ng, size_t lds1,
 hipError_t DFWFM_PER_D(launch_forward_d)(const FwdArgs& a, int tpw, int ks, int ng, size_t lds, hipStream_t s) {
   return launch_fwd_d<DFWFM_KD>(a, tpw, ks, ng, lds, s);
 }
-hipError_t DFWFM_PER_D(launch_forward_split_d)(const FwdArgs& a, int tpw, int ng, size_t lds1, size_t lds2,
-                                               hipStream_t s) {
-  return launch_split_d<DFWFM_KD>(a, tpw, ng, lds1, lds2, s);
-}
 hipError_t DFWFM_PER_D(launch_forward_gather_d)(const FwdArgs& a, size_t lds1, hipStream_t s) {
   return launch_fwd_t<DFWFM_KD, 1, 1, false, 1, 4>(a, lds1, s);
 }
 #else
-hipError_t launch_forward_split(const FwdArgs& a, int D, int tpw, int ng, size_t lds1, size_t lds2, hipStream_t s) {
-  switch (D) {
-    case 4: return launch_forward_split_d4(a, tpw, ng, lds1, lds2, s);
-    case 8: return launch_forward_split_d8(a, tpw, ng, lds1, lds2, s);
-    case 10: return launch_forward_split_d10(a, tpw, ng, lds1, lds2, s);
-    case 16: return launch_forward_split_d16(a, tpw, ng, lds1, lds2, s);
-    case 32: return launch_forward_split_d32(a, tpw, ng, lds1, lds2, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
 hipError_t launch_forward_gather(const FwdArgs& a, int D, size_t lds1, hipStream_t s) {
   switch (D) {
     case 4: return launch_forward_gather_d4(a, lds1, s);

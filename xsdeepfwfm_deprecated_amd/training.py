@@ -162,8 +162,6 @@ def check_exchange(world, nbytes, fams, max_bytes=None):
     return total
 
 
-# DFWFM_TRAIN_FORK: the one-process step's graph layout
-_FORKS = frozenset(("none", "reduce", "spread", "tiles"))
 
 
 class FusedTrainStep:
@@ -234,18 +232,11 @@ class FusedTrainStep:
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
         self.state = torch.zeros(_lib.ADAM_STATE_BYTES // 8, dtype=torch.int64, device=dev)
-        # under data parallelism and in the forked layouts Adam runs as two launches -- everything but the MLP
+        # under data parallelism Adam runs as two launches -- everything but the MLP
         # (state), the MLP weights and biases (state_b) -- so that the first can overlap the weight-gradient GEMM;
         # each state's step counter is bumped once per step, so both hold the same step and bias corrections.  The
         # one-stream step (default on one process) runs one launch over every tensor on `state`
         self.state_b = torch.zeros_like(self.state)
-        # one process: the step's graph layout (A/B only, read once per instance): none = one stream, the whole
-        # Adam as one launch (default); reduce / spread / tiles = the graph forks after the backward's reductions /
-        # after the scatter / right after the per-tile backward, the weight-gradient GEMM and the MLP's Adam on a
-        # side stream
-        self.fork = os.environ.get("DFWFM_TRAIN_FORK", "none")
-        if self.fork not in _FORKS:
-            raise ValueError(f"DFWFM_TRAIN_FORK={self.fork!r}: expected one of {sorted(_FORKS)}")
         views = {}
         adam = (_lib.dfwfm_adam_tensor * len(params))()
         for i, p in enumerate(params):
@@ -437,7 +428,7 @@ class FusedTrainStep:
                        "dfwfm_adam_step_dev")
 
     def _part2(self):
-        if self.dist is None and self.fork == "none":
+        if self.dist is None:
             self._adam_all()  # one counter (`state`) for every step of this instance, graph-replayed or not
             return
         self._adam_main()
@@ -529,36 +520,16 @@ class FusedTrainStep:
         g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         ga = None
         if self.dist is None and self.n_adam > self.n_main:
-            # one process, default: ONE stream -- fill, re-pack, forward, loss gradient, backward, reductions,
-            # scatter, weight-gradient GEMM, one Adam launch.  The forked layouts (the GEMM and the MLP's Adam on a
-            # side stream beside the reductions / scatter / main Adam) measured level with it (0.302-0.307 ms,
-            # profiles/r04/r04h_tr-*.log) at 160-230 us of host enqueue per step against 17-29 us: with the
-            # GEMM's 225 workgroups resident, whatever ran beside it (reductions, scatter, Adam) was starved of CU
-            # slots and stretched by about what the overlap saved
-            fork = self.fork
-            if fork == "none":
-                with torch.cuda.stream(s):
-                    with torch.cuda.graph(g1, stream=s):
-                        self._part1(self.B, denom)
-                        self._part2()
-                torch.cuda.current_stream(self.dev).wait_stream(s)
-                return g1, None, None, None, None
-            late = fork == "spread"
-            first = fork == "reduce"
-            s1 = torch.cuda.Stream(self.dev)
+            # one process: ONE stream -- fill, re-pack, forward, loss gradient, backward, reductions, scatter,
+            # weight-gradient GEMM, one Adam launch.  The forked layouts (the GEMM and the MLP's Adam on a side stream
+            # beside the reductions / scatter / main Adam) measured level with it (0.302-0.307 ms,
+            # profiles/r04/r04h_tr-*.log) at 160-230 us of host enqueue per step against 17-29 us: with the GEMM's 225
+            # workgroups resident, whatever ran beside it was starved of CU slots and stretched by about what the
+            # overlap saved; removed in round 6
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g1, stream=s):
-                    self._part1(self.B, denom, phases=_lib.BWD_TABLES if late else _lib.BWD_TILES)
-                    if first:
-                        self._backward_phase(_lib.BWD_REDUCE)
-                    s1.wait_stream(s)
-                    with torch.cuda.stream(s1):
-                        self._part1b()
-                        self._adam_mlp()
-                    if not late:
-                        self._backward_phase(_lib.BWD_SCATTER if first else _lib.BWD_SPREAD)
-                    self._adam_main()
-                    s.wait_stream(s1)
+                    self._part1(self.B, denom)
+                    self._part2()
             torch.cuda.current_stream(self.dev).wait_stream(s)
             return g1, None, None, None, None
         if self._comm_in_graph():
@@ -696,12 +667,12 @@ class FusedTrainStep:
         input buffers), captured as ONE graph of len(batches) steps: the same kernels and the same results as
         calling step() on each in turn (the dropout seed and Adam's step count come from the device counter every
         step bumps), without the ~9 us of idle between two graph replays.  One process, one-stream step only;
-        otherwise (data parallelism, a forked layout, the first step, a batch that is not full or not readable in
+        otherwise (data parallelism, the first step, a batch that is not full or not readable in
         place, or resident_inputs=False: each new set of input pointers would be a K-step capture) it runs step()
         per batch.  Returns the running loss sum like step()."""
         direct = [self._direct_inputs(xi, xv, y, int(xi.shape[0])) for xi, xv, y in batches] \
             if self.resident_inputs else [None]
-        if (not batches or not self.use_graph or self.dist is not None or self.fork != "none" or self.steps < 1
+        if (not batches or not self.use_graph or self.dist is not None or self.steps < 1
                 or any(int(xi.shape[0]) != self.B for xi, _, _ in batches) or any(d is None for d in direct)):
             for xi, xv, y in batches:
                 loss = self.step(xi, xv, y)
