@@ -566,7 +566,8 @@ def main():
     if a.config == "pruned" and sparse_on:
         kname = "dfwfm::fwd_kernel<10,1,1,false,1,4> + dfwfm::sparse_mlp_kernel<64>"
         mfma_bound = "valu"  # the sparse MLP runs on the f32 vector FMAs (same 157.3 TF/s peak on gfx950)
-    workload_id = f"{a.config}/{a.first_order}/scale{K}/{a.inputs}" + ("/set" if M > 1 else "")
+    workload_id = f"{a.config}/{a.first_order}/scale{K}/{a.inputs}" + ("/set" if M > 1 else "") + \
+        ("/packed" if getattr(eng, "_packed_on", False) else "")
     traffic = pmc_traffic(kname, workload_id, units // BATCH)
 
     result = {

@@ -30,7 +30,9 @@
 extern "C" {
 #endif
 
-#define DFWFM_ABI_VERSION 3  /* 3: dfwfm_sparse_grads removed, dfwfm_model_set_dense_zero / dfwfm_backward_phases_bce added */
+#define DFWFM_ABI_VERSION 4  /* 4: dfwfm_model_pack_tables / dfwfm_forward_gather added, the split forward of
+                                dfwfm_forward_ws removed (its workspace now serves the sparse tower only); 3:
+                                dfwfm_sparse_grads removed, dfwfm_model_set_dense_zero / dfwfm_backward_phases_bce added */
 
 typedef enum {
   DFWFM_OK = 0,

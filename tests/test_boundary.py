@@ -45,7 +45,7 @@ def test_library_exports_every_header_symbol(built):
 
 def test_abi_version_and_error_string(built):
     L = built.lib()
-    assert L.dfwfm_abi_version() == 3
+    assert L.dfwfm_abi_version() == 4
     assert isinstance(L.dfwfm_last_error(), bytes)
     # invalid arguments are reported, never abort (no HIP call is reached)
     assert L.dfwfm_model_create(None, None) == -1

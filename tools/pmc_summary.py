@@ -30,8 +30,9 @@ def workload_of(args):
     def opt(name, default):
         return a[a.index(name) + 1] if name in a else default
     m = int(opt('--batch-set', '32'))
+    packed = opt('--pack-tables', '1') != '0' and opt('--config', 'deepfwfm') != 'qr'  # the tables' serving copy
     return f"{opt('--config', 'deepfwfm')}/{opt('--first-order', 'lw')}/scale{opt('--table-scale', '1')}/" \
-           f"{opt('--inputs', 'uniform')}" + ("/set" if m > 1 else "")
+           f"{opt('--inputs', 'uniform')}" + ("/set" if m > 1 else "") + ("/packed" if packed else "")
 
 
 def batches_per_launch(args):

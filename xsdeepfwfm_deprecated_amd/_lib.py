@@ -344,7 +344,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.dfwfm_abi_version() != 3:
+        if L.dfwfm_abi_version() != 4:
             raise DfwfmError("libdfwfm ABI mismatch")
         _lib = L
     return _lib
