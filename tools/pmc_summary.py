@@ -57,13 +57,14 @@ for k, v in vals.items():
     med = {c: st.median(x) for c, x in v.items()}
     # a set run's per-call leg (one batch per launch, thousands of dispatches; tools/pmc.sh now passes
     # --no-per-call) is its own workload
-    kwl = wl[:-4] + "/call" if wl.endswith("/set") and len(durs[k]) > 10 * fewest else wl
+    is_set = "/set" in wl
+    kwl = wl.replace("/set", "/call") if is_set and len(durs[k]) > 10 * fewest else wl
     e = {"kernel": k, "workload": kwl, "bench_args": bench_args, "tag": tag,
          "counters_median_per_dispatch": med, "profiled_duration_us_median": st.median(durs[k]) / 1e3,
          "dispatches": len(durs[k])}
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         e["hbm_bytes_per_launch"] = int(2 * med["FETCH_SIZE"] * 1024 + med["WRITE_SIZE"] * 1024)
-        if kwl.endswith("/set"):  # a launch is a set of M batches: bench.py scales the per-batch bytes to its sets
+        if "/set" in kwl:  # a launch is a set of M batches: bench.py scales the per-batch bytes to its sets
             e["batches_per_launch"] = batches_per_launch(bench_args)
             e["hbm_bytes_per_batch"] = e["hbm_bytes_per_launch"] // e["batches_per_launch"]
     if "SQ_VALU_MFMA_BUSY_CYCLES" in med and "GRBM_GUI_ACTIVE" in med:
