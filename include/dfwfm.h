@@ -223,11 +223,11 @@ typedef struct {
  * / batch for the reference's BCE-with-logits mean, :634).  Replaces loss.backward() (:636). */
 int dfwfm_backward(dfwfm_model* m, const float* dlogit, const dfwfm_grads* grads, void* stream);
 
-/* Deterministic backward (off by default, like torch.use_deterministic_algorithms): on, every gradient sum is
- * formed in a fixed order -- the categorical tables' contributions sorted by (row, sample) and summed by one owner
- * per row, the weight-gradient GEMM's batch splits summed in split order -- so two runs of the same step give the
- * same bits (the reference's CPU step, model/DeepFMs.py:634-637, is reproducible).  Off, both use float atomics
- * (sums in arrival order; faster).  Affects the launches enqueued after the call. */
+/* Deterministic backward (ON by default since ABI 4's round-6 build; +2.6 % per Criteo-39 training step): every
+ * gradient sum is formed in a fixed order -- the categorical tables' contributions sorted by (row, sample) and summed
+ * by one owner per row, the weight-gradient GEMM's batch splits summed in split order -- so two runs of the same step
+ * give the same bits (the reference's CPU step, model/DeepFMs.py:634-637, is reproducible).  Off (on = 0), both use
+ * float atomics (sums in arrival order).  Affects the launches enqueued after the call. */
 int dfwfm_set_deterministic(dfwfm_model* m, int32_t on);
 
 /* The same backward in two parts, so that a data-parallel caller can start the all-reduce of every

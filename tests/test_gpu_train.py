@@ -621,7 +621,7 @@ def _dp_step_worker(rank, world, port, q, name, sparse, steps):
         dist.destroy_process_group()
 
 
-def _dp_steps(name, sparse, steps, dist, rank, world):
+def _dp_steps(name, sparse, steps, dist, rank, world, deterministic=False):
     """`steps` FusedTrainSteps on the global batches of train golden `name` (64 rows each), this rank taking
     its contiguous share; returns first-step grads / logits and the final parameters."""
     from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
@@ -630,7 +630,8 @@ def _dp_steps(name, sparse, steps, dist, rank, world):
     G = 64
     bs = G // world
     m = build(cfg, params, dev, is_deep_dropout=False)
-    t = FusedTrainStep(m, bs, lr=1e-3, weight_decay=3e-7, dist=dist, sparse_exchange=sparse)
+    t = FusedTrainStep(m, bs, lr=1e-3, weight_decay=3e-7, dist=dist, sparse_exchange=sparse,
+                       deterministic=deterministic)
     first = None
     for k in range(steps):
         lo = k * G + rank * bs
@@ -754,7 +755,7 @@ def test_step_many_equals_single_steps(gpu):
     assert losses[0] == losses[1], losses
 
 
-def _nccl_world1_worker(port, q, name, graph_comm):
+def _nccl_world1_worker(port, q, name, graph_comm, det=False):
     """A world-size-1 RCCL process group (backend "nccl" is RCCL on ROCm): the packed touched-row all-gather
     (all_gather_into_tensor branch of gather_packed) and FusedTrainStep's bucketed exchange run over RCCL --
     captured into the step's graph (graph_comm) or issued between its graphs."""
@@ -773,8 +774,8 @@ def _nccl_world1_worker(port, q, name, graph_comm):
         recv = torch.zeros(1, send.numel(), dtype=torch.uint8, device=dev)
         gather_packed(dist, send, recv, async_op=True).wait()
         gathered_ok = bool(torch.equal(recv[0], send))
-        sparse = _dp_steps(name, True, 3, dist, 0, 1)   # touched-row lists over all_gather_into_tensor
-        dense = _dp_steps(name, False, 3, dist, 0, 1)   # bucketed all-reduces of the whole buffer
+        sparse = _dp_steps(name, True, 3, dist, 0, 1, det)   # touched-row lists over all_gather_into_tensor
+        dense = _dp_steps(name, False, 3, dist, 0, 1, det)   # bucketed all-reduces of the whole buffer
         q.put(("ok", gathered_ok, sparse, dense))
     except Exception as e:  # report, do not hang the parent
         q.put(("error", repr(e), None, None))
@@ -811,6 +812,33 @@ def test_rccl_exchange_world_one_matches_single_process(gpu, name, graph_comm):
             assert np.abs(g[k] - gs[k]).max() <= G_TOL * sc + 1e-12, k
         e = np.concatenate([np.abs(pr[k] - ps[k]).reshape(-1) / 1e-3 for k in ps])
         assert np.median(e) < 1e-4 and np.quantile(e, 0.999) < 0.02
+
+
+@pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult"])
+def test_rccl_world_one_deterministic_bit_identical(gpu, name):
+    """with deterministic steps the world-size-1 RCCL group's three FusedTrainSteps (sparse and dense
+    exchange, collectives inside the step's graph) give the single-process step's gradients, logits and parameters
+    bit for bit -- the exchange adds nothing to one rank's sums and reorders none of them."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1_worker, args=(port, q, name, True, True))
+    p.start()
+    status, gathered_ok, sparse, dense = q.get(timeout=300)
+    p.join(60)
+    assert status == "ok", gathered_ok
+    assert p.exitcode == 0
+    (gs, os_), ps = _dp_steps(name, True, 3, None, 0, 1, True)
+    for which, ((g, o), pr) in (("sparse", sparse), ("dense", dense)):
+        assert np.array_equal(o, os_), which
+        for k in gs:
+            assert np.array_equal(g[k], gs[k]), (which, k)
+        for k in ps:
+            assert np.array_equal(pr[k], ps[k]), (which, k)
 
 
 def test_sparse_exchange_capacity_is_per_table_rows(gpu):
@@ -1029,9 +1057,9 @@ def _hot_case(B, seed=4):
 
 @pytest.mark.parametrize("B", [3000, 9000])  # 9000: three sorted passes of <= 4096 samples
 def test_sorted_scatter_bit_identical_and_matches_atomic(gpu, monkeypatch, B):
-    """Deterministic mode (sorted table scatter, split-K slices): two backward passes give the same bits, and equal
-    the atomic scatter (the default, arrival-order sums) within fp32 reassociation, hot rows and multi-pass batches
-    included."""
+    """Deterministic mode (the default: sorted table scatter, split-K slices): two backward passes give the same
+    bits, and equal the atomic scatter (arrival-order sums) within fp32 reassociation, hot rows and multi-pass
+    batches included."""
     m, xi, xv, y = _hot_case(B)
     m = m.to(gpu).train()
     m.init_weights()
@@ -1049,9 +1077,10 @@ def test_sorted_scatter_bit_identical_and_matches_atomic(gpu, monkeypatch, B):
 
 @pytest.mark.parametrize("name", ["train_deepfwfm_lw", "train_qr_mult"])
 def test_fused_step_runs_are_bit_identical(gpu, name):
-    """Two FusedTrainStep(deterministic=True) instances from the same weights over the same 4 batches (dropout on,
-    graph-replayed steps) end with bit-identical parameters and loss: the sorted scatter, the split-K slices of the
-    weight-gradient GEMM and the tile-ordered reductions leave no arrival-order sum in the step."""
+    """Two default FusedTrainStep instances (deterministic unless asked otherwise) from the same weights over the
+    same 4 batches (dropout on, graph-replayed steps) end with bit-identical parameters and loss: the sorted scatter,
+    the split-K slices of the weight-gradient GEMM and the tile-ordered reductions leave no arrival-order sum in the
+    step."""
     from xsdeepfwfm_deprecated_amd.training import FusedTrainStep
     cfg, params, xi, xv, y, *_ = load_train_golden(name)
     B = 64
@@ -1060,7 +1089,8 @@ def test_fused_step_runs_are_bit_identical(gpu, name):
     for _ in range(2):
         m = build(cfg, params, gpu, is_deep_dropout=True)
         torch.manual_seed(11)
-        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7, deterministic=True)
+        t = FusedTrainStep(m, B, lr=1e-3, weight_decay=3e-7)
+        assert t.deterministic and m.deterministic
         for k in range(4):
             t.step(*bat[k % 3])
         torch.cuda.synchronize()

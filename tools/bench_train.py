@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--first-order", choices=["lw", "fwlw"], default="lw")
     ap.add_argument("--no-dropout", action="store_true")
     ap.add_argument("--deterministic", action="store_true",
-                    help="fixed-order gradient sums (dfwfm_set_deterministic): bit-identical runs")
+                    help="fixed-order gradient sums (dfwfm_set_deterministic; the default): bit-identical runs")
+    ap.add_argument("--atomic", action="store_true", help="float-atomic gradient sums (arrival order)")
     ap.add_argument("--copy-inputs", action="store_true",
                     help="copy every batch into the fused step's own input buffers (fit()'s path) instead of "
                          "reading the resident batches in place")
@@ -95,7 +96,7 @@ def main():
         # the four resident batches are read in place (one captured graph set each), like a loader's ring of
         # device input buffers; --copy-inputs copies each batch into the step's own buffers first
         trainer = FusedTrainStep(model, B, lr=1e-3, weight_decay=3e-7, dist=dist, resident_inputs=not a.copy_inputs,
-                                 deterministic=a.deterministic)
+                                 deterministic=not a.atomic)
 
     def step(i):
         xi, xv, y = batches[i % 4]
@@ -143,7 +144,7 @@ def main():
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms / a.steps, 4), "per_gpu_batch": B,
            "first_order": a.first_order, "dropout": not a.no_dropout, "wall_s": round(wall, 3),
            "host_enqueue_us_per_step": round(host * 1e6 / a.steps, 1),
-           "mode": a.mode, "deterministic": bool(a.deterministic), "steps_per_graph": K, "inputs": "copied" if (a.copy_inputs or a.mode != "fused") else "resident (read in place)",
+           "mode": a.mode, "deterministic": not a.atomic, "steps_per_graph": K, "inputs": "copied" if (a.copy_inputs or a.mode != "fused") else "resident (read in place)",
            "final_loss_sum": round(float(loss.item()), 4)}
     if trainer is not None and getattr(trainer, "sparse", False):
         # touched-row lists all-gathered per step (fixed capacity: sum over tables of min(batch, rows))

@@ -1,7 +1,8 @@
 """Time the backward's table scatter alone (DFWFM_BWD_SCATTER after one train forward + per-tile backward) at
-Criteo-39 sizes, B = 4096, with the diagnostic phase switches DFWFM_DIAG scatter= (results invalid when set).
+Criteo-39 sizes, B = 4096, with the diagnostic phase switches DFWFM_DIAG scatter= (results invalid when set);
+--stamps: the sorted scatter's per-workgroup phase clocks (DFWFM_DIAG stamps=3), summarised per task.
 
-    python tools/scatter_diag.py [--iters 50]
+    python tools/scatter_diag.py [--iters 50] [--stamps]
 """
 import argparse
 import ctypes
@@ -14,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def one(iters):
+def one(iters, stamps=False):
     import torch
     from xsdeepfwfm_deprecated_amd import DeepFMs, _lib, synth
     dev = torch.device("cuda:0")
@@ -46,6 +47,32 @@ def one(iters):
     for _ in range(5):
         _lib.check(L.dfwfm_backward_phases(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(g),
                                            _lib.BWD_SCATTER, st), "scatter")
+    if stamps:
+        import numpy as np
+        os.environ["DFWFM_DIAG"] = ",".join(x for x in (os.environ.get("DFWFM_DIAG", ""), "stamps=3") if x)
+        for _ in range(3):
+            _lib.check(L.dfwfm_backward_phases(eng.handle, ctypes.c_void_p(dl.data_ptr()), ctypes.byref(g),
+                                               _lib.BWD_SCATTER, st), "scatter")
+        torch.cuda.synchronize()
+        n = 512 * 16
+        buf = (ctypes.c_uint64 * n)()
+        got = L.dfwfm_diag_stamps(eng.handle, buf, n, st)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16)[:got].astype(np.int64)
+        a = a[a[:, 0] > 0]
+        names = ["load", "scan", "sort", "flags", "sums", "cuts"]
+        rows = []
+        for task in np.unique(a[:, 8]):
+            w = a[a[:, 8] == task]
+            d = np.diff(w[:, 0:7], axis=1)
+            rows.append({"task": int(task), "wgs": len(w), "keys_max": int(w[:, 9].max()),
+                         "unsorted": int(w[:, 10].sum()),
+                         "life": int((w[:, 6] - w[:, 0]).max()),
+                         **{k: int(d[:, i].max()) for i, k in enumerate(names)}})
+        for r in rows:
+            print(json.dumps(r))
+        print("per-workgroup shader-clock cycles (max over the task's workgroups); longest life:",
+              int((a[:, 6] - a[:, 0]).max()))
+        return 0.0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
@@ -60,7 +87,11 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--stamps", action="store_true")
     a = ap.parse_args()
+    if a.stamps:
+        one(5, stamps=True)
+        sys.exit(0)
     if a.child:
         print(json.dumps({"us": one(a.iters)}))
         sys.exit(0)

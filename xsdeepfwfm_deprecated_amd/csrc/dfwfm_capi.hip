@@ -77,6 +77,9 @@ struct dfwfm_model {
   float* sv_x[kMaxH + 1];
   float* sv_g[kMaxH + 1];
   float* sv_de;
+  int32_t* sv_keys;     // the training forward's clamped categorical indices, column-major (sorted scatter keys)
+  int64_t keys_stride;
+  bool t_keys;          // the last training forward wrote sv_keys
   float* sv_x0;           // X_0 after deep-tower dropout (without dropout X_0 is sv_e)
   float* red_part;        // per-16-row-tile partial sums of the shallow reductions
   float* dw_part;         // weight-gradient GEMM: per (block, split) slices (deterministic split-K, dwr_block)
@@ -211,6 +214,7 @@ int dfwfm_model_create(const dfwfm_config* cfg, dfwfm_model** out) {
   dfwfm_model* m = new dfwfm_model();
   memset(m, 0, sizeof *m);
   m->cfg = c;
+  m->deterministic = true;  // fixed-order gradient sums unless dfwfm_set_deterministic(m, 0)
   hipError_t e = hipGetDevice(&m->device);
   if (e != hipSuccess) {
     delete m;
@@ -562,6 +566,8 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   const int64_t FD = (int64_t)m->F * m->D;
   const int64_t SE = r4((int)FD);
   const int64_t per_row = SE + FD + m->F + (m->H > 0 ? SE + 2 * (int64_t)m->H * m->N : 0);
+  const int64_t keys_stride = (batch + 3) & ~(int64_t)3;  // the categorical keys, column-major
+  const int64_t keys_words = (int64_t)(m->F - m->num) * keys_stride;
   const int64_t red_blocks = (batch + kBM - 1) / kBM;
   const int64_t red_floats = red_blocks * red_outputs(m->F, m->D, m->N, m->num);
   int per_split = 0;
@@ -574,7 +580,7 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   if (m->d_ws) (void)hipFree(m->d_ws);
   m->d_ws = nullptr;
   m->ws_batch = 0;
-  const size_t total = (size_t)(per_row * batch + red_floats + dw_floats + 64);
+  const size_t total = (size_t)(per_row * batch + red_floats + dw_floats + keys_words + 64);
   HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->d_ws), sizeof(float) * total));
   // every array starts 16-byte aligned: the row counts are multiples of 4 or the offsets are padded
   auto al = [](int64_t x) { return (x + 3) & ~(int64_t)3; };
@@ -586,6 +592,8 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   m->sv_de = p;  p += al(FD * batch);
   m->red_part = p;  p += al(red_floats);
   m->sv_fo = p;  p += al((int64_t)m->F * batch);
+  m->sv_keys = reinterpret_cast<int32_t*>(p);  p += keys_words;
+  m->keys_stride = keys_stride;
   for (int h = 0; h <= kMaxH; ++h) m->sv_x[h] = m->sv_g[h] = nullptr;
   if (m->H > 0) {
     m->sv_x0 = p;  p += SE * batch;
@@ -962,6 +970,7 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
                         int64_t batch, float* out, float dropout_p, uint32_t seed, void* stream) {
   if (!m) return fail(DFWFM_ERR_INVALID_ARG, "null model");
   m->trained = false;
+  m->t_keys = false;
   m->bwd_tables = false;
   m->bwd_fused_red = false;
   m->bwd_loss_sum = nullptr;
@@ -1006,6 +1015,10 @@ int dfwfm_train_forward(dfwfm_model* m, const int64_t* xi, int64_t xi_stride, co
   const int dg = diag_opt("ft", 0);  // diagnostics only (results invalid)
   a.flags |= ((dg & 1) ? kFtDiagHwId : 0) | ((dg & 2) ? kFtDiagNoMlp : 0);
   const bool helpers = m->lds_ftrain > 0 && diag_opt("ftrain", 1) != 0;
+  // the helper-wave forward also writes the categorical indices column-major for the sorted scatter
+  a.sv_keys = helpers ? m->sv_keys : nullptr;
+  a.keys_stride = m->keys_stride;
+  m->t_keys = helpers;
   hipError_t e = helpers ? launch_ftrain(a, m->D, m->lds_ftrain, (hipStream_t)stream)
                          : launch_forward(a, m->D, m->TPWI > 0 ? m->TPWI : 1, 1, m->NG, m->lds_inf, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "train forward launch");
@@ -1169,6 +1182,8 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
     sa.sv_de = m->sv_de;
     sa.dlogit = dlogit;
     sa.lw = (m->flags & kFoLw) ? m->d_lw : nullptr;
+    sa.keys = (m->t_keys && batch <= m->ws_batch) ? m->sv_keys : nullptr;
+    sa.keys_stride = m->keys_stride;
     sa.diag = diag_opt("scatter", 0);  // diagnostics only: results invalid
     const bool need2 = (m->flags & kNeedE) != 0, need1 = (m->flags & kFoTables) != 0;
     auto add = [&](float* g2, float* g1, const float* o2, const float* o1, int64_t c, int f, int kind,
@@ -1180,16 +1195,18 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
         hipError_t er = launch_sort_scatter(sa, sblocks, s);
         if (er != hipSuccess) return hip_fail(er, "scatter launch");
         sa.ntasks = 0;
+        sa.key64 = 0;
         sblocks = 0;
       }
       SortScatterTask& t = sa.t[sa.ntasks++];
       // row buckets, one workgroup each: tables of at most 64 rows one row per bucket (no sort; a few hundred samples
       // each), larger ones eight buckets of ~B/8 samples (sorted in 45 LDS stages at B = 4096, not 4096 keys' 78)
       t.onerow = rows <= 64 ? 1 : 0;
-      t.nbuck = (int16_t)(rows <= 64 ? (rows > 0 ? rows : 1) : 8);
+      t.nbuck = (int16_t)(rows <= 64 ? (rows > 0 ? rows : 1) : diag_opt("nbuck", 8));
       t.block0 = sblocks;
       t.pad8 = 0;
       sblocks += t.nbuck;
+      if ((rows + t.nbuck - 1) / t.nbuck >= kSortKey32Rows) sa.key64 = 1;
       t.g2 = g2;
       t.g1 = g1;
       t.o2 = need2 ? o2 : nullptr;
@@ -1216,6 +1233,8 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       }
     }
     if (rc != DFWFM_OK) return rc;
+    // diagnostics only: DFWFM_DIAG stamps=3 records this (last) launch's phase clocks per workgroup
+    if ((rc = diag_stamps_buffer(m, (int64_t)sblocks * kBM, 3, &sa.stamps)) != DFWFM_OK) return rc;
     e = launch_sort_scatter(sa, sblocks, s);
     if (e != hipSuccess) return hip_fail(e, "scatter launch");
   }

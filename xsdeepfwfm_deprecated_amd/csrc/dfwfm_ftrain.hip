@@ -178,6 +178,20 @@ __global__ void __launch_bounds__(kNTH) ftrain_kernel(FwdArgs p) {
     if (i < n_fwlw) fw[k] = p.fwlw[i];
   }
   const float lwv = ((flags & kFoLw) && tid < F) ? p.lw[tid] : 0.f;
+  if (p.sv_keys != nullptr) {  // the sorted scatter's keys: the clamped categorical indices, column-major
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = tid + k * kNTH;
+      const int f = r >> 4;
+      const int64_t gb = b0 + (r & 15);
+      if (f >= num && f < F && gb < p.batch) {
+        int64_t n;
+        if constexpr (QR) n = p.fields[f].n;
+        else n = rd_n[k];
+        p.sv_keys[(int64_t)(f - num) * p.keys_stride + gb] = (key[k] < 0 || key[k] >= n) ? 0 : (int32_t)key[k];
+      }
+    }
+  }
   if constexpr (QR) {
 #pragma unroll
     for (int k = 0; k < kDescPT; ++k) {

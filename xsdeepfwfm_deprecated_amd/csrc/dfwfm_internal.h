@@ -98,6 +98,9 @@ struct FwdArgs {
   float drop_scale;         // 1 / (1 - p)
   uint32_t seed;            // dropout hash seed of this step
   const int64_t* seed_src;  // device step counter mixed into the seed (graph replay), or null
+  int32_t* sv_keys;         // training: [F - num][keys_stride] the categorical indices, clamped, column-major (the
+                            // sorted scatter's keys), or null
+  int64_t keys_stride;
   // gather launch (PART 1; the sparse deep tower reads them) or dfwfm_forward_gather (PART 3)
   float* part_e;            // [B][part_stride] E tile rows (W0 columns, zero padded past F*D)
   float* part_fs;           // [B] first + second order
@@ -281,7 +284,7 @@ struct ScatterArgs {
 // (second order, width D; first order, width 1).  A workgroup sorts the batch's (row, sample) keys in LDS and sums
 // every row's contributions in a fixed order, so the gradients are the same bits on every run.
 constexpr int kSortSeg = 4096;      // samples sorted per pass (larger batches: passes in sample order)
-constexpr int kSortCh = 32;         // sorted positions per chunk of the segmented sums
+constexpr int kSortCh = 16;         // sorted positions per chunk of the segmented sums
 constexpr int kSortThreads = 512;
 struct SortScatterTask {
   float* g2;            // second-order table grad (width D) or null
@@ -309,8 +312,15 @@ struct SortScatterArgs {
   const float* sv_de;
   const float* dlogit;
   const float* lw;      // [F] or null (dfo = dlogit)
-  int32_t diag;         // diagnostics only (DFWFM_DIAG scatter=): 1 skip the sort, 2 skip the sums, 4 no row adds
+  const int32_t* keys;  // the training forward's clamped categorical indices [F - num][keys_stride] or null (xi)
+  int64_t keys_stride;  // a multiple of 4
+  int32_t key64;        // 1: some task's buckets reach 2^20 rows (64-bit sort keys)
+  int32_t diag;         // diagnostics only (DFWFM_DIAG scatter=): 1 skip the sort, 2 skip the sums, 4 no row adds,
+                        // 8 empty, 16 key loads only, 32 every position reads one sample
+  uint64_t* stamps;     // diagnostics only (DFWFM_DIAG stamps=3): phase clocks per workgroup, normally null
 };
+// a task's sort keys are (row / nbuck) << 12 | sample in 32 bits when every bucket's rows stay under 2^20, else 64
+constexpr int kSortKey32Rows = 1 << 20;
 size_t sort_scatter_lds_bytes(int D);
 
 // Touched-row gradients of one table family (dfwfm_sparse.hip): one task per categorical table.

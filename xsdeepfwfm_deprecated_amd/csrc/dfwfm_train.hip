@@ -952,27 +952,30 @@ __global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Deterministic categorical-table scatter (deterministic mode, dfwfm_set_deterministic; the default scatter_kernel's
-// atomics add a row's contributions in arrival order, so two runs of the same step can differ in the last bits).  A task is one field and row kind, both
-// table families at once; its rows are split into nbuck buckets (row % nbuck), one workgroup each, so every row has
-// ONE owner workgroup.  Per pass over <= kSortSeg samples the owner:
-//   1. keeps its bucket's samples in sample order (a block scan) as keys (row << 12 | sample) in LDS -- unique, so any
-//      correct sort gives the same order -- with each sample's QR partner row; 2. bitonic sort in LDS; 3. walks the
+// Deterministic categorical-table scatter (deterministic mode, dfwfm_set_deterministic; the atomic scatter_kernel
+// adds a row's contributions in arrival order, so two runs of the same step can differ in the last bits).  A task is
+// one field and row kind, both table families at once; its rows are split into nbuck buckets (row % nbuck), one
+// workgroup each, so every row has ONE owner workgroup.  Per pass over <= kSortSeg samples the owner:
+//   1. reads the field's keys (the training forward's clamped indices, column-major: 32 contiguous bytes per
+//      thread; xi when absent), keeps its bucket's samples in sample order (wave ballots, one barrier) as keys
+//      (row / nbuck) << 12 | sample -- unique, so any correct sort gives the same order -- in 32 bits when the
+//      bucket's rows stay under 2^20, with each sample's QR partner row; 2. bitonic sort in registers (partners inside
+//      a row of 16 lanes by DPP, 16 apart by swizzle, 32 by the LDS crossbar, farther through LDS); 3. walks the
 //      sorted positions in chunks of kSortCh: a work item (chunk, component) sums each run of equal rows in position
 //      order; a run that starts and ends inside the chunk is added to its row at once, a run cut by the chunk's start /
 //      end leaves its partial sum in LDS (lead / trail); 4. the chunk holding a cut run's head adds trail + the
 //      following chunks' leads in chunk order.  Every row is added by exactly one thread per pass (passes follow each
 //      other behind a barrier), in an order fixed by the sorted positions: the same bits on every run.
 // ---------------------------------------------------------------------------
-template <int NTH>
-__device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid) {
+template <int NTH, typename K>
+__device__ __forceinline__ void bitonic_sort_lds(K* key, int np, int tid) {
   for (int k = 2; k <= np; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int i = tid; i < (np >> 1); i += NTH) {
         const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
         const int hi = lo + j;
         const bool asc = (lo & k) == 0;
-        const uint64_t x = key[lo], y = key[hi];
+        const K x = key[lo], y = key[hi];
         if ((x > y) == asc) {
           key[lo] = y;
           key[hi] = x;
@@ -982,70 +985,91 @@ __device__ __forceinline__ void bitonic_sort_lds(uint64_t* key, int np, int tid)
     }
 }
 
-// the same network with each thread's E consecutive keys in registers (np = E * NTH): stages of partner distance
-// j < E inside the thread, E <= j < 64 E across the wave (lane ^ j / E, no LDS and no barrier), and only the
-// distances past a wave through LDS -- at np = 512 on 512 threads 6 of the 45 stages take a barrier
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-  return ((uint64_t)hi << 32) | lo;
+// the value of lane ^ M (M = 1 .. 32): DPP moves on the VALU inside a row of 16 lanes (quad permutes, rotations:
+// row_ror:n reads lane (i - n) mod 16), a swizzle for 16, the LDS crossbar (bpermute) for 32
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
+  const int x = (int)v;
+  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  else if constexpr (M == 4) {
+    const int from_lo = __builtin_amdgcn_mov_dpp(x, 0x124, 0xF, 0xF, false);  // row_ror:4: lane i - 4
+    const int from_hi = __builtin_amdgcn_mov_dpp(x, 0x12C, 0xF, 0xF, false);  // row_ror:12: lane i + 4
+    return (uint32_t)((lane & 4) ? from_lo : from_hi);
+  } else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false);  // row_ror:8
+  else if constexpr (M == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x401F);  // bitmask mode, xor 16
+  else return (uint32_t)__shfl_xor(x, M);
 }
-template <int NTH, int E>
-__device__ __forceinline__ void bitonic_sort_reg(uint64_t* key, int tid) {
-  constexpr int np = NTH * E;
-  uint64_t x[E];
+template <int M>
+__device__ __forceinline__ uint64_t xor_lane(uint64_t v, int lane) {
+  return ((uint64_t)xor_lane<M>((uint32_t)(v >> 32), lane) << 32) | xor_lane<M>((uint32_t)v, lane);
+}
+
+// one compare-exchange stage (merge size KK, partner distance J) of the network over NTH * E keys, each thread's E
+// consecutive keys in registers: J < E inside the thread, E <= J < 64 E across the wave (lane ^ J / E), past a wave
+// through LDS (two barriers)
+template <int NTH, int E, int KK, int J, typename K>
+__device__ __forceinline__ void bitonic_stage(K (&x)[E], K* key, int tid, int lane) {
+  if constexpr (J < E) {
 #pragma unroll
-  for (int e = 0; e < E; ++e) x[e] = key[tid * E + e];
-  for (int k = 2; k <= np; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j < E) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int i = tid * E + e;
-          if ((e & j) == 0) {
-            const bool asc = (i & k) == 0;
-            const uint64_t lo = x[e], hi = x[e + j];
-            if ((lo > hi) == asc) {
-              x[e] = hi;
-              x[e + j] = lo;
-            }
-          }
+    for (int e = 0; e < E; ++e) {
+      if ((e & J) == 0) {
+        const bool asc = ((tid * E + e) & KK) == 0;
+        const K lo = x[e], hi = x[e + J];
+        if ((lo > hi) == asc) {
+          x[e] = hi;
+          x[e + J] = lo;
         }
-      } else if (j < 64 * E) {
-        const int m = j / E;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int i = tid * E + e;
-          const uint64_t y = shfl_xor_u64(x[e], m);
-          const bool asc = (i & k) == 0, lower = (i & j) == 0;
-          const bool take_min = asc == lower;
-          x[e] = take_min ? (y < x[e] ? y : x[e]) : (y > x[e] ? y : x[e]);
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < E; ++e) key[tid * E + e] = x[e];
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int i = tid * E + e;
-          const uint64_t y = key[i ^ j];
-          const bool asc = (i & k) == 0, lower = (i & j) == 0;
-          const bool take_min = asc == lower;
-          x[e] = take_min ? (y < x[e] ? y : x[e]) : (y > x[e] ? y : x[e]);
-        }
-        __syncthreads();
       }
     }
+  } else if constexpr (J < 64 * E) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = tid * E + e;
+      const K y = xor_lane<J / E>(x[e], lane);
+      const bool take_min = ((i & KK) == 0) == ((i & J) == 0);
+      x[e] = take_min ? (y < x[e] ? y : x[e]) : (y > x[e] ? y : x[e]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) key[tid * E + e] = x[e];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = tid * E + e;
+      const K y = key[i ^ J];
+      const bool take_min = ((i & KK) == 0) == ((i & J) == 0);
+      x[e] = take_min ? (y < x[e] ? y : x[e]) : (y > x[e] ? y : x[e]);
+    }
+    __syncthreads();
+  }
+}
+template <int NTH, int E, int KK, int J, typename K>
+__device__ __forceinline__ void bitonic_net(K (&x)[E], K* key, int tid, int lane) {
+  bitonic_stage<NTH, E, KK, J>(x, key, tid, lane);
+  if constexpr (J > 1) bitonic_net<NTH, E, KK, J / 2>(x, key, tid, lane);
+  else if constexpr (KK < NTH * E) bitonic_net<NTH, E, KK * 2, KK>(x, key, tid, lane);
+}
+
+// the whole network unrolled at compile time (every stage's partner move static): at np = 512 on 512 threads 6 of
+// the 45 stages take a barrier
+template <int NTH, int E, typename K>
+__device__ __forceinline__ void bitonic_sort_reg(K* key, int tid) {
+  K x[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) x[e] = key[tid * E + e];
+  bitonic_net<NTH, E, 2, 1>(x, key, tid, tid & 63);
 #pragma unroll
   for (int e = 0; e < E; ++e) key[tid * E + e] = x[e];
   __syncthreads();
 }
 
 // np keys (a power of two, 2 <= np <= kSortSeg) in LDS, sorted ascending in place
-template <int NTH>
-__device__ __forceinline__ void sort_keys(uint64_t* key, int np, int tid) {
+template <int NTH, typename K>
+__device__ __forceinline__ void sort_keys(K* key, int np, int tid) {
   if (np <= NTH) {
     // pad to NTH keys (sentinels sort last), one per thread
-    for (int i = np + tid; i < NTH; i += NTH) key[i] = ~0ull;
+    for (int i = np + tid; i < NTH; i += NTH) key[i] = ~(K)0;
     __syncthreads();
     bitonic_sort_reg<NTH, 1>(key, tid);
   } else if (np == 2 * NTH) {
@@ -1061,23 +1085,24 @@ __device__ __forceinline__ void sort_keys(uint64_t* key, int np, int tid) {
 
 __host__ __device__ inline int sort_scatter_nch() { return kSortSeg / kSortCh; }
 
+template <typename K>
 __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterArgs a) {
   constexpr int NTH = kSortThreads;
   constexpr int CH = kSortCh;
   constexpr int SPT = kSortSeg / NTH;  // samples per thread when selecting the bucket's samples
+  static_assert(SPT == 8, "two 16-byte key loads per thread");
   const int NCH = sort_scatter_nch();
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int D = a.D, FD = a.F * D, ncomp = D + 1;  // components: 0..D-1 second-order row, D first order
-  uint64_t* key = reinterpret_cast<uint64_t*>(smem);
-  int32_t* partv = reinterpret_cast<int32_t*>(key + kSortSeg);
-  int32_t* cnt_s = partv + kSortSeg;                         // [NTH] kept samples per thread, then their prefix
-  float* lead = reinterpret_cast<float*>(cnt_s + NTH);      // [NCH][ncomp]
+  K* key = reinterpret_cast<K*>(smem);
+  int32_t* partv = reinterpret_cast<int32_t*>(smem + kSortSeg * 2);  // room for 64-bit keys
+  int32_t* wtot_s = partv + kSortSeg;                                  // [NTH / 64] kept samples per wave
+  float* lead = reinterpret_cast<float*>(wtot_s + NTH / 64);          // [NCH][ncomp]
   float* trail = lead + NCH * ncomp;
   uint8_t* cflag = reinterpret_cast<uint8_t*>(trail + NCH * ncomp);  // bit 0: first run continues from the
                                                                      // previous chunk, 1: last run continues into
                                                                      // the next, 2: one run
-  __shared__ int s_total;
   // this workgroup's task and bucket
   int lo = 0, hi = a.ntasks - 1;
   const int bid = blockIdx.x;
@@ -1088,6 +1113,8 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
   }
   const SortScatterTask T = a.t[lo];
   const int bucket = bid - T.block0, nbuck = T.nbuck;
+  stamp(a.stamps, 0, tid);
+  if (a.stamps && tid == 0) a.stamps[(size_t)bid * kStampSlots + 8] = (uint64_t)lo;
   if (a.diag & 8) return;
   const FieldDev fd = a.fields[T.field];
   const int f = T.field, col = f - a.num;
@@ -1095,72 +1122,106 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
   for (int64_t s0 = 0; s0 < a.batch; s0 += kSortSeg) {
     const int ns = (int)((a.batch - s0) < kSortSeg ? (a.batch - s0) : kSortSeg);
     // 1. this bucket's samples of the pass, in sample order: thread t looks at samples [SPT t, SPT t + SPT)
-    int64_t rw[SPT];
+    int64_t idxv[SPT];
+    if (a.keys) {  // clamped by the training forward
+      const int32_t* kc = a.keys + (int64_t)col * a.keys_stride + s0 + tid * SPT;
+      if (tid * SPT + SPT <= ns) {
+        const int4 k0 = reinterpret_cast<const int4*>(kc)[0], k1 = reinterpret_cast<const int4*>(kc)[1];
+        idxv[0] = k0.x; idxv[1] = k0.y; idxv[2] = k0.z; idxv[3] = k0.w;
+        idxv[4] = k1.x; idxv[5] = k1.y; idxv[6] = k1.z; idxv[7] = k1.w;
+      } else {
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) idxv[u] = tid * SPT + u < ns ? kc[u] : -1;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        const int i = tid * SPT + u;
+        int64_t idx = -1;
+        if (i < ns) {
+          idx = a.xi[(s0 + i) * a.xi_stride + col];
+          if (idx < 0 || idx >= fd.n) idx = 0;  // the forward clamped (and flagged) it the same way
+        }
+        idxv[u] = idx;
+      }
+    }
+    K kk[SPT];
     int32_t pt[SPT];
-    int kept = 0;
+    bool keep[SPT];
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
-      const int i = tid * SPT + u;
-      rw[u] = -1;
-      pt[u] = 0;
-      if (i < ns) {
-        int64_t idx = a.xi[(s0 + i) * a.xi_stride + col];
-        if (idx < 0 || idx >= fd.n) idx = 0;  // the forward clamped (and flagged) it the same way
-        int64_t row = idx, part = 0;
-        if (T.kind == 1) {
-          row = idx / T.c;
-          part = idx - row * T.c;
-        } else if (T.kind == 2) {
-          part = idx / T.c;
-          row = idx - part * T.c;
-        }
-        if ((int)((uint32_t)row % (uint32_t)nbuck) == bucket) {  // rows < 2^31
-          rw[u] = row;
-          pt[u] = (int32_t)part;
-          ++kept;
-        }
+      const int64_t idx = idxv[u];
+      int64_t row = idx, part = 0;
+      if (T.kind == 1) {
+        row = idx / T.c;
+        part = idx - row * T.c;
+      } else if (T.kind == 2) {
+        part = idx / T.c;
+        row = idx - part * T.c;
       }
+      keep[u] = idx >= 0 && (int)((uint32_t)row % (uint32_t)nbuck) == bucket;  // rows < 2^31
+      kk[u] = ((K)((uint32_t)row / (uint32_t)nbuck) << 12) | (K)(tid * SPT + u);
+      pt[u] = (int32_t)part;
     }
     if (a.diag & 16) {  // diagnostics: the key loads only
-      if (kept == 99999) cnt_s[0] = (int)rw[0];
+      if (keep[0] && kk[0] == (K)99999) wtot_s[0] = 1;
       return;
     }
-    cnt_s[tid] = kept;
-    __syncthreads();
-    for (int o = 1; o < NTH; o <<= 1) {  // inclusive scan of the per-thread counts
-      const int x = tid >= o ? cnt_s[tid - o] : 0;
-      __syncthreads();
-      cnt_s[tid] += x;
-      __syncthreads();
-    }
-    int pos = cnt_s[tid] - kept;
-    if (tid == NTH - 1) s_total = cnt_s[NTH - 1];
+    stamp(a.stamps, 1, tid);
+    // positions in sample order: the kept samples of lower lanes (one ballot per slot u), then of lower waves
+    int before = 0, wtot = 0;
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
-      if (rw[u] >= 0) {
-        const int i = tid * SPT + u;
-        key[pos++] = ((uint64_t)rw[u] << 12) | (uint64_t)i;
-        partv[i] = pt[u];
+      const uint64_t bal = __ballot(keep[u]);
+      before += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      wtot += __popcll(bal);
+    }
+    if (lane == 0) wtot_s[wave] = wtot;
+    __syncthreads();
+    int pos = before, n = 0;
+#pragma unroll
+    for (int w = 0; w < NTH / 64; ++w) {
+      const int c = wtot_s[w];
+      pos += w < wave ? c : 0;
+      n += c;
+    }
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      if (keep[u]) {
+        key[pos++] = kk[u];
+        partv[tid * SPT + u] = pt[u];
       }
     }
     __syncthreads();
-    const int n = s_total;
+    stamp(a.stamps, 2, tid);
+    if (a.stamps && tid == 0) a.stamps[(size_t)bid * kStampSlots + 9] = (uint64_t)n;
     if (n > 0) {
       int np = 2;
       while (np < n) np <<= 1;
-      for (int i = n + tid; i < np; i += NTH) key[i] = ~0ull;
+      for (int i = n + tid; i < np; i += NTH) key[i] = ~(K)0;
       __syncthreads();
       // one row per bucket (small tables): the keys are already in order (sample order, one run)
       if (!(a.diag & 1) && !T.onerow) sort_keys<NTH>(key, np, tid);
+      stamp(a.stamps, 3, tid);
+      if (a.stamps) {  // diagnostics: count out-of-order neighbours (slot 10; 0 for a correct sort)
+        __shared__ int s_bad;
+        if (tid == 0) s_bad = 0;
+        __syncthreads();
+        for (int i = tid; i + 1 < n; i += NTH)
+          if (key[i] > key[i + 1]) atomicAdd(&s_bad, 1);
+        __syncthreads();
+        if (tid == 0) a.stamps[(size_t)bid * kStampSlots + 10] = (uint64_t)s_bad;
+      }
       const int nch = (n + CH - 1) / CH;
       for (int c = tid; c < nch; c += NTH) {
         const int p0 = c * CH, p1 = (p0 + CH < n ? p0 + CH : n) - 1;
-        const uint64_t r0 = key[p0] >> 12, r1 = key[p1] >> 12;
+        const K r0 = key[p0] >> 12, r1 = key[p1] >> 12;
         const bool cin = p0 > 0 && (key[p0 - 1] >> 12) == r0;
         const bool cout = p1 + 1 < n && (key[p1 + 1] >> 12) == r1;
         cflag[c] = (uint8_t)((cin ? 1 : 0) | (cout ? 2 : 0) | (r0 == r1 ? 4 : 0));
       }
       __syncthreads();
+      stamp(a.stamps, 4, tid);
       // 3. runs inside each chunk.  Items: (chunk, d) of the second-order family with d fastest -- the lanes of one
       // chunk read one sample's 40-byte dE row per position and add one 40-byte table row per run: coalesced --
       // then one item per chunk for the first-order family
@@ -1184,31 +1245,38 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
         const float* o = fam2 ? T.o2 : T.o1;
         const int p0 = c * CH, cnt = n - p0 < CH ? n - p0 : CH;
         const int fl = cflag[c];
+        // every position's load issued before any is used (unguarded: positions past the batch read the chunk's last
+        // key and are zeroed), so the chunk waits for one memory round trip, not one per position
+        const float* src = fam2 ? a.sv_de + (int64_t)f * D + jj : a.dlogit;
+        const int64_t sstride = fam2 ? FD : 1;
+        const float scale = fam2 ? 1.f : lwf;
         float v[CH];
         uint32_t rq[CH];
+        int sm[CH];
 #pragma unroll
         for (int q = 0; q < CH; ++q) {
-          v[q] = 0.f;
-          rq[q] = 0xffffffffu;
-          if (q < cnt) {
-            const uint64_t k = key[p0 + q];
-            const int sm = (int)(k & 4095);
-            rq[q] = (uint32_t)(k >> 12);
-            const int64_t b = s0 + sm;
-            float x = fam2 ? a.sv_de[b * FD + f * D + jj] : a.dlogit[b] * lwf;
-            if (o) x *= o[(int64_t)partv[sm] * w + jj];
-            v[q] = x;
-          }
+          const K k = key[p0 + (q < cnt ? q : cnt - 1)];
+          sm[q] = (a.diag & 32) ? 0 : (int)(k & 4095);  // diagnostics: one sample's row
+          rq[q] = q < cnt ? (uint32_t)(k >> 12) : 0xffffffffu;
         }
+#pragma unroll
+        for (int q = 0; q < CH; ++q) v[q] = src[(s0 + sm[q]) * sstride] * scale;
+        if (o) {
+#pragma unroll
+          for (int q = 0; q < CH; ++q) v[q] *= o[(int64_t)partv[sm[q]] * w + jj];
+        }
+#pragma unroll
+        for (int q = 0; q < CH; ++q) v[q] = q < cnt ? v[q] : 0.f;
         float sum = 0.f;
         uint32_t cur = rq[0];
         bool first = true;
+        auto row_of = [&](uint32_t rl) { return (int64_t)rl * nbuck + bucket; };
 #pragma unroll
         for (int q = 0; q < CH; ++q) {
           if (q < cnt) {
             if (rq[q] != cur) {  // a run ends inside the chunk
               if (first && (fl & 1)) lead[c * ncomp + j] = sum;
-              else if (adds) atomicAdd(g + (int64_t)cur * w + jj, sum);  // the row's only adder in this pass
+              else if (adds) atomicAdd(g + row_of(cur) * w + jj, sum);  // the row's only adder in this pass
               first = false;
               cur = rq[q];
               sum = 0.f;
@@ -1218,10 +1286,15 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
         }
         if (first && (fl & 1)) lead[c * ncomp + j] = sum;  // continues from the previous chunk (maybe into the next)
         else if (fl & 2) trail[c * ncomp + j] = sum;     // its head is here, its tail in the next chunk(s)
-        else if (adds) atomicAdd(g + (int64_t)cur * w + jj, sum);
+        else if (adds) atomicAdd(g + row_of(cur) * w + jj, sum);
       }
-      __syncthreads();
+      // LDS-only barrier: the leads / trails are visible, the row adds stay in flight (phase 4 adds other rows)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      stamp(a.stamps, 5, tid);
       // 4. runs cut by chunk ends: the chunk with the head adds its trail and the following chunks' leads in order
+      // (eight chunks' flags and leads read at a time: a long run's walk is not one LDS round trip per chunk)
       for (int it = tid; it < n2 + n1; it += NTH) {
         int c, j;
         item(it, c, j);
@@ -1231,34 +1304,54 @@ __global__ void __launch_bounds__(kSortThreads) sort_scatter_kernel(SortScatterA
         float* g = fam2 ? T.g2 : T.g1;
         float sum = trail[c * ncomp + j];
         int c2 = c + 1;
-        while (true) {
-          sum += lead[c2 * ncomp + j];
-          if ((cflag[c2] & 6) == 6) ++c2;  // one run that continues: the whole chunk belongs to the run
-          else break;
+        bool done = false;
+        while (!done) {
+          uint8_t f8[8];
+          float l8[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int cc = c2 + t < nch ? c2 + t : nch - 1;
+            f8[t] = cflag[cc];
+            l8[t] = lead[cc * ncomp + j];
+          }
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            if (!done) {
+              sum += l8[t];
+              done = (f8[t] & 6) != 6;  // the run ends in this chunk unless the whole chunk continues it
+            }
+          }
+          c2 += 8;
         }
         const int p1 = c * CH + CH - 1;  // a chunk with a continuing last run is full
-        const uint32_t row = (uint32_t)(key[p1] >> 12);
-        if (adds) atomicAdd(g + (int64_t)row * (fam2 ? D : 1) + (fam2 ? j : 0), sum);
+        const int64_t row = (int64_t)(uint32_t)(key[p1] >> 12) * nbuck + bucket;
+        if (adds) atomicAdd(g + row * (fam2 ? D : 1) + (fam2 ? j : 0), sum);
       }
     }
     // the next pass's adds to the same rows come after these (this workgroup's own atomics, retired before the
-    // barrier; no device-scope fence: nothing another workgroup reads)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
+    // barrier; no device-scope fence: nothing another workgroup reads); the last pass leaves them in flight
+    if (s0 + kSortSeg < a.batch) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __syncthreads();
+    }
   }
+  stamp(a.stamps, 6, tid);
 }
 
 size_t sort_scatter_lds_bytes(int D) {
   const int NCH = sort_scatter_nch();
-  return (size_t)kSortSeg * 12 + (size_t)kSortThreads * 4 + (size_t)2 * NCH * (D + 1) * 4 + (size_t)NCH;
+  return (size_t)kSortSeg * 12 + (size_t)(kSortThreads / 64) * 4 + (size_t)2 * NCH * (D + 1) * 4 + (size_t)NCH;
 }
 
 hipError_t launch_sort_scatter(const SortScatterArgs& a, int total_blocks, hipStream_t s) {
   if (a.ntasks <= 0 || a.batch <= 0 || total_blocks <= 0) return hipSuccess;
   const size_t lds = sort_scatter_lds_bytes(a.D);
-  hipError_t e = ensure_lds_limit(reinterpret_cast<const void*>(sort_scatter_kernel), lds);
+  const void* fn = a.key64 ? reinterpret_cast<const void*>(sort_scatter_kernel<uint64_t>)
+                           : reinterpret_cast<const void*>(sort_scatter_kernel<uint32_t>);
+  hipError_t e = ensure_lds_limit(fn, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sort_scatter_kernel, dim3(total_blocks), dim3(kSortThreads), lds, s, a);
+  if (a.key64) hipLaunchKernelGGL(sort_scatter_kernel<uint64_t>, dim3(total_blocks), dim3(kSortThreads), lds, s, a);
+  else hipLaunchKernelGGL(sort_scatter_kernel<uint32_t>, dim3(total_blocks), dim3(kSortThreads), lds, s, a);
   return hipGetLastError();
 }
 

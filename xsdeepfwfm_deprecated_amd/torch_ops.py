@@ -110,7 +110,7 @@ def _backward(ctx, grad_out, grad_token):
     dg["lin_w"] = [by_id.get(id(t)) for t in dense["lin_w"]]
     dg["lin_b"] = [by_id.get(id(t)) for t in dense["lin_b"]]
     xi, xv = ctx.saved_tensors  # alive (see _setup_context) until the backward is enqueued
-    eng.set_deterministic(getattr(m, "deterministic", False))
+    eng.set_deterministic(getattr(m, "deterministic", True))
     eng.backward(ctx.token, grad_out.contiguous(), fg, dg)
     m._grad_flat = flat
     del xi, xv
