@@ -52,11 +52,13 @@ else:
     with torch.no_grad():
         for _ in range(a.iters):
             if a.batches > 1:
+                m._sync_inference(dev)  # the tables' serving copy, as bench.py
                 m._sync_engine(dev).forward_batches(data, outs)
             else:
                 m(xi, xv)
 torch.cuda.synchronize()
-rows = 32 if diag_get("r32") == "1" else 16  # r32=1: fwd32_kernel's 32-sample workgroups
+# fwd32_kernel's 32-sample workgroups: batch sets of the deep model unless r32=0 (r32=1 forces them)
+rows = 32 if (diag_get("r32") == "1" or (a.batches > 1 and not a.fwfm and not a.train and diag_get("r32") != "0")) else 16
 grid = a.batches * ((a.batch + rows - 1) // rows)
 buf = (ctypes.c_uint64 * (grid * 16))()
 n = _lib.lib().dfwfm_diag_stamps(m._engine.handle, buf, grid * 16,
@@ -100,7 +102,7 @@ elif a.train and diag_get("ftrain", "1") != "0":  # ftrain_kernel: helper waves 
              "  . epilogue (wave 0)", "  . barriers, split tile", "MLP layer 2", "MLP layer 3", "combine"]
     slots = [(0, 1), (1, 2), (2, 10), (10, 9), (4, 11), (5, 7), (3, 4), (3, 12), (12, 13), (13, 4), (4, 5), (5, 6),
              (6, 8)]
-elif diag_get("r32") == "1":  # fwd32 has no slot 7
+elif rows == 32:  # fwd32 has no slot 7
     names = names[:7] + names[9:]
     slots = slots[:7] + slots[9:]
 for nm, sl in zip(names, slots):
