@@ -607,7 +607,7 @@ int ensure_workspace(dfwfm_model* m, int64_t batch) {
   return DFWFM_OK;
 }
 
-// split forward workspace: E rows [B][NC0*16] then first + second [B]
+// the sparse deep tower's forward workspace (dfwfm_forward_ws): the gather launch's E rows [B][NC0*16], then first + second [B]
 size_t split_e_floats(const dfwfm_model* m, int64_t batch) { return (size_t)batch * m->NC0 * 16; }
 size_t split_ws_bytes(const dfwfm_model* m, int64_t batch) {
   return sizeof(float) * (split_e_floats(m, batch) + (size_t)batch);
