@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end evidence on the gpurun box (tools/gpu_steps.sh steps; TAG = $1): the GPU test suite, smoke(), the
 # driver's bench command under rocprofv3 (kernel trace + stats) and plain, the steady-state and per-config lines,
-# the training step (plain, deterministic, several steps per graph, under rocprofv3, phase stamps), the single-call
+# the training step (deterministic default, float-atomic, several steps per graph, under rocprofv3, phase stamps), the single-call
 # latency table.
 T=${1:-final}
 bash tools/gpu_steps.sh "$T" \
@@ -19,7 +19,7 @@ bash tools/gpu_steps.sh "$T" \
  'pruned20|200|python bench.py --config pruned --steps 20 --warmup 5 --no-cpu-baseline' \
  'train|200|python tools/bench_train.py --steps 500 --warmup 20' \
  'train4|200|python tools/bench_train.py --steps 500 --warmup 20 --steps-per-graph 4' \
- 'traindet|200|python tools/bench_train.py --steps 500 --warmup 20 --deterministic' \
+ 'trainatomic|200|python tools/bench_train.py --steps 500 --warmup 20 --atomic' \
  'train0|200|DFWFM_DIAG=ftrain=0 python tools/bench_train.py --steps 500 --warmup 20' \
  "proftrain|200|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_proftrain -o run --output-format csv -- python3 tools/bench_train.py --steps 50" \
  'st-train|120|python tools/phase_stamps.py --train --batch 4096 --iters 10' \
