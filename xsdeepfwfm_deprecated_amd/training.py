@@ -410,6 +410,17 @@ class FusedTrainStep:
                                                 ctypes.byref(self.grads), _lib.BWD_MLP_WEIGHTS, self._stream()),
                    "dfwfm_backward_phases")
 
+    def _one_process_step(self, denom, s, s1):
+        """One step on one process, captured on stream s: forward, loss gradient, per-tile backward; the table scatter
+        on s1 beside the reductions' final sums + weight-gradient GEMM on s; Adam after both."""
+        self._part1(self.B, denom, phases=_lib.BWD_TILES)
+        s1.wait_stream(s)
+        with torch.cuda.stream(s1):
+            self._backward_phase(_lib.BWD_SCATTER)
+        self._backward_phase(_lib.BWD_REDUCE | _lib.BWD_MLP_WEIGHTS)
+        s.wait_stream(s1)
+        self._part2()
+
     def _bucketed(self):
         return self.dist is not None and self.n_bucket_a < self.grad.numel()
 
@@ -520,16 +531,16 @@ class FusedTrainStep:
         g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         ga = None
         if self.dist is None and self.n_adam > self.n_main:
-            # one process: ONE stream -- fill, re-pack, forward, loss gradient, backward, reductions, scatter,
-            # weight-gradient GEMM, one Adam launch.  The forked layouts (the GEMM and the MLP's Adam on a side stream
-            # beside the reductions / scatter / main Adam) measured level with it (0.302-0.307 ms,
-            # profiles/r04/r04h_tr-*.log) at 160-230 us of host enqueue per step against 17-29 us: with the GEMM's 225
-            # workgroups resident, whatever ran beside it was starved of CU slots and stretched by about what the
-            # overlap saved; removed in round 6
+            # one process, one graph: fill, re-pack, forward, loss gradient and per-tile backward; then the table
+            # scatter on a side stream beside the reductions' final sums + weight-gradient GEMM (one launch); one Adam
+            # launch.  The scatter (latency-bound: one 512-thread workgroup per bucket, 60 KB of LDS) fits on the CUs
+            # beside the GEMM's 225 register-heavy four-wave workgroups: 0.2722 -> 0.2665 ms per step
+            # (profiles/r06/r06_fork.log).  (Round 4's forks -- the GEMM and the MLP's Adam beside the reductions /
+            # atomic scatter / main Adam -- measured level: what ran beside the GEMM was starved of CU slots.)
+            s1 = torch.cuda.Stream(self.dev)
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g1, stream=s):
-                    self._part1(self.B, denom)
-                    self._part2()
+                    self._one_process_step(denom, s, s1)
             torch.cuda.current_stream(self.dev).wait_stream(s)
             return g1, None, None, None, None
         if self._comm_in_graph():
@@ -690,12 +701,12 @@ class FusedTrainStep:
             s = torch.cuda.Stream(self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
             g = torch.cuda.CUDAGraph()
+            s1 = torch.cuda.Stream(self.dev)
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s):
                     for d in direct:
                         self._in = d
-                        self._part1(self.B, denom)
-                        self._part2()
+                        self._one_process_step(denom, s, s1)
             torch.cuda.current_stream(self.dev).wait_stream(s)
             hit = ((g, None, None, None, None), direct)
         self._many_sets[key] = hit
