@@ -237,6 +237,9 @@ class FusedTrainStep:
         # each state's step counter is bumped once per step, so both hold the same step and bias corrections.  The
         # one-stream step (default on one process) runs one launch over every tensor on `state`
         self.state_b = torch.zeros_like(self.state)
+        # one process: the categorical tables' Adam runs on the scatter's side stream right behind it (its own
+        # counter, state_t), beside the weight-gradient GEMM; everything else on `state` after the GEMM
+        self.state_t = torch.zeros_like(self.state)
         views = {}
         adam = (_lib.dfwfm_adam_tensor * len(params))()
         for i, p in enumerate(params):
@@ -249,6 +252,12 @@ class FusedTrainStep:
         self.n_main = sum(1 for p in params if id(p) not in mlp_ids)  # params are ordered with the MLP last
         self.adam_mlp = ctypes.cast(ctypes.addressof(adam) + self.n_main * ctypes.sizeof(_lib.dfwfm_adam_tensor),
                                     ctypes.POINTER(_lib.dfwfm_adam_tensor))
+        self.n_cat = sum(1 for p in params if id(p) in cat_ids)  # params are ordered with the tables first
+        self.adam_rest = ctypes.cast(ctypes.addressof(adam) + self.n_cat * ctypes.sizeof(_lib.dfwfm_adam_tensor),
+                                     ctypes.POINTER(_lib.dfwfm_adam_tensor))
+        # one process: Adam as two launches, the categorical tables (state_t) and the rest (state), on every path
+        # (eager, graph, step_many), so the two counters always hold the same step
+        self.split_adam = dist is None and 0 < self.n_cat < len(params)
         ptr = lambda t: None if t is None else views[id(t)].data_ptr()  # noqa: E731
         # sparse exchange: the backward scatters the categorical tables' gradients into a rank-local buffer (same
         # offsets as in self.grad, whose categorical region the lists fill); dfwfm_sparse_grads_local turns its
@@ -417,9 +426,20 @@ class FusedTrainStep:
         s1.wait_stream(s)
         with torch.cuda.stream(s1):
             self._backward_phase(_lib.BWD_SCATTER)
+            if self.split_adam:  # the tables' Adam right behind their scatter, beside the GEMM
+                self._adam_range(self.adam, self.n_cat, self.state_t)
         self._backward_phase(_lib.BWD_REDUCE | _lib.BWD_MLP_WEIGHTS)
+        if self.split_adam:
+            self._adam_range(self.adam_rest, self.n_adam - self.n_cat, self.state)
+        else:
+            self._part2()
         s.wait_stream(s1)
-        self._part2()
+
+    def _adam_range(self, tensors, n, state):
+        b1, b2 = self.betas
+        _lib.check(self.L.dfwfm_adam_step_dev(tensors, n, self.lr, b1, b2, self.eps, self.wd,
+                                              ctypes.c_void_p(state.data_ptr()), self._stream()),
+                   "dfwfm_adam_step_dev")
 
     def _bucketed(self):
         return self.dist is not None and self.n_bucket_a < self.grad.numel()
@@ -439,6 +459,10 @@ class FusedTrainStep:
                        "dfwfm_adam_step_dev")
 
     def _part2(self):
+        if self.split_adam:  # the tables (state_t) then the rest (state): both counters bumped every step
+            self._adam_range(self.adam, self.n_cat, self.state_t)
+            self._adam_range(self.adam_rest, self.n_adam - self.n_cat, self.state)
+            return
         if self.dist is None:
             self._adam_all()  # one counter (`state`) for every step of this instance, graph-replayed or not
             return
@@ -532,11 +556,13 @@ class FusedTrainStep:
         ga = None
         if self.dist is None and self.n_adam > self.n_main:
             # one process, one graph: fill, re-pack, forward, loss gradient and per-tile backward; then the table
-            # scatter on a side stream beside the reductions' final sums + weight-gradient GEMM (one launch); one Adam
-            # launch.  The scatter (latency-bound: one 512-thread workgroup per bucket, 60 KB of LDS) fits on the CUs
-            # beside the GEMM's 225 register-heavy four-wave workgroups: 0.2722 -> 0.2665 ms per step
-            # (profiles/r06/r06_fork.log).  (Round 4's forks -- the GEMM and the MLP's Adam beside the reductions /
-            # atomic scatter / main Adam -- measured level: what ran beside the GEMM was starved of CU slots.)
+            # scatter and the tables' Adam on a side stream beside the reductions' final sums + weight-gradient GEMM
+            # (one launch) and the other tensors' Adam.  The scatter (latency-bound: one 512-thread workgroup per
+            # bucket, 60 KB of LDS) fits on the CUs beside the GEMM's 225 register-heavy four-wave workgroups, and the
+            # tables' HBM-bound Adam streams beside its MFMAs: 0.2722 -> 0.2665 ms per step with the scatter alone
+            # there (profiles/r06/r06_fork.log), -8 us more with the tables' Adam (r06_splitadam.log).  (Round 4's
+            # forks -- the GEMM and the MLP's Adam beside the reductions / atomic scatter / main Adam -- measured
+            # level: what ran beside the GEMM was starved of CU slots.)
             s1 = torch.cuda.Stream(self.dev)
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g1, stream=s):
