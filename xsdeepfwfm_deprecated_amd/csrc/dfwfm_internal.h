@@ -285,7 +285,7 @@ struct ScatterArgs {
 // every row's contributions in a fixed order, so the gradients are the same bits on every run.
 constexpr int kSortSeg = 4096;      // samples sorted per pass (larger batches: passes in sample order)
 constexpr int kSortCh = 16;         // sorted positions per chunk of the segmented sums
-constexpr int kSortThreads = 512;
+constexpr int kSortThreads = 1024;
 struct SortScatterTask {
   float* g2;            // second-order table grad (width D) or null
   float* g1;            // first-order table grad (width 1) or null

@@ -423,6 +423,8 @@ class FusedTrainStep:
         """One step on one process, captured on stream s: forward, loss gradient, per-tile backward; the table scatter
         on s1 beside the reductions' final sums + weight-gradient GEMM on s; Adam after both."""
         self._part1(self.B, denom, phases=_lib.BWD_TILES)
+        # (the scatter alone first, then the GEMM beside the tables' Adam: 0.2799-0.2818 ms against 0.2715-0.2720,
+        # profiles/r06/r06_layout.log -- the latency-bound scatter is best hidden under the GEMM)
         s1.wait_stream(s)
         with torch.cuda.stream(s1):
             self._backward_phase(_lib.BWD_SCATTER)
@@ -549,7 +551,8 @@ class FusedTrainStep:
 
     def _capture(self, denom):
         """Graphs: forward + backward (its MLP-weight part separately under DP, see _exchange), then Adam;
-        the RCCL all-reduces run between them."""
+        the RCCL all-reduces run between them.  Captures are thread-local: the process group's watchdog thread
+        queries its events while a step is being captured, which under the global mode invalidates the capture."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         g1, g1b, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -565,7 +568,7 @@ class FusedTrainStep:
             # level: what ran beside the GEMM was starved of CU slots.)
             s1 = torch.cuda.Stream(self.dev)
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g1, stream=s):
+                with torch.cuda.graph(g1, stream=s, capture_error_mode="thread_local"):
                     self._one_process_step(denom, s, s1)
             torch.cuda.current_stream(self.dev).wait_stream(s)
             return g1, None, None, None, None
@@ -577,7 +580,7 @@ class FusedTrainStep:
             s1 = torch.cuda.Stream(self.dev)
             lo, hi = (self.n_tables if self.sparse else 0), self.n_bucket_a
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g1, stream=s):
+                with torch.cuda.graph(g1, stream=s, capture_error_mode="thread_local"):
                     self._part1(self.B, denom)
                     bucketed = self._bucketed()
                     if bucketed:
@@ -602,28 +605,28 @@ class FusedTrainStep:
             torch.cuda.current_stream(self.dev).wait_stream(s)
             return g1, None, None, None, None
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g1, stream=s):
+            with torch.cuda.graph(g1, stream=s, capture_error_mode="thread_local"):
                 self._part1(self.B, denom)
             if self._bucketed():
-                with torch.cuda.graph(g1b, stream=s):
+                with torch.cuda.graph(g1b, stream=s, capture_error_mode="thread_local"):
                     self._part1b()
             else:
                 g1b = None
             if self.sparse:
                 ga = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga, stream=s):
+                with torch.cuda.graph(ga, stream=s, capture_error_mode="thread_local"):
                     self._apply_sparse()
             # bucketed: the MLP's Adam is its own graph, replayed on a side stream behind the weight-gradient
             # GEMM and the MLP bucket's all-reduce, while the main Adam runs behind the first bucket (_replay_dp)
             g2b = None
-            with torch.cuda.graph(g2, stream=s):
+            with torch.cuda.graph(g2, stream=s, capture_error_mode="thread_local"):
                 if g1b is not None:
                     self._adam_main()
                 else:
                     self._part2()
             if g1b is not None:
                 g2b = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2b, stream=s):
+                with torch.cuda.graph(g2b, stream=s, capture_error_mode="thread_local"):
                     self._adam_mlp()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         return g1, g1b, ga, g2, g2b
@@ -729,7 +732,7 @@ class FusedTrainStep:
             g = torch.cuda.CUDAGraph()
             s1 = torch.cuda.Stream(self.dev)
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     for d in direct:
                         self._in = d
                         self._one_process_step(denom, s, s1)
