@@ -1200,9 +1200,10 @@ static int backward_impl(dfwfm_model* m, const float* dlogit, const dfwfm_grads*
       }
       SortScatterTask& t = sa.t[sa.ntasks++];
       // row buckets, one workgroup each: tables of at most 64 rows one row per bucket (no sort; a few hundred samples
-      // each), larger ones eight buckets of ~B/8 samples (sorted in 45 LDS stages at B = 4096, not 4096 keys' 78)
+      // each), larger ones eight buckets of ~B/8 samples (~540 keys at B = 4096: one 55-stage network over 1024
+      // threads; 12 / 16 buckets measured slower, more workgroups than CUs)
       t.onerow = rows <= 64 ? 1 : 0;
-      t.nbuck = (int16_t)(rows <= 64 ? (rows > 0 ? rows : 1) : diag_opt("nbuck", 8));
+      t.nbuck = (int16_t)(rows <= 64 ? (rows > 0 ? rows : 1) : 8);
       t.block0 = sblocks;
       t.pad8 = 0;
       sblocks += t.nbuck;
