@@ -234,8 +234,8 @@ class FusedTrainStep:
         self.state = torch.zeros(_lib.ADAM_STATE_BYTES // 8, dtype=torch.int64, device=dev)
         # under data parallelism Adam runs as two launches -- everything but the MLP
         # (state), the MLP weights and biases (state_b) -- so that the first can overlap the weight-gradient GEMM;
-        # each state's step counter is bumped once per step, so both hold the same step and bias corrections.  The
-        # one-stream step (default on one process) runs one launch over every tensor on `state`
+        # each state's step counter is bumped once per step, so both hold the same step and bias corrections.  On one
+        # process the split is tables (state_t) / everything else (state) instead (split_adam, below)
         self.state_b = torch.zeros_like(self.state)
         # one process: the categorical tables' Adam runs on the scatter's side stream right behind it (its own
         # counter, state_t), beside the weight-gradient GEMM; everything else on `state` after the GEMM
@@ -472,7 +472,7 @@ class FusedTrainStep:
         self._adam_mlp()
 
     def _adam_all(self):
-        """Every tensor's Adam in one launch (one step counter, `state`): the one-stream step."""
+        """Every tensor's Adam in one launch (one step counter, `state`): one process without categorical tables."""
         b1, b2 = self.betas
         _lib.check(self.L.dfwfm_adam_step_dev(self.adam, self.n_adam, self.lr, b1, b2, self.eps, self.wd,
                                               ctypes.c_void_p(self.state.data_ptr()), self._stream()),
@@ -706,7 +706,7 @@ class FusedTrainStep:
         """Consecutive steps over a list of full, resident batches [(xi, xv, y), ...] (a loader's ring of device
         input buffers), captured as ONE graph of len(batches) steps: the same kernels and the same results as
         calling step() on each in turn (the dropout seed and Adam's step count come from the device counter every
-        step bumps), without the ~9 us of idle between two graph replays.  One process, one-stream step only;
+        step bumps), without the ~9 us of idle between two graph replays.  One process only;
         otherwise (data parallelism, the first step, a batch that is not full or not readable in
         place, or resident_inputs=False: each new set of input pointers would be a K-step capture) it runs step()
         per batch.  Returns the running loss sum like step()."""
