@@ -12,7 +12,7 @@ import csv, sys, statistics as st, collections
 d = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(f"gpurun_out/pmctr_{sys.argv[1]}/run_counter_collection.csv")):
     k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-    if any(x in k for x in ("dw_kernel", "bwd_kernel", "fwd_kernel", "scatter", "adam_dev")):
+    if any(x in k for x in ("dw_kernel", "dwr_", "dw_sum", "bwd_kernel", "fwd_kernel", "ftrain", "scatter", "adam_dev")):
         d[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, c in d.items():
     print(k[:40], {n: round(st.median(v)) for n, v in c.items()})
