@@ -401,6 +401,8 @@ struct DwArgs {
   // order by dw_sum_kernel; see dwr_block
   float* part;
   float* bpart;
+  int32_t xcd_gs;       // dwr_reduce_kernel: blocks per XCD-local group (0: blockIdx order), and the groups
+  int32_t xcd_groups;
 };
 
 // One tensor of a fused Adam step.

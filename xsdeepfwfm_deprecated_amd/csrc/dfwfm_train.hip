@@ -1606,10 +1606,21 @@ __global__ void __launch_bounds__(256) dw_sum_kernel(DwArgs a) {
 // (39) run there instead of in a launch of their own after it
 template <int kDwrP, int NW>
 __global__ void __launch_bounds__(64 * NW) dwr_reduce_kernel(DwArgs a, RedArgs r, int nblk, int dw_blocks) {
-  if ((int)blockIdx.x < dw_blocks)
-    dwr_block<kDwrP, NW>(a, blockIdx.x);
-  else
+  if ((int)blockIdx.x < dw_blocks) {
+    int li = blockIdx.x;
+    if (a.xcd_gs > 0) {
+      // XCD-local groups (workgroup p runs on XCD p % 8): the a.xcd_gs blocks that share one 80-column slice of G_l
+      // (same layer, split and output block; consecutive logical blocks) go to one XCD, so one of them fetches the
+      // slice and the others read it from that XCD's L2; physical slots past the last group exit
+      const int p = blockIdx.x, x = p & 7, s = p >> 3;
+      const int g = (s / a.xcd_gs) * 8 + x;
+      if (g >= a.xcd_groups) return;
+      li = g * a.xcd_gs + s % a.xcd_gs;
+    }
+    dwr_block<kDwrP, NW>(a, li);
+  } else {
     reduce_final_block(r, nblk, (int)blockIdx.x - dw_blocks);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1894,10 +1905,21 @@ hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r,
   const int nblk = (int)((r.batch + kBM - 1) / kBM);
   const int P = red_outputs(r.F, r.D, r.N, r.num);
   const int rblocks = (P + 63) / 64;
-  hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(total_blocks + rblocks), dim3(256), 0, s, a, r, nblk,
-                     total_blocks);
+  // XCD-local block groups when every layer has the same number of 80-wide K blocks (DFWFM_DIAG dwr_xcd=0: off)
+  DwArgs b = a;
+  b.xcd_gs = 0;
+  b.xcd_groups = 0;
+  int phys = total_blocks;
+  bool uniform = a.H >= 1;
+  for (int l = 2; l <= a.H; ++l) uniform = uniform && a.nkb[l] == a.nkb[1];
+  if (uniform && diag_opt("dwr_xcd", 1) && total_blocks % a.nkb[1] == 0) {
+    b.xcd_gs = a.nkb[1];
+    b.xcd_groups = total_blocks / a.nkb[1];
+    phys = 8 * ((b.xcd_groups + 7) / 8) * b.xcd_gs;
+  }
+  hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(phys + rblocks), dim3(256), 0, s, b, r, nblk, phys);
   hipError_t e = hipGetLastError();
-  return e != hipSuccess ? e : launch_dw_sum(a, s);
+  return e != hipSuccess ? e : launch_dw_sum(b, s);
 }
 
 hipError_t launch_adam(const AdamList& list, int total_blocks, float step_size, float omb1, float b2, float omb2,
