@@ -1609,13 +1609,19 @@ __global__ void __launch_bounds__(64 * NW) dwr_reduce_kernel(DwArgs a, RedArgs r
   if ((int)blockIdx.x < dw_blocks) {
     int li = blockIdx.x;
     if (a.xcd_gs > 0) {
-      // XCD-local groups (workgroup p runs on XCD p % 8): the a.xcd_gs blocks that share one 80-column slice of G_l
-      // (same layer, split and output block; consecutive logical blocks) go to one XCD, so one of them fetches the
-      // slice and the others read it from that XCD's L2; physical slots past the last group exit
+      // XCD-local groups (workgroup p runs on XCD p % 8): a group of a.xcd_gs consecutive logical blocks that share
+      // operand slices goes to one XCD, so one block fetches a slice and the others read it from that XCD's L2.
+      // Whole rounds of eight groups first (XCD x takes groups x, x + 8, ...), then the leftover groups' blocks
+      // round-robin over the XCDs; physical slots past the last block exit
       const int p = blockIdx.x, x = p & 7, s = p >> 3;
-      const int g = (s / a.xcd_gs) * 8 + x;
-      if (g >= a.xcd_groups) return;
-      li = g * a.xcd_gs + s % a.xcd_gs;
+      const int full = a.xcd_groups / 8 * 8, head = full / 8 * a.xcd_gs;
+      if (s < head) {
+        li = ((s / a.xcd_gs) * 8 + x) * a.xcd_gs + s % a.xcd_gs;
+      } else {
+        const int e = (s - head) * 8 + x;
+        if (e >= (a.xcd_groups - full) * a.xcd_gs) return;
+        li = full * a.xcd_gs + e;
+      }
     }
     dwr_block<kDwrP, NW>(a, li);
   } else {
@@ -1912,10 +1918,15 @@ hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r,
   int phys = total_blocks;
   bool uniform = a.H >= 1;
   for (int l = 2; l <= a.H; ++l) uniform = uniform && a.nkb[l] == a.nkb[1];
-  if (uniform && diag_opt("dwr_xcd", 1) && total_blocks % a.nkb[1] == 0) {
-    b.xcd_gs = a.nkb[1];
-    b.xcd_groups = total_blocks / a.nkb[1];
-    phys = 8 * ((b.xcd_groups + 7) / 8) * b.xcd_gs;
+  const int mode = diag_opt("dwr_xcd", 2);
+  if (uniform && mode && total_blocks % a.nkb[1] == 0) {
+    // mode 2: a group is a whole (layer, split): its nnb x nkb blocks share every G_l and X_{l-1} slice (when the
+    // group fits an XCD's 32 CUs); mode 1: the nkb blocks of one output block (one G_l slice)
+    const int sg = a.nnb * a.nkb[1];
+    b.xcd_gs = (mode == 2 && sg <= 32) ? sg : a.nkb[1];
+    b.xcd_groups = total_blocks / b.xcd_gs;
+    const int full = b.xcd_groups / 8 * 8;
+    phys = 8 * (full / 8 * b.xcd_gs + ((b.xcd_groups - full) * b.xcd_gs + 7) / 8);
   }
   hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(phys + rblocks), dim3(256), 0, s, b, r, nblk, phys);
   hipError_t e = hipGetLastError();
