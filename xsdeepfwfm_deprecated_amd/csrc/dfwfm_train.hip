@@ -1542,9 +1542,23 @@ __device__ __forceinline__ void dwr_block(const DwArgs& a, int bid) {
   }
 }
 
+// XCD-local groups (workgroup p runs on XCD p % 8): a group of a.xcd_gs consecutive logical blocks that share operand
+// slices goes to one XCD, so one block fetches a slice and the others read it from that XCD's L2.  Whole rounds of
+// eight groups first (XCD x takes groups x, x + 8, ...), then the leftover groups' blocks round-robin over the XCDs;
+// -1 for the physical slots past the last block (those workgroups exit)
+__device__ __forceinline__ int dwr_logical(const DwArgs& a, int p) {
+  if (a.xcd_gs <= 0) return p;
+  const int x = p & 7, s = p >> 3;
+  const int full = a.xcd_groups / 8 * 8, head = full / 8 * a.xcd_gs;
+  if (s < head) return ((s / a.xcd_gs) * 8 + x) * a.xcd_gs + s % a.xcd_gs;
+  const int e = (s - head) * 8 + x;
+  return e < (a.xcd_groups - full) * a.xcd_gs ? full * a.xcd_gs + e : -1;
+}
+
 template <int kDwrP, int NW>
 __global__ void __launch_bounds__(64 * NW) dwr_kernel(DwArgs a) {
-  dwr_block<kDwrP, NW>(a, blockIdx.x);
+  const int li = dwr_logical(a, blockIdx.x);
+  if (li >= 0) dwr_block<kDwrP, NW>(a, li);
 }
 
 // the split slices of every weight / bias gradient element added in split order (the GEMM's second launch when it
@@ -1607,23 +1621,8 @@ __global__ void __launch_bounds__(256) dw_sum_kernel(DwArgs a) {
 template <int kDwrP, int NW>
 __global__ void __launch_bounds__(64 * NW) dwr_reduce_kernel(DwArgs a, RedArgs r, int nblk, int dw_blocks) {
   if ((int)blockIdx.x < dw_blocks) {
-    int li = blockIdx.x;
-    if (a.xcd_gs > 0) {
-      // XCD-local groups (workgroup p runs on XCD p % 8): a group of a.xcd_gs consecutive logical blocks that share
-      // operand slices goes to one XCD, so one block fetches a slice and the others read it from that XCD's L2.
-      // Whole rounds of eight groups first (XCD x takes groups x, x + 8, ...), then the leftover groups' blocks
-      // round-robin over the XCDs; physical slots past the last block exit
-      const int p = blockIdx.x, x = p & 7, s = p >> 3;
-      const int full = a.xcd_groups / 8 * 8, head = full / 8 * a.xcd_gs;
-      if (s < head) {
-        li = ((s / a.xcd_gs) * 8 + x) * a.xcd_gs + s % a.xcd_gs;
-      } else {
-        const int e = (s - head) * 8 + x;
-        if (e >= (a.xcd_groups - full) * a.xcd_gs) return;
-        li = full * a.xcd_gs + e;
-      }
-    }
-    dwr_block<kDwrP, NW>(a, li);
+    const int li = dwr_logical(a, blockIdx.x);
+    if (li >= 0) dwr_block<kDwrP, NW>(a, li);
   } else {
     reduce_final_block(r, nblk, (int)blockIdx.x - dw_blocks);
   }
@@ -1880,6 +1879,24 @@ hipError_t launch_scatter(const ScatterArgs& a, int total_blocks, hipStream_t s)
   return hipGetLastError();
 }
 
+// the XCD-local grouping of the weight-gradient GEMM's blocks (dwr_logical) and the physical grid it needs: each
+// (layer, split)'s nnb x nkb blocks share every G_l and X_{l-1} slice and fit one XCD's 32 CUs (DFWFM_DIAG dwr_xcd=1:
+// the nkb blocks of one G_l slice per group, 0: blockIdx order)
+static int dwr_xcd_plan(const DwArgs& a, int total_blocks, DwArgs& b) {
+  b = a;
+  b.xcd_gs = 0;
+  b.xcd_groups = 0;
+  bool uniform = a.H >= 1;
+  for (int l = 2; l <= a.H; ++l) uniform = uniform && a.nkb[l] == a.nkb[1];
+  const int mode = diag_opt("dwr_xcd", 2);
+  if (!uniform || !mode || total_blocks % a.nkb[1] != 0) return total_blocks;
+  const int sg = a.nnb * a.nkb[1];
+  b.xcd_gs = (mode == 2 && sg <= 32) ? sg : a.nkb[1];
+  b.xcd_groups = total_blocks / b.xcd_gs;
+  const int full = b.xcd_groups / 8 * 8;
+  return 8 * (full / 8 * b.xcd_gs + ((b.xcd_groups - full) * b.xcd_gs + 7) / 8);
+}
+
 static hipError_t launch_dw_sum(const DwArgs& a, hipStream_t s) {
   if (a.splits <= 1 || !a.part) return hipSuccess;
   const int blocks = a.blk0[a.H + 1] / a.splits;  // unsplit 80 x 80 blocks over every layer
@@ -1896,9 +1913,11 @@ hipError_t launch_dw(const DwArgs& a, int total_blocks, hipStream_t s) {
     const int64_t w = a.ldx[l] > a.N ? a.ldx[l] : a.N;
     if (q * w * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(total_blocks), dim3(256), 0, s, a);
+  DwArgs b;
+  const int phys = dwr_xcd_plan(a, total_blocks, b);
+  hipLaunchKernelGGL((dwr_kernel<4, 4>), dim3(phys), dim3(256), 0, s, b);
   hipError_t e = hipGetLastError();
-  return e != hipSuccess ? e : launch_dw_sum(a, s);
+  return e != hipSuccess ? e : launch_dw_sum(b, s);
 }
 
 hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r, hipStream_t s) {
@@ -1911,23 +1930,8 @@ hipError_t launch_dw_reduce(const DwArgs& a, int total_blocks, const RedArgs& r,
   const int nblk = (int)((r.batch + kBM - 1) / kBM);
   const int P = red_outputs(r.F, r.D, r.N, r.num);
   const int rblocks = (P + 63) / 64;
-  // XCD-local block groups when every layer has the same number of 80-wide K blocks (DFWFM_DIAG dwr_xcd=0: off)
-  DwArgs b = a;
-  b.xcd_gs = 0;
-  b.xcd_groups = 0;
-  int phys = total_blocks;
-  bool uniform = a.H >= 1;
-  for (int l = 2; l <= a.H; ++l) uniform = uniform && a.nkb[l] == a.nkb[1];
-  const int mode = diag_opt("dwr_xcd", 2);
-  if (uniform && mode && total_blocks % a.nkb[1] == 0) {
-    // mode 2: a group is a whole (layer, split): its nnb x nkb blocks share every G_l and X_{l-1} slice (when the
-    // group fits an XCD's 32 CUs); mode 1: the nkb blocks of one output block (one G_l slice)
-    const int sg = a.nnb * a.nkb[1];
-    b.xcd_gs = (mode == 2 && sg <= 32) ? sg : a.nkb[1];
-    b.xcd_groups = total_blocks / b.xcd_gs;
-    const int full = b.xcd_groups / 8 * 8;
-    phys = 8 * (full / 8 * b.xcd_gs + ((b.xcd_groups - full) * b.xcd_gs + 7) / 8);
-  }
+  DwArgs b;
+  const int phys = dwr_xcd_plan(a, total_blocks, b);
   hipLaunchKernelGGL((dwr_reduce_kernel<4, 4>), dim3(phys + rblocks), dim3(256), 0, s, b, r, nblk, phys);
   hipError_t e = hipGetLastError();
   return e != hipSuccess ? e : launch_dw_sum(b, s);
